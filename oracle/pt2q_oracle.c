@@ -1,0 +1,533 @@
+/*
+ * PT2Q CPU ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the checker for the MI355X hot path, never the product.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * It restates, in plain C, the per-layer PT2-LLM ternary PTQ loop of the reference:
+ *   - main.py:102-230   PT2LLMQuantizer.quantize_layer   (variant M, AGA on activations)
+ *   - gptq.py:59-199    GPTQ.add_batch / GPTQ.quantize    (variant G, AGA on the Hessian block)
+ *   - quantizer.py:32-293  AsymmetricTernaryQuantizer (init / grid / round / ITF / AGA)
+ *   - reorder.py:36-61,107-143  SSR similarity-to-mean and ordered top-k block pick
+ * under the PT2Q arithmetic contract: every floating-point reduction has one
+ * fixed order, every elementwise op is rounded separately (built with -ffp-contract=off),
+ * and every dot-product chain is a k-ascending fmaf chain (the bit-exact semantics of the
+ * gfx950 f32 MFMA, verified on hardware by tools/probe_numerics.hip).  The HIP kernels follow
+ * the same contract, so GPU == oracle bit-for-bit; the oracle itself is pinned against the
+ * reference's own outputs by the golden fixtures in tests/golden/ (gen_golden.py).
+ *
+ * Parallelised with OpenMP over independent outputs only; each output's chain is computed by
+ * one thread in canonical order, so results do not depend on the thread count.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_OK 0
+#define ORC_E_NOT_SPD 2
+#define ORC_E_ARG 3
+
+/* clamp(min=1e-8) with torch semantics: NaN propagates (quantizer.py:66,100,125,240). */
+static inline float clampmin(float x) { return (x < 1e-8f) ? 1e-8f : x; }
+
+/* ---------------------------------------------------------------- canonical reductions */
+
+/* Butterfly over L lanes with xor offsets L/2 .. 1 (== __shfl_xor tree on the GPU). */
+static float butterfly(float* p, int L) {
+  float q[64];
+  for (int off = L >> 1; off >= 1; off >>= 1) {
+    for (int l = 0; l < L; ++l) q[l] = p[l] + p[l ^ off];
+    memcpy(p, q, sizeof(float) * (size_t)L);
+  }
+  return p[0];
+}
+
+/* SUM16 over b entries with stride: lane l = k mod 16 accumulates k ascending, then butterfly. */
+static float sum16(const float* v, int b, long stride) {
+  float p[16] = {0};
+  for (int k = 0; k < b; ++k) p[k & 15] = p[k & 15] + v[(long)k * stride];
+  return butterfly(p, 16);
+}
+static float dot16(const float* a, long sa, const float* c, int b) {
+  float p[16] = {0};
+  for (int k = 0; k < b; ++k) p[k & 15] = fmaf(a[(long)k * sa], c[k], p[k & 15]);
+  return butterfly(p, 16);
+}
+
+/* SUMN over a logical vector of length n: lane t = (i>>2)&63 accumulates i ascending
+ * (the float4-per-lane pattern {256u + 4t + q}), then butterfly over 64 lanes. */
+static float sumn(const float* v, long n, long stride) {
+  float p[64] = {0};
+  for (long i = 0; i < n; ++i) p[(i >> 2) & 63] = p[(i >> 2) & 63] + v[i * stride];
+  return butterfly(p, 64);
+}
+static float sumsqn(const float* v, long n) {
+  float p[64] = {0};
+  for (long i = 0; i < n; ++i) p[(i >> 2) & 63] = fmaf(v[i], v[i], p[(i >> 2) & 63]);
+  return butterfly(p, 64);
+}
+
+/* ---------------------------------------------------------------- ATQ (quantizer.py) */
+
+/* ternary_init quantizer.py:32-69 on W (n x b, row stride ldw). T as float. */
+void orc_ternary_init(const float* W, long ldw, int n, int b, float* alpha, float* mu,
+                      float* T, long ldt) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    const float* w = W + (long)i * ldw;
+    float wc[4096 * 4];
+    float* wcp = (b <= 16384) ? wc : (float*)malloc(sizeof(float) * (size_t)b);
+    float m = sum16(w, b, 1) / (float)b;
+    for (int k = 0; k < b; ++k) wcp[k] = w[k] - m;
+    float absv[16] = {0};
+    for (int k = 0; k < b; ++k) absv[k & 15] = absv[k & 15] + fabsf(wcp[k]);
+    float delta = 0.75f * (butterfly(absv, 16) / (float)b);
+    float pn[16] = {0}, pd[16] = {0};
+    for (int k = 0; k < b; ++k) {
+      float t = (wcp[k] > delta) ? 1.0f : ((wcp[k] < -delta) ? -1.0f : 0.0f);
+      T[(long)i * ldt + k] = t;
+      pn[k & 15] = pn[k & 15] + t * wcp[k];
+      pd[k & 15] = pd[k & 15] + fabsf(t);
+    }
+    float num = butterfly(pn, 16), den = clampmin(butterfly(pd, 16));
+    alpha[i] = num / den;
+    mu[i] = m;
+    if (wcp != wc) free(wcp);
+  }
+}
+
+/* build_optimal_grid quantizer.py:71-108 for one row. */
+static void grid_row(const float* w, const float* t, int b, float wsum, float* a, float* m) {
+  float pwt[16] = {0}, pt[16] = {0}, pt2[16] = {0};
+  for (int k = 0; k < b; ++k) {
+    pwt[k & 15] = pwt[k & 15] + w[k] * t[k];
+    pt[k & 15] = pt[k & 15] + t[k];
+    pt2[k & 15] = pt2[k & 15] + t[k] * t[k];
+  }
+  float swt = butterfly(pwt, 16), ts = butterfly(pt, 16), t2 = butterfly(pt2, 16);
+  float fb = (float)b;
+  float den = clampmin(fb * t2 - ts * ts);
+  *a = (fb * swt - ts * wsum) / den;
+  *m = (t2 * wsum - ts * swt) / den;
+}
+
+/* flexible_round quantizer.py:110-134 for one row. Returns 1 if any code changed. */
+static int round_row(const float* w, int b, float a, float m, float* t) {
+  float as = clampmin(a);
+  int changed = 0;
+  for (int k = 0; k < b; ++k) {
+    float z = (w[k] - m) / as;
+    float nt = (z > 0.5f) ? 1.0f : ((z < -0.5f) ? -1.0f : 0.0f);
+    if (nt != t[k]) changed = 1;
+    t[k] = nt;
+  }
+  return changed;
+}
+
+void orc_build_optimal_grid(const float* W, long ldw, const float* T, long ldt, int n, int b,
+                            float* alpha, float* mu) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    const float* w = W + (long)i * ldw;
+    grid_row(w, T + (long)i * ldt, b, sum16(w, b, 1), &alpha[i], &mu[i]);
+  }
+}
+
+void orc_flexible_round(const float* W, long ldw, const float* alpha, const float* mu, int n,
+                        int b, float* T, long ldt) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    float* t = T + (long)i * ldt;
+    for (int k = 0; k < b; ++k) t[k] = 0.0f;
+    round_row(W + (long)i * ldw, b, alpha[i], mu[i], t);
+  }
+}
+
+/* iterative_ternary_fitting quantizer.py:136-175, literal BLOCK-level loop: T_prev starts at
+ * zero and the loop stops when torch.equal(T, T_prev) holds for the whole block.
+ * alpha/mu/T are in-out (init values in). iters_out = number of grid+round applications. */
+int orc_itf(const float* W, long ldw, int n, int b, int max_iter, float* alpha, float* mu,
+            float* T, long ldt) {
+  float* prev = (float*)calloc((size_t)n * (size_t)b, sizeof(float));
+  float* wsum = (float*)malloc(sizeof(float) * (size_t)n);
+  for (int i = 0; i < n; ++i) wsum[i] = sum16(W + (long)i * ldw, b, 1);
+  int it;
+  for (it = 0; it < max_iter; ++it) {
+    int equal = 1;
+    for (int i = 0; i < n && equal; ++i)
+      for (int k = 0; k < b; ++k)
+        if (T[(long)i * ldt + k] != prev[(long)i * b + k]) { equal = 0; break; }
+    if (equal) break;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      float* t = T + (long)i * ldt;
+      memcpy(prev + (long)i * b, t, sizeof(float) * (size_t)b);
+      grid_row(W + (long)i * ldw, t, b, wsum[i], &alpha[i], &mu[i]);
+      round_row(W + (long)i * ldw, b, alpha[i], mu[i], t);
+    }
+  }
+  free(prev);
+  free(wsum);
+  return it;
+}
+
+/* activation_aware_grid_alignment quantizer.py:177-248 given S1 = S·1 and d = 1ᵀS1. */
+void orc_aga(const float* W, long ldw, const float* T, long ldt, int n, int b, const float* S1,
+             float d, float* alpha, float* mu) {
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    const float* w = W + (long)i * ldw;
+    const float* t = T + (long)i * ldt;
+    float pv[16] = {0}, pws[16] = {0}, pwts[16] = {0}, pt2s[16] = {0};
+    for (int k = 0; k < b; ++k) {
+      int l = k & 15;
+      pv[l] = fmaf(t[k], S1[k], pv[l]);
+      pws[l] = fmaf(w[k], S1[k], pws[l]);
+      pwts[l] = fmaf(w[k] * t[k], S1[k], pwts[l]);
+      pt2s[l] = fmaf(t[k] * t[k], S1[k], pt2s[l]);
+    }
+    float v = butterfly(pv, 16), ws1 = butterfly(pws, 16), wts1 = butterfly(pwts, 16),
+          t2s1 = butterfly(pt2s, 16);
+    float v2 = v * v;
+    float den = clampmin(d * t2s1 - v2);
+    alpha[i] = (d * wts1 - v * ws1) / den;
+    mu[i] = (t2s1 * ws1 - v * wts1) / den;
+  }
+}
+
+/* S = XᵀX (k-ascending fmaf chain, quantizer.py:207), S1 = S·1 (l ascending), d = 1ᵀS1. */
+void orc_s1_from_x(const float* X, long ldx, long N, int b, float* S1, float* d) {
+#pragma omp parallel for schedule(static)
+  for (int j = 0; j < b; ++j) {
+    float s = 0.0f;
+    for (int l = 0; l < b; ++l) {
+      float acc = 0.0f;
+      for (long k = 0; k < N; ++k) acc = fmaf(X[k * ldx + j], X[k * ldx + l], acc);
+      s = s + acc;
+    }
+    S1[j] = s;
+  }
+  float dd = 0.0f;
+  for (int j = 0; j < b; ++j) dd = dd + S1[j];
+  *d = dd;
+}
+
+/* S1/d from a symmetric matrix sub-block M[idx][idx] (variant M: raw Gram G, so S = X_bᵀX_b). */
+static void s1_from_gram(const float* G, long ldg, const int64_t* idx, int b, float* S1,
+                         float* d) {
+  for (int j = 0; j < b; ++j) {
+    float s = 0.0f;
+    for (int l = 0; l < b; ++l) s = s + G[idx[j] * ldg + idx[l]];
+    S1[j] = s;
+  }
+  float dd = 0.0f;
+  for (int j = 0; j < b; ++j) dd = dd + S1[j];
+  *d = dd;
+}
+
+/* Variant G (gptq.py:147-150): X_block = H[blk][:,blk], S = X_blockᵀ X_block. */
+static void s1_from_hess_block(const float* H, long ldh, const int64_t* idx, int b, float* S1,
+                               float* d) {
+  float* hb = (float*)malloc(sizeof(float) * (size_t)b * (size_t)b);
+  for (int t = 0; t < b; ++t)
+    for (int j = 0; j < b; ++j) hb[(long)t * b + j] = H[idx[t] * ldh + idx[j]];
+  orc_s1_from_x(hb, b, b, b, S1, d);
+  free(hb);
+}
+
+/* Full ATQ on a block (quantizer.py:250-277): init -> ITF -> AGA (if aga). */
+int orc_atq_quantize(const float* W, long ldw, int n, int b, int aga, const float* S1, float d,
+                     int max_iter, float* alpha, float* mu, float* T, long ldt) {
+  orc_ternary_init(W, ldw, n, b, alpha, mu, T, ldt);
+  int it = orc_itf(W, ldw, n, b, max_iter, alpha, mu, T, ldt);
+  if (aga) orc_aga(W, ldw, T, ldt, n, b, S1, d, alpha, mu);
+  return it;
+}
+
+/* ---------------------------------------------------------------- SSR (reorder.py) */
+
+/* compute_column_similarity_to_mean reorder.py:36-61 on Wt (feature-major, m x ldw).
+ * wbar = chunked sum (chunks of 128 rem entries, each k-ascending; chunks summed ascending)
+ * / r; nw = sqrt(SUMN fma w²); wn = wbar / clamp(nw); per column: nj = sqrt(SUMN fma x²),
+ * s = SUMN fma (x / clamp(nj)) * wn. */
+void orc_ssr_similarity(const float* Wt, long ldw, int n, const int64_t* rem, int r,
+                        float* sim) {
+  float* tot = (float*)calloc((size_t)n, sizeof(float));
+  float* wn = (float*)malloc(sizeof(float) * (size_t)n);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    float t = 0.0f;
+    for (int c0 = 0; c0 < r; c0 += 128) {
+      float p = 0.0f;
+      int c1 = (c0 + 128 < r) ? c0 + 128 : r;
+      for (int e = c0; e < c1; ++e) p = p + Wt[rem[e] * ldw + i];
+      t = t + p;
+    }
+    tot[i] = t / (float)r;
+  }
+  float nw = clampmin(sqrtf(sumsqn(tot, n)));
+  for (int i = 0; i < n; ++i) wn[i] = tot[i] / nw;
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < r; ++e) {
+    const float* x = Wt + rem[e] * ldw;
+    float nj = clampmin(sqrtf(sumsqn(x, n)));
+    float p[64] = {0};
+    for (long i = 0; i < n; ++i) p[(i >> 2) & 63] = fmaf(x[i] / nj, wn[i], p[(i >> 2) & 63]);
+    sim[e] = butterfly(p, 64);
+  }
+  free(tot);
+  free(wn);
+}
+
+typedef struct { float v; int64_t e; } KeyIdx;
+static int cmp_desc(const void* a, const void* b) {
+  const KeyIdx* x = (const KeyIdx*)a;
+  const KeyIdx* y = (const KeyIdx*)b;
+  if (x->v > y->v) return -1;
+  if (x->v < y->v) return 1;
+  return (x->e < y->e) ? -1 : (x->e > y->e);
+}
+
+/* select_next_block_ssr reorder.py:107-143. Ties: (value desc, position asc).
+ * blk gets min(b, r) entries; newrem gets the rest in ascending (original) order. */
+int orc_ssr_select(const float* Wt, long ldw, int n, const int64_t* rem, int r, int b,
+                   int64_t* blk, int64_t* newrem, float* sim_out) {
+  if (r <= b) {
+    for (int e = 0; e < r; ++e) blk[e] = rem[e];
+    return r;
+  }
+  float* sim = (float*)malloc(sizeof(float) * (size_t)r);
+  orc_ssr_similarity(Wt, ldw, n, rem, r, sim);
+  KeyIdx* ki = (KeyIdx*)malloc(sizeof(KeyIdx) * (size_t)r);
+  for (int e = 0; e < r; ++e) { ki[e].v = sim[e]; ki[e].e = e; }
+  qsort(ki, (size_t)r, sizeof(KeyIdx), cmp_desc);
+  char* sel = (char*)calloc((size_t)r, 1);
+  for (int t = 0; t < b; ++t) { blk[t] = rem[ki[t].e]; sel[ki[t].e] = 1; }
+  int q = 0;
+  for (int e = 0; e < r; ++e) if (!sel[e]) newrem[q++] = rem[e];
+  if (sim_out) memcpy(sim_out, sim, sizeof(float) * (size_t)r);
+  free(sim); free(ki); free(sel);
+  return b;
+}
+
+/* ---------------------------------------------------------------- Hessian (gptq.py / main.py) */
+
+/* G = XᵀX, X is N x m (row stride ldx); G[i][j] = k-ascending fmaf chain from 0 (main.py:128,
+ * gptq.py:75).  Symmetric by construction (fma is commutative in its product). */
+void orc_gram(const float* X, long ldx, long N, int m, float* G, long ldg) {
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int i = 0; i < m; ++i) {
+    float* acc = G + (long)i * ldg;
+    for (int j = 0; j < m; ++j) acc[j] = 0.0f;
+    for (long k = 0; k < N; ++k) {
+      float xi = X[k * ldx + i];
+      const float* xr = X + k * ldx;
+      for (int j = 0; j < m; ++j) acc[j] = fmaf(xi, xr[j], acc[j]);
+    }
+  }
+}
+
+/* GPTQ.add_batch gptq.py:59-76: H = H + (inpᵀ inp) (product rounded, then one add). */
+void orc_gram_accumulate(const float* X, long ldx, long N, int m, float* H, long ldh) {
+  float* P = (float*)malloc(sizeof(float) * (size_t)m * (size_t)m);
+  orc_gram(X, ldx, N, m, P, m);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) H[(long)i * ldh + j] = H[(long)i * ldh + j] + P[(long)i * m + j];
+  free(P);
+}
+
+/* main.py:128-133 / gptq.py:94-98: H = G / nsamples; damp = percdamp * mean(diag H);
+ * H_ii += damp.  mean = SUMN(diag) / m (torch mean = sum / count). Returns damp. */
+float orc_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
+                          float* H, long ldh) {
+  float fn = (float)nsamples;
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < m; ++j) H[(long)i * ldh + j] = G[(long)i * ldg + j] / fn;
+  float dsum = sumn(H, m, ldh + 1);
+  float damp = percdamp * (dsum / (float)m);
+  for (int i = 0; i < m; ++i) H[(long)i * ldh + i] = H[(long)i * ldh + i] + damp;
+  return damp;
+}
+
+/* Canonical Cholesky H = UᵀU (upper U, row-major): for k <= i,
+ *   acc = H[k][i]; for j < k ascending: acc = fmaf(-U[j][k], U[j][i], acc);
+ *   U[k][k] = sqrt(acc) (fail if !(acc > 0)); U[k][i] = acc / U[k][k].
+ * Returns 0 or k+1 of the first failing pivot (LAPACK spotrf convention). */
+int orc_cholesky_upper(const float* H, long ldh, int m, float* U, long ldu) {
+  for (int k = 0; k < m; ++k)
+    for (int i = 0; i < m; ++i) U[(long)k * ldu + i] = (i >= k) ? H[(long)k * ldh + i] : 0.0f;
+  /* right-looking: after row k is final, apply its rank-1 term to rows > k (j ascending). */
+  for (int k = 0; k < m; ++k) {
+    float* uk = U + (long)k * ldu;
+    float akk = uk[k];
+    if (!(akk > 0.0f)) return k + 1;
+    float dkk = sqrtf(akk);
+    uk[k] = dkk;
+    for (int i = k + 1; i < m; ++i) uk[i] = uk[i] / dkk;
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int r = k + 1; r < m; ++r) {
+      float nuk = -uk[r];
+      float* ur = U + (long)r * ldu;
+      for (int i = r; i < m; ++i) ur[i] = fmaf(nuk, uk[i], ur[i]);
+    }
+  }
+  return 0;
+}
+
+/* Canonical triangular inverse Uinv = U⁻¹ (upper): Uinv[k][k] = 1/U[k][k];
+ * for i > k: acc = j-ascending fmaf chain of Uinv[k][j]*U[j][i] over j in [k, i) from 0;
+ * Uinv[k][i] = -acc / U[i][i]. */
+void orc_trtri_upper(const float* U, long ldu, int m, float* Ui, long ldi) {
+#pragma omp parallel for schedule(dynamic, 8)
+  for (int k = 0; k < m; ++k) {
+    float* x = Ui + (long)k * ldi;
+    for (int i = 0; i < m; ++i) x[i] = 0.0f; /* acc then value */
+    for (int j = k; j < m; ++j) {
+      float xj = (j == k) ? 1.0f / U[(long)k * ldu + k] : -x[j] / U[(long)j * ldu + j];
+      x[j] = xj;
+      const float* uj = U + (long)j * ldu;
+      for (int i = j + 1; i < m; ++i) x[i] = fmaf(xj, uj[i], x[i]);
+    }
+  }
+}
+
+/* Hinv = Uinv·Uinvᵀ: Hinv[i][k] = j-ascending fmaf chain over j >= max(i,k) of
+ * Uinv[i][j]*Uinv[k][j], from 0; mirrored (cholesky_inverse main.py:139, gptq.py:103). */
+void orc_lauum_upper(const float* Ui, long ldi, int m, float* Hinv, long ldh) {
+#pragma omp parallel for schedule(dynamic, 8)
+  for (int i = 0; i < m; ++i) {
+    const float* ui = Ui + (long)i * ldi;
+    for (int k = i; k < m; ++k) {
+      const float* uk = Ui + (long)k * ldi;
+      float acc = 0.0f;
+      for (int j = k; j < m; ++j) acc = fmaf(ui[j], uk[j], acc);
+      Hinv[(long)i * ldh + k] = acc;
+      Hinv[(long)k * ldh + i] = acc;
+    }
+  }
+}
+
+int orc_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi) {
+  float* U = (float*)malloc(sizeof(float) * (size_t)m * (size_t)m);
+  float* Ui = (float*)malloc(sizeof(float) * (size_t)m * (size_t)m);
+  int info = orc_cholesky_upper(H, ldh, m, U, m);
+  if (info == 0) {
+    orc_trtri_upper(U, m, m, Ui, m);
+    orc_lauum_upper(Ui, m, m, Hinv, ldhi);
+  }
+  free(U);
+  free(Ui);
+  return info ? ORC_E_NOT_SPD : ORC_OK;
+}
+
+/* ---------------------------------------------------------------- block loop */
+
+/* ATQ on block blk of Wt (b columns), whole-block semantics of quantizer.py + the
+ * error-term E = Wb - (alpha*T + mu) (main.py:188-189). Outputs per row i:
+ * alpha[i], mu[i], T[k*ldtt + i] (int8 at Tt row blk[k]), E[k*n + i]. */
+static int atq_block_from_wt(const float* Wt, long ldw, int n, const int64_t* blk, int b,
+                             int aga, const float* S1, float d, int max_iter, float* alpha,
+                             float* mu, float* Tf, float* Wb) {
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < b; ++k) Wb[(long)i * b + k] = Wt[blk[k] * ldw + i];
+  return orc_atq_quantize(Wb, b, n, b, aga, S1, d, max_iter, alpha, mu, Tf, b);
+}
+
+/* Error feedback main.py:187-214 / gptq.py:158-186 for one block, given E (bs x n, block order):
+ * C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k]); Wt[rem_e][i] -= chain_k C[k][e]*E[k][i]. */
+void orc_error_feedback(float* Wt, long ldw, int n, const int64_t* blk, int bs,
+                        const int64_t* rem, int nr, const float* E, const float* Hinv, long ldh) {
+  float* C = (float*)malloc(sizeof(float) * (size_t)bs * (size_t)nr);
+  for (int k = 0; k < bs; ++k) {
+    float dg = clampmin(Hinv[blk[k] * ldh + blk[k]]);
+    for (int e = 0; e < nr; ++e) C[(long)k * nr + e] = Hinv[blk[k] * ldh + rem[e]] / dg;
+  }
+#pragma omp parallel for schedule(static)
+  for (int e = 0; e < nr; ++e) {
+    float* wr = Wt + rem[e] * ldw;
+    float acc[1024];
+    for (int i0 = 0; i0 < n; i0 += 1024) {
+      int i1 = (i0 + 1024 < n) ? i0 + 1024 : n;
+      for (int i = i0; i < i1; ++i) acc[i - i0] = 0.0f;
+      for (int k = 0; k < bs; ++k) {
+        float c = C[(long)k * nr + e];
+        const float* ek = E + (long)k * n;
+        for (int i = i0; i < i1; ++i) acc[i - i0] = fmaf(c, ek[i], acc[i - i0]);
+      }
+      for (int i = i0; i < i1; ++i) wr[i] = wr[i] - acc[i - i0];
+    }
+  }
+  free(C);
+}
+
+/* The per-layer block loop of main.py:158-215 (variant M) / gptq.py:124-187 (variant G).
+ * Wt: m x ldw feature-major working weights (modified in place by error feedback).
+ * aga_src: 0 none, 1 activations (A = raw Gram G = XᵀX), 2 Hessian block (A = damped H).
+ * Hinv: m x m.  Outputs: alpha_t/mu_t (B x n), Tt (m x ldw int8, original feature order),
+ * perm (m), iters (B). Returns number of blocks. */
+int orc_quantize_blocks(float* Wt, long ldw, int n, int m, int bsz, int use_ssr, int aga_src,
+                        const float* A, long lda, const float* Hinv, long ldh, int max_iter,
+                        float* alpha_t, float* mu_t, int8_t* Tt, int64_t* perm, int* iters) {
+  int64_t* rem = (int64_t*)malloc(sizeof(int64_t) * (size_t)m);
+  int64_t* newrem = (int64_t*)malloc(sizeof(int64_t) * (size_t)m);
+  int64_t* blk = (int64_t*)malloc(sizeof(int64_t) * (size_t)m);
+  float* Wb = (float*)malloc(sizeof(float) * (size_t)n * (size_t)(bsz < m ? bsz : m));
+  float* Tf = (float*)malloc(sizeof(float) * (size_t)n * (size_t)(bsz < m ? bsz : m));
+  float* E = (float*)malloc(sizeof(float) * (size_t)n * (size_t)(bsz < m ? bsz : m));
+  float* S1 = (float*)malloc(sizeof(float) * (size_t)m);
+  for (int e = 0; e < m; ++e) rem[e] = e;
+  int r = m, processed = 0, kb = 0;
+  while (processed < m) {
+    int bs, nr;
+    if (use_ssr) {
+      bs = orc_ssr_select(Wt, ldw, n, rem, r, bsz, blk, newrem, NULL);
+      nr = r - bs;
+    } else {
+      bs = (processed + bsz < m) ? bsz : m - processed;
+      for (int t = 0; t < bs; ++t) blk[t] = processed + t;
+      nr = m - processed - bs;
+      for (int e = 0; e < nr; ++e) newrem[e] = processed + bs + e;
+    }
+    float d = 0.0f;
+    if (aga_src == 1) s1_from_gram(A, lda, blk, bs, S1, &d);
+    else if (aga_src == 2) s1_from_hess_block(A, lda, blk, bs, S1, &d);
+    float* al = alpha_t + (long)kb * n;
+    float* mu = mu_t + (long)kb * n;
+    int it = atq_block_from_wt(Wt, ldw, n, blk, bs, aga_src != 0, S1, d, max_iter, al, mu, Tf, Wb);
+    if (iters) iters[kb] = it;
+    for (int k = 0; k < bs; ++k)
+      for (int i = 0; i < n; ++i) {
+        float t = Tf[(long)i * bs + k];
+        Tt[blk[k] * ldw + i] = (int8_t)t;
+        E[(long)k * n + i] = Wb[(long)i * bs + k] - (al[i] * t + mu[i]);
+      }
+    if (nr > 0) orc_error_feedback(Wt, ldw, n, blk, bs, newrem, nr, E, Hinv, ldh);
+    for (int t = 0; t < bs; ++t) perm[processed + t] = blk[t];
+    for (int e = 0; e < nr; ++e) rem[e] = newrem[e];
+    r = nr;
+    processed += bs;
+    ++kb;
+  }
+  free(rem); free(newrem); free(blk); free(Wb); free(Tf); free(E); free(S1);
+  return kb;
+}
+
+void orc_set_threads(int t) {
+#ifdef _OPENMP
+  if (t > 0) omp_set_num_threads(t);
+#else
+  (void)t;
+#endif
+}
+
+int orc_get_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

@@ -1,0 +1,52 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TESTS = os.path.join(ROOT, "tests")
+GOLDEN = os.path.join(TESTS, "golden")
+for p in (ROOT, TESTS):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: larger CPU case")
+
+
+def load_golden(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def golden_names(prefix):
+    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith(prefix) and f.endswith(".npz"))
+
+
+def layer_inputs(g):
+    """Regenerate (W, X) of a full-layer fixture from its seeds (tests/synth.py)."""
+    import synth
+    n, m, N = int(g["n"]), int(g["m"]), int(g["N"])
+    W = synth.weights(int(g["wseed"]), n, m)
+    X = synth.activations(int(g["xseed"]), N, m, outliers=bool(g.get("outliers", True)))
+    if "zero_col" in g:
+        X[:, int(g["zero_col"])] = 0.0
+    return W, X
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def pt2q():
+    """The product package (HIP path). Loaded by file path: the directory name is not an identifier."""
+    import pt2q_loader
+    return pt2q_loader.load()

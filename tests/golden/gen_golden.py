@@ -1,0 +1,265 @@
+"""Generate the golden parity fixtures from the REFERENCE implementation.
+
+Run here (the reference is importable only in the build container):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+It imports /root/reference (quantizer.py, reorder.py, gptq.py, main.py), runs them on CPU with
+torch.set_num_threads(1) (the pinned oracle configuration) on counter-generated
+inputs (tests/synth.py), and stores ONLY data: the seeds/shapes needed to regenerate the inputs
+and the reference's outputs.  No reference source is copied.  The test-suite checks the CPU
+oracle (oracle/) against these, and the HIP path against the oracle.
+
+The per-block "trace" fixtures drive the reference's own components in the order of
+main.py:158-215 and assert that the traced loop reproduces PT2LLMQuantizer.quantize_layer
+bit-for-bit before anything is saved.
+"""
+import contextlib
+import io
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))          # tests/ (synth)
+REF = "/root/reference"
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import synth  # noqa: E402
+
+torch.set_num_threads(1)
+import quantizer as rq  # noqa: E402
+import reorder as rr  # noqa: E402
+import gptq as rg  # noqa: E402
+import main as rm  # noqa: E402
+
+OUT = HERE
+
+
+def save(name, **kw):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **kw)
+    print(f"  {name}.npz {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+def linear(W):
+    lin = torch.nn.Linear(W.shape[1], W.shape[0], bias=False)
+    lin.weight.data = torch.from_numpy(W.copy())
+    return lin
+
+
+def ref_layer_m(W, X, use_ssr, bs=128, percdamp=0.01):
+    q = rm.PT2LLMQuantizer(model=None, tokenizer=None, device="cpu", block_size=bs,
+                           use_ssr=use_ssr, percdamp=percdamp)
+    with contextlib.redirect_stdout(io.StringIO()):
+        return q.quantize_layer(linear(W), "layer", torch.from_numpy(X.copy()))
+
+
+def ref_layer_g(W, X, use_ssr, bs=128, nbatch=2):
+    g = rg.GPTQ(linear(W), bs, 0.01)
+    for c in np.array_split(X, nbatch):
+        g.add_batch(torch.from_numpy(c.copy()))
+    a, mu, T, perm = g.quantize(use_ssr=use_ssr)
+    return dict(alpha=a, mu=mu, T=T, perm=perm)
+
+
+def gen_layers():
+    print("full-layer fixtures (variant M, main.py:102-230)")
+    cases = [
+        ("layer_m_c1_ssr", 512, 512, 128, True, 128, True),
+        ("layer_m_c1_nossr", 512, 512, 128, False, 128, True),
+        ("layer_m_1024x768_n2048", 1024, 768, 2048, True, 128, True),
+        ("layer_m_384x300_n200", 384, 300, 200, True, 128, True),
+        ("layer_m_perchannel_256x256", 256, 256, 512, True, 512, True),
+        ("layer_m_512x512_n2048_noout", 512, 512, 2048, True, 128, False),
+    ]
+    for name, n, m, N, ssr, bs, outl in cases:
+        ws, xs = 1 + n, 2 + m
+        W = synth.weights(ws, n, m)
+        X = synth.activations(xs, N, m, outliers=outl)
+        r = ref_layer_m(W, X, ssr, bs)
+        save(name, variant="M", n=n, m=m, N=N, wseed=ws, xseed=xs, outliers=outl, use_ssr=ssr,
+             block_size=bs, alpha=r["alpha"].numpy(), mu=r["mu"].numpy(),
+             T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
+    print("full-layer fixtures (variant G, gptq.py:59-199; no outlier channels: with x20 outliers the"
+          " H_bb² AGA is catastrophically ill-conditioned in the reference itself)")
+    gcases = [
+        ("layer_g_768x640_n1024_ssr", 768, 640, 1024, True),
+        ("layer_g_384x300_n200_ssr", 384, 300, 200, True),
+        ("layer_g_512x512_n1024_nossr", 512, 512, 1024, False),
+    ]
+    for name, n, m, N, ssr in gcases:
+        ws, xs = 3 + n, 4 + m
+        W = synth.weights(ws, n, m)
+        X = synth.activations(xs, N, m, outliers=False)
+        r = ref_layer_g(W, X, ssr)
+        save(name, variant="G", n=n, m=m, N=N, wseed=ws, xseed=xs, outliers=False, use_ssr=ssr,
+             block_size=128, nbatch=2, alpha=r["alpha"].numpy(), mu=r["mu"].numpy(),
+             T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
+    # not positive definite: zero input column + percdamp 0 -> cholesky fails -> pinv (main.py:140)
+    n, m, N = 128, 256, 64
+    W = synth.weights(77, n, m)
+    X = synth.activations(78, N, m)
+    X[:, 5] = 0.0
+    H = torch.from_numpy(X).T @ torch.from_numpy(X) / N
+    try:
+        torch.linalg.cholesky(H)
+        spd = True
+    except RuntimeError:
+        spd = False
+    assert not spd
+    r = ref_layer_m(W, X, True, 128, percdamp=0.0)
+    save("layer_m_notspd", variant="M", n=n, m=m, N=N, wseed=77, xseed=78, zero_col=5,
+         percdamp=0.0, use_ssr=True, block_size=128, alpha=r["alpha"].numpy(),
+         mu=r["mu"].numpy(), T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
+
+
+def gen_atq():
+    print("ATQ known answers (quantizer.py:32-293)")
+    atq = rq.AsymmetricTernaryQuantizer()
+    for seed in (0, 1):
+        W = torch.from_numpy(synth.weights(100 + seed, 4096, 128))
+        X = torch.from_numpy(synth.activations(200 + seed, 512, 128))
+        a0, m0, T0 = atq.ternary_init(W)
+        a1, m1, T1 = atq.iterative_ternary_fitting(W, a0, m0, T0)
+        a2, m2 = atq.activation_aware_grid_alignment(W, T1, X)
+        af, mf, Tf = atq.quantize(W, X)
+        an, mn, Tn = atq.quantize(W)
+        assert torch.equal(Tf, T1) and torch.equal(Tn, T1)
+        assert torch.equal(af, a2) and torch.equal(an, a1)
+        save(f"atq_4096x128_s{seed}", wseed=100 + seed, xseed=200 + seed, n=4096, b=128, N=512,
+             a_init=a0.numpy().ravel(), m_init=m0.numpy().ravel(), T_init=T0.numpy().astype(np.int8),
+             a_itf=a1.numpy().ravel(), m_itf=m1.numpy().ravel(), T_itf=T1.numpy().astype(np.int8),
+             a_aga=a2.numpy().ravel(), m_aga=m2.numpy().ravel())
+    # general block width (per-channel path): b = 1000 (not a multiple of 16)
+    W = torch.from_numpy(synth.weights(110, 256, 1000))
+    X = torch.from_numpy(synth.activations(210, 300, 1000))
+    af, mf, Tf = atq.quantize(W, X)
+    save("atq_256x1000", wseed=110, xseed=210, n=256, b=1000, N=300, alpha=af.numpy().ravel(),
+         mu=mf.numpy().ravel(), T=Tf.numpy().astype(np.int8))
+    # edge cases: zero block, constant rows, explicit negative alpha in flexible_round,
+    # build_optimal_grid on a given T
+    Z = torch.zeros(64, 128)
+    az, mz, Tz = atq.quantize(Z)
+    azx, mzx, Tzx = atq.quantize(Z, torch.from_numpy(synth.activations(220, 64, 128)))
+    Wc = torch.from_numpy(synth.weights(120, 64, 128))
+    Wc[::4] = Wc[::4, :1]                       # every 4th row constant
+    Wc[1] = 0.0                                 # one all-zero row
+    ac, mc, Tc = atq.quantize(Wc)
+    acx, mcx, Tcx = atq.quantize(Wc, torch.from_numpy(synth.activations(221, 64, 128)))
+    Wr = torch.from_numpy(synth.weights(130, 32, 128))
+    alpha_neg = torch.from_numpy(np.linspace(-0.02, 0.02, 32, dtype=np.float32))[:, None]
+    mu_r = torch.from_numpy(synth.weights(131, 32, 1))
+    Tr = atq.flexible_round(Wr, alpha_neg, mu_r)
+    Tg = torch.from_numpy((synth.centered24(132, 32 * 128).reshape(32, 128) % 3 - 1).astype(np.float32))
+    ag, mg = atq.build_optimal_grid(Wr, Tg)
+    save("atq_edges", zero_alpha=az.numpy().ravel(), zero_mu=mz.numpy().ravel(),
+         zero_T=Tz.numpy().astype(np.int8), zerox_alpha=azx.numpy().ravel(),
+         zerox_mu=mzx.numpy().ravel(), zerox_T=Tzx.numpy().astype(np.int8),
+         const_W=Wc.numpy(), const_alpha=ac.numpy().ravel(), const_mu=mc.numpy().ravel(),
+         const_T=Tc.numpy().astype(np.int8), constx_alpha=acx.numpy().ravel(),
+         constx_mu=mcx.numpy().ravel(), constx_T=Tcx.numpy().astype(np.int8),
+         round_alpha=alpha_neg.numpy().ravel(), round_mu=mu_r.numpy().ravel(),
+         round_T=Tr.numpy().astype(np.int8), grid_T=Tg.numpy().astype(np.int8),
+         grid_alpha=ag.numpy().ravel(), grid_mu=mg.numpy().ravel())
+
+
+def gen_ssr():
+    print("SSR known answers (reorder.py:36-61,107-143)")
+    W = torch.from_numpy(synth.weights(11, 4096, 4096))
+    rem = torch.arange(4096)
+    sim = rr.compute_column_similarity_to_mean(W, rem)
+    blk, newrem = rr.select_next_block_ssr(W, rem, 128)
+    save("ssr_4096x4096", wseed=11, n=4096, m=4096, sim=sim.numpy(), blk=blk.numpy(),
+         newrem=newrem.numpy())
+    W = torch.from_numpy(synth.weights(12, 1024, 1000))
+    keep = np.sort(np.argsort(synth.centered24(13, 1000))[:700]).astype(np.int64)
+    rem = torch.from_numpy(keep)
+    sim = rr.compute_column_similarity_to_mean(W, rem)
+    blk, newrem = rr.select_next_block_ssr(W, rem, 128)
+    save("ssr_1024x1000_subset", wseed=12, n=1024, m=1000, rem=keep, sim=sim.numpy(),
+         blk=blk.numpy(), newrem=newrem.numpy())
+
+
+def gen_hessian():
+    print("Hessian / inverse (main.py:127-141)")
+    for N in (512, 128):
+        m = 256
+        X = torch.from_numpy(synth.activations(300 + N, N, m))
+        H = X.T @ X
+        H = H / X.shape[0]
+        damp = 0.01 * torch.diag(H).mean()
+        H.diagonal().add_(damp)
+        Hinv = torch.cholesky_inverse(torch.linalg.cholesky(H.float()))
+        save(f"hess_256_n{N}", xseed=300 + N, N=N, m=m, H=H.numpy(), Hinv=Hinv.numpy(),
+             damp=np.float32(damp.item()))
+
+
+def gen_trace():
+    """Teacher-forced per-block trace of main.py:158-215 using the reference's own components."""
+    print("per-block trace (variant M, SSR on)")
+    n, m, N, bs = 512, 384, 1024, 128
+    W0 = synth.weights(401, n, m)
+    X0 = synth.activations(402, N, m)
+    W = torch.from_numpy(W0.copy())
+    X = torch.from_numpy(X0.copy())
+    H = X.T @ X
+    H = H / X.shape[0]
+    H.diagonal().add_(0.01 * torch.diag(H).mean())
+    H_inv = torch.cholesky_inverse(torch.linalg.cholesky(H.float()))
+    atq = rq.AsymmetricTernaryQuantizer()
+    rem = torch.arange(m)
+    rec = {}
+    k = 0
+    T_full = torch.zeros(n, m, dtype=torch.int8)
+    alphas, mus, perm = [], [], []
+    while len(rem) > 0:
+        if len(rem) > bs:
+            rec[f"sim{k}"] = rr.compute_column_similarity_to_mean(W, rem).numpy()
+        blk, rem = rr.select_next_block_ssr(W, rem, bs)
+        Wb = W[:, blk]
+        a, mu, Tb = atq.quantize(Wb, X[:, blk])
+        rec[f"blk{k}"] = blk.numpy()
+        rec[f"alpha{k}"] = a.numpy().ravel()
+        rec[f"mu{k}"] = mu.numpy().ravel()
+        rec[f"T{k}"] = Tb.numpy().astype(np.int8)
+        T_full[:, blk] = Tb.to(torch.int8)
+        alphas.append(a); mus.append(mu); perm += blk.tolist()
+        E = Wb - (a * Tb + mu)
+        if len(rem) > 0:
+            C = H_inv[blk][:, rem] / H_inv[blk, blk].unsqueeze(1).clamp(min=1e-8)
+            W[:, rem] -= E @ C
+        k += 1
+    ref = ref_layer_m(W0, X0, True, bs)
+    assert torch.equal(ref["T"], T_full) and ref["perm"].tolist() == perm
+    assert torch.equal(ref["alpha"], torch.cat(alphas, 1)) and torch.equal(ref["mu"], torch.cat(mus, 1))
+    save("trace_m_512x384_n1024", wseed=401, xseed=402, n=n, m=m, N=N, block_size=bs, nblocks=k,
+         Hinv=H_inv.numpy(), **rec)
+
+
+def gen_examples():
+    print("examples.py smoke values (examples.py:15-77)")
+    torch.manual_seed(42)
+    W = torch.randn(256, 512)
+    X = torch.randn(32, 512)
+    atq = rq.AsymmetricTernaryQuantizer(max_iter=100)
+    a0, m0, T0 = atq.ternary_init(W)
+    e0 = rq.compute_quantization_error(W, atq.dequantize(a0, m0, T0))
+    a1, m1, T1 = atq.iterative_ternary_fitting(W, a0, m0, T0)
+    e1 = rq.compute_quantization_error(W, atq.dequantize(a1, m1, T1))
+    a2, m2 = atq.activation_aware_grid_alignment(W, T1, X)
+    ox0 = rq.compute_output_error(W, atq.dequantize(a1, m1, T1), X)
+    ox1 = rq.compute_output_error(W, atq.dequantize(a2, m2, T1), X)
+    save("examples_atq", W=W.numpy(), X=X.numpy(), err_init=e0, err_itf=e1, out_err_itf=ox0,
+         out_err_aga=ox1, T_itf=T1.numpy().astype(np.int8))
+
+
+if __name__ == "__main__":
+    gen_layers()
+    gen_atq()
+    gen_ssr()
+    gen_hessian()
+    gen_trace()
+    gen_examples()
