@@ -1,0 +1,147 @@
+/*
+ * pt2q.h — C ABI of the MI355X ternary PTQ calibration engine (libpt2q.so).
+ *
+ * The reference (shuhan-wang1/SNLP---Tenary-Post-train-Quantization) is pure PyTorch and has no
+ * FFI; each entry point below replaces the reference operation cited next to it, and the
+ * Python package (snlp---tenary-post-train-quantization_amd/) binds them with ctypes behind the
+ * reference's own class surface.
+ *
+ * Conventions
+ *   - All tensor arguments are DEVICE pointers (HIP, gfx950) owned by the caller; nothing is
+ *     retained after return.  Scratch comes from a caller-supplied workspace.
+ *   - `stream` is a hipStream_t passed as void*; every call is stream-ordered and asynchronous
+ *     (no host synchronisation, no allocation), so a caller may capture it into a hipGraph.
+ *   - Matrices are row-major with explicit leading dimensions (in elements).
+ *   - Return value: PT2Q_OK or an error code; launch-time argument errors only.  Numerical
+ *     status discovered on the device (Cholesky breakdown) is written to `info_dev`.
+ *   - Arithmetic follows the PT2Q contract: results are bit-identical to the CPU
+ *     oracle (oracle/pt2q_oracle.c) for every input.
+ */
+#ifndef PT2Q_H
+#define PT2Q_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define PT2Q_OK 0
+#define PT2Q_E_ARG 1
+#define PT2Q_E_NOT_SPD 2 /* reported through info_dev; caller falls back to pinv (main.py:140) */
+#define PT2Q_E_UNSUPPORTED 3
+#define PT2Q_E_HIP 4
+#define PT2Q_E_WORKSPACE 5
+
+/* element types */
+#define PT2Q_F32 0
+#define PT2Q_F16 1
+#define PT2Q_BF16 2
+#define PT2Q_I8 3
+
+/* quantize flags */
+#define PT2Q_FLAG_SSR 0x1          /* SSR block selection (reorder.py:107) instead of sequential */
+#define PT2Q_AGA_NONE 0x0          /* ATQ without activations (quantizer.py:274 X is None) */
+#define PT2Q_AGA_ACT 0x10          /* variant M: S = X_bᵀX_b from the raw Gram (main.py:177) */
+#define PT2Q_AGA_HESS 0x20         /* variant G: S = H_bbᵀH_bb from the damped Hessian (gptq.py:147) */
+#define PT2Q_AGA_MASK 0x30
+
+/* ATQ stage modes (quantizer.py per-method surface) */
+#define PT2Q_STAGE_INIT 0   /* ternary_init            quantizer.py:32  */
+#define PT2Q_STAGE_GRID 1   /* build_optimal_grid      quantizer.py:71  */
+#define PT2Q_STAGE_ROUND 2  /* flexible_round          quantizer.py:110 */
+#define PT2Q_STAGE_ITF 3    /* iterative_ternary_fitting quantizer.py:136 */
+#define PT2Q_STAGE_AGA 4    /* activation_aware_grid_alignment quantizer.py:177 (given S1, d) */
+#define PT2Q_STAGE_FULL 5   /* quantize                quantizer.py:250 (init+ITF[+AGA]) */
+
+const char* pt2q_version(void);
+const char* pt2q_strerror(int status);
+
+/* Workspace bytes needed by pt2q_quantize_layer / pt2q_quantize_blocks / pt2q_cholesky_inverse
+ * for an n x m layer with block size b. */
+size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags);
+size_t pt2q_cholesky_workspace_bytes(int m);
+
+/* G = XᵀX (accumulate=0) or G = G + XᵀX (accumulate=1).  X: N x m of type xdtype.
+ * Replaces main.py:128 (H = X.T @ X) and gptq.py:59-76 (GPTQ.add_batch). Writes the full
+ * symmetric matrix. */
+int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G, int64_t ldg,
+              int accumulate, void* stream);
+
+/* H = G / nsamples; H_ii += percdamp * mean(diag H).  Replaces main.py:129-133 and
+ * gptq.py:94-98.  damp_dev (nullable) receives the damping value. */
+int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples, float percdamp,
+                         float* H, int64_t ldh, float* damp_dev, void* stream);
+
+/* Hinv = cholesky_inverse(cholesky(H)) (main.py:136-139, gptq.py:101-103), full symmetric.
+ * info_dev receives 0, or k+1 for the first non-positive pivot (then Hinv is undefined and the
+ * caller applies torch.linalg.pinv, main.py:140-141). */
+int pt2q_cholesky_inverse(const float* H, int64_t ldh, int m, float* Hinv, int64_t ldhi,
+                          void* workspace, size_t workspace_bytes, int* info_dev, void* stream);
+
+/* The block loop of main.py:158-230 (flags & PT2Q_AGA_ACT) or gptq.py:124-199 (PT2Q_AGA_HESS).
+ *   W      n x m weights (row-major, wdtype), read only.
+ *   A      AGA matrix: raw Gram XᵀX (ACT) or damped H (HESS); m x m; may be NULL for NONE.
+ *   Hinv   m x m inverse Hessian.
+ *   alpha, mu  n x B fp32 (B = ceil(m/b)), column k = k-th selected block.
+ *   T      n x m codes in ORIGINAL column order, int8 (tdtype PT2Q_I8) or fp32 (PT2Q_F32).
+ *   perm   m int64, concatenated block indices in selection order.
+ *   iters_dev  (nullable) B ints, ITF iterations per block. */
+int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int n, int m, int b, int flags,
+                         const float* A, int64_t lda, const float* Hinv, int64_t ldhi,
+                         int max_iter, float* alpha, float* mu, void* T, int tdtype,
+                         int64_t* perm, int* iters_dev, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Whole layer, variant M (main.py:102-230): gram -> prepare -> cholesky_inverse -> blocks.
+ * If info_dev reports a breakdown the outputs are undefined; the caller recomputes Hinv with
+ * pinv and calls pt2q_quantize_blocks (the staged path). */
+int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n, int m, const void* X,
+                        int xdtype, int64_t N, int64_t ldx, int b, int flags, float percdamp,
+                        int max_iter, float* alpha, float* mu, void* T, int tdtype,
+                        int64_t* perm, int* iters_dev, int* info_dev, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
+/* One ATQ stage on W (n x b, row-major fp32, leading dim ldw) (quantizer.py:32-293).
+ * alpha, mu: n fp32 (in for ROUND/ITF, out otherwise); T: n x b fp32, leading dim ldt
+ * (in for GRID/ITF/AGA, out for INIT/ROUND/ITF/FULL); S1 (b) and d_dev (1) for AGA/FULL
+ * (NULL S1 in FULL = no activations).  iters_dev (nullable) receives ITF iterations. */
+int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int b, float* alpha, float* mu,
+                   float* T, int64_t ldt, const float* S1, const float* d_dev, int max_iter,
+                   int* iters_dev, void* workspace, size_t workspace_bytes, void* stream);
+
+/* S1 = S·1 and d = 1ᵀS1 for a symmetric b x b matrix S (quantizer.py:215-218). */
+int pt2q_s1_from_gram(const float* S, int64_t lds, int b, float* S1, float* d_dev, void* stream);
+
+/* compute_column_similarity_to_mean + select_next_block_ssr (reorder.py:36-61,107-143) on W
+ * (n x m row-major fp32).  rem: r int64 ascending.  Writes min(b,r) entries of blk (selection
+ * order), r - min(b,r) entries of newrem (ascending), and r similarities to sim (nullable;
+ * untouched when r <= b). */
+size_t pt2q_ssr_workspace_bytes(int n, int m);
+int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const int64_t* rem, int r, int b,
+                    int64_t* blk, int64_t* newrem, float* sim, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/* Reconstruct W_q[:, perm[kb:(k+1)b]] = alpha[:,k] * T + mu[:,k] (gptq.py:201-230). T int8 or
+ * fp32 (tdtype), out fp32 n x m. */
+int pt2q_dequantize(const float* alpha, const float* mu, const void* T, int tdtype,
+                    const int64_t* perm, int n, int m, int b, float* out, void* stream);
+
+/* 2-bit packing of ternary codes, utils.py:189-219 layout ({-1,0,1} -> {0,1,2}, 4 per byte,
+ * little end first). count codes -> ceil(count/4) bytes. */
+int pt2q_pack_ternary(const int8_t* T, int64_t count, uint8_t* packed, void* stream);
+int pt2q_unpack_ternary(const uint8_t* packed, int64_t count, int8_t* T, void* stream);
+
+/* Counter-based synthetic tensors (tests/synth.py): out[i] = c_i * scale with
+ * c_i = (splitmix64(splitmix64(seed) + i) >> 40) - 2^23; when outlier_every > 0, columns j
+ * (= i % cols) with splitmix64(splitmix64(seed ^ 0x5BD1E995) + j) % outlier_every == 0 use
+ * scale_outlier instead. fp32 out. */
+int pt2q_fill_synthetic(float* out, int64_t count, uint64_t seed, float scale, int64_t cols,
+                        int outlier_every, float scale_outlier, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT2Q_H */

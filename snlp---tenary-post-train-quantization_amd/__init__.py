@@ -1,0 +1,27 @@
+"""pt2q — MI355X-native ternary PTQ calibration engine (PT²-LLM: ATQ + SSR inside a GPTQ loop).
+
+Drop-in for the reference's hot-path surface:
+    AsymmetricTernaryQuantizer, compute_quantization_error, compute_output_error  (quantizer.py)
+    compute_column_similarity_to_mean, select_next_block_ssr                      (reorder.py)
+    GPTQ, GPTQQuantizer                                                            (gptq.py)
+    PT2LLMQuantizer.quantize_layer                                                 (main.py)
+    pack_ternary, unpack_ternary                                                   (utils.py)
+All compute runs in libpt2q.so (HIP, gfx950); importing fails loudly if it is not built.
+"""
+from . import _lib
+from .quantizer import AsymmetricTernaryQuantizer, compute_output_error, compute_quantization_error
+from .reorder import compute_column_similarity_to_mean, select_next_block_ssr
+from .gptq import GPTQ, GPTQQuantizer
+from .pt2llm import PT2LLMQuantizer
+from .engine import (LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
+                     gram, pack_ternary, prepare_hessian, quantize_blocks, quantize_layer,
+                     unpack_ternary)
+
+__version__ = "0.1.0"
+__all__ = [
+    "AsymmetricTernaryQuantizer", "compute_quantization_error", "compute_output_error",
+    "compute_column_similarity_to_mean", "select_next_block_ssr", "GPTQ", "GPTQQuantizer",
+    "PT2LLMQuantizer", "LayerOutput", "LayerWorkspace", "gram", "prepare_hessian",
+    "cholesky_inverse", "quantize_blocks", "quantize_layer", "dequantize", "pack_ternary",
+    "unpack_ternary", "fill_synthetic",
+]

@@ -1,0 +1,105 @@
+"""ctypes binding of libpt2q.so (include/pt2q.h) for PyTorch-ROCm device tensors.
+
+The library is the product: there is no CPU or eager-PyTorch fallback.  If the shared object
+is missing this module raises at import, and every op requires tensors on a HIP device.
+"""
+import ctypes
+import os
+
+import torch
+
+_DIR = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_DIR, "libpt2q.so")
+
+PT2Q_OK = 0
+PT2Q_E_NOT_SPD = 2
+F32, F16, BF16, I8 = 0, 1, 2, 3
+FLAG_SSR = 0x1
+AGA_NONE, AGA_ACT, AGA_HESS = 0x0, 0x10, 0x20
+STAGE_INIT, STAGE_GRID, STAGE_ROUND, STAGE_ITF, STAGE_AGA, STAGE_FULL = range(6)
+
+_DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.int8: I8}
+
+
+class Pt2qError(RuntimeError):
+    pass
+
+
+if not os.path.exists(SO_PATH):
+    raise ImportError(
+        f"libpt2q.so not found at {SO_PATH}: build it with `python -c \"import __graft_entry__ as g; "
+        f"g.build()\"` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+
+_h = ctypes.CDLL(SO_PATH)
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+F = ctypes.c_float
+SZ = ctypes.c_size_t
+
+_SIGS = {
+    "pt2q_version": (ctypes.c_char_p, []),
+    "pt2q_strerror": (ctypes.c_char_p, [I]),
+    "pt2q_layer_workspace_bytes": (SZ, [I, I, I, I]),
+    "pt2q_cholesky_workspace_bytes": (SZ, [I]),
+    "pt2q_ssr_workspace_bytes": (SZ, [I, I]),
+    "pt2q_gram": (I, [P, I, I64, I, I64, P, I64, I, P]),
+    "pt2q_prepare_hessian": (I, [P, I64, I, I64, F, P, I64, P, P]),
+    "pt2q_cholesky_inverse": (I, [P, I64, I, P, I64, P, SZ, P, P]),
+    "pt2q_quantize_blocks": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, I, P, P, P, I, P, P, P,
+                                 SZ, P]),
+    "pt2q_quantize_layer": (I, [P, I, I64, I, I, P, I, I64, I64, I, I, F, I, P, P, P, I, P, P, P,
+                                P, SZ, P]),
+    "pt2q_atq_stage": (I, [I, P, I64, I, I, P, P, P, I64, P, P, I, P, P, SZ, P]),
+    "pt2q_s1_from_gram": (I, [P, I64, I, P, P, P]),
+    "pt2q_ssr_select": (I, [P, I64, I, I, P, I, I, P, P, P, P, SZ, P]),
+    "pt2q_dequantize": (I, [P, P, P, I, P, I, I, I, P, P]),
+    "pt2q_pack_ternary": (I, [P, I64, P, P]),
+    "pt2q_unpack_ternary": (I, [P, I64, P, P]),
+    "pt2q_fill_synthetic": (I, [P, I64, ctypes.c_uint64, F, I64, I, F, P]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(_h, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    return _h
+
+
+def version():
+    return _h.pt2q_version().decode()
+
+
+def check(rc, what=""):
+    if rc != PT2Q_OK:
+        raise Pt2qError(f"{what}: {_h.pt2q_strerror(rc).decode()} (status {rc})")
+
+
+def dtype_code(t):
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise Pt2qError("pt2q kernels need tensors on a HIP device (MI355X); got "
+                        f"{getattr(t, 'device', type(t))}")
+    return t.device
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -1,0 +1,332 @@
+// Exported C ABI of libpt2q (include/pt2q.h): argument checks, workspace carving and the
+// per-layer launch schedule.  All launches are stream-ordered; nothing here synchronises or
+// allocates, so a caller may capture a whole layer into a hipGraph.
+#include <string.h>
+
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+struct Carve {
+  char* p;
+  size_t left;
+  bool ok = true;
+  template <typename T>
+  T* take(size_t count) {
+    size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    if (!p || bytes > left) {
+      ok = false;
+      return nullptr;
+    }
+    T* r = (T*)p;
+    p += bytes;
+    left -= bytes;
+    return r;
+  }
+};
+
+inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
+
+struct BlockWs {
+  float* Wt;
+  int8_t* Tt;
+  float* Et;
+  float* Ck;
+  float* alpha_t;
+  float* mu_t;
+  float* S1;
+  float* d;
+  float* ssr;
+  int* rem[2];
+  int* blk;
+  int* counters;
+  int* iters;
+  long ldw;
+};
+
+bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
+  const long ldw = round_up(n, 64);
+  const int bb = b < m ? b : m;
+  const int B = b < m ? ceil_div(m, b) : 1;
+  w.ldw = ldw;
+  w.Wt = c.take<float>((size_t)m * ldw);
+  w.Tt = c.take<int8_t>((size_t)m * ldw);
+  w.Et = c.take<float>((size_t)bb * ldw);
+  w.Ck = c.take<float>((size_t)bb * m);
+  w.alpha_t = c.take<float>((size_t)B * n);
+  w.mu_t = c.take<float>((size_t)B * n);
+  w.S1 = c.take<float>((size_t)bb);
+  w.d = c.take<float>(1);
+  w.ssr = c.take<float>(pt2q_ssr_scratch_floats(n, m));
+  w.rem[0] = c.take<int>((size_t)m);
+  w.rem[1] = c.take<int>((size_t)m);
+  w.blk = c.take<int>((size_t)bb);
+  w.counters = c.take<int>((size_t)2 * B);
+  w.iters = c.take<int>((size_t)B);
+  return c.ok;
+}
+
+size_t blocks_bytes(int n, int m, int b) {
+  Carve c{nullptr, 0};
+  // dry run: count
+  size_t total = 0;
+  auto add = [&](size_t bytes) { total += (bytes + 255) & ~(size_t)255; };
+  const long ldw = round_up(n, 64);
+  const int bb = b < m ? b : m;
+  const int B = b < m ? ceil_div(m, b) : 1;
+  add((size_t)m * ldw * 4);
+  add((size_t)m * ldw);
+  add((size_t)bb * ldw * 4);
+  add((size_t)bb * m * 4);
+  add((size_t)B * n * 4);
+  add((size_t)B * n * 4);
+  add((size_t)bb * 4);
+  add(4);
+  add(pt2q_ssr_scratch_floats(n, m) * 4);
+  add((size_t)m * 4);
+  add((size_t)m * 4);
+  add((size_t)bb * 4);
+  add((size_t)2 * B * 4);
+  add((size_t)B * 4);
+  (void)c;
+  return total;
+}
+
+__global__ void i64_to_i32_kernel(const int64_t* a, int n, int* b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = (int)a[i];
+}
+__global__ void i32_to_i64_kernel(const int* a, int n, int64_t* b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int flags,
+               const float* A, long lda, const float* Hinv, long ldhi, int max_iter, float* alpha,
+               float* mu, void* T, int tdtype, int64_t* perm, int* iters_dev, BlockWs& w,
+               hipStream_t st) {
+  int rc;
+  const int B = b < m ? ceil_div(m, b) : 1;
+  const bool ssr = (flags & PT2Q_FLAG_SSR) != 0;
+  const int aga = flags & PT2Q_AGA_MASK;
+  int* iters = iters_dev ? iters_dev : w.iters;
+  // W (n x m) -> Wt (m x ldw, fp32)
+  if ((rc = pt2q_launch_transpose_to_f32(W, wdtype, ldw_in, n, m, w.Wt, w.ldw, st)) != PT2Q_OK)
+    return rc;
+  if (hipMemsetAsync(w.counters, 0, sizeof(int) * 2 * B, st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(iters, 0, sizeof(int) * B, st) != hipSuccess) return PT2Q_E_HIP;
+  // rem0 = [0, m)
+  if ((rc = pt2q_launch_select_seq(0, 0, 0, m, nullptr, w.blk, w.rem[0], nullptr, st)) != PT2Q_OK)
+    return rc;
+  float* part = w.ssr;
+  float* wn = part + (size_t)ceil_div(m, 128) * n;
+  float* sim = wn + n;
+  int processed = 0, r = m, cur = 0;
+  for (int k = 0; k < B; ++k) {
+    const int bs = r < b ? r : b;
+    const int nr = r - bs;
+    int* rem = w.rem[cur];
+    int* nrem = w.rem[cur ^ 1];
+    if (ssr) {
+      if (r > b) {
+        if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st)) != PT2Q_OK)
+          return rc;
+        if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
+          return rc;
+      } else {
+        if ((rc = pt2q_launch_select_seq(1, 0, bs, m, rem, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
+          return rc;
+      }
+    } else {
+      if ((rc = pt2q_launch_select_seq(0, processed, bs, m, nullptr, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
+        return rc;
+    }
+    const float* S1 = nullptr;
+    if (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_HESS) {
+      if ((rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK)
+        return rc;
+      S1 = w.S1;
+    }
+    if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
+                                    w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
+                                    w.Et, w.ldw, iters + k, w.counters + 2 * k, st)) != PT2Q_OK)
+      return rc;
+    if (nr > 0) {
+      if ((rc = pt2q_launch_ef_coeffs(Hinv, ldhi, w.blk, bs, nrem, nr, w.Ck, m, st)) != PT2Q_OK)
+        return rc;
+      GemmDesc g{};
+      g.M = nr; g.N = n; g.K = bs;
+      g.A = w.Ck; g.lda = m; g.a_layout = LAY_KMAJOR;     // (e, k) = C[k][e]
+      g.B = w.Et; g.ldb = w.ldw; g.b_layout = LAY_KMAJOR; // (k, i) = E[k][i]
+      g.in_dtype = PT2Q_F32;
+      g.C = w.Wt; g.ldc = w.ldw; g.crow = nrem;
+      g.mode = GEMM_SUB;
+      if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
+    }
+    processed += bs;
+    r = nr;
+    cur ^= 1;
+  }
+  // outputs: T (n x m) from Tt (m x ldw); alpha/mu (n x B) from (B x n)
+  if ((rc = pt2q_launch_transpose_i8(w.Tt, w.ldw, m, n, T, tdtype, m, st)) != PT2Q_OK) return rc;
+  if ((rc = pt2q_launch_transpose_f32(w.alpha_t, n, B, n, alpha, B, st)) != PT2Q_OK) return rc;
+  if ((rc = pt2q_launch_transpose_f32(w.mu_t, n, B, n, mu, B, st)) != PT2Q_OK) return rc;
+  return PT2Q_OK;
+}
+
+bool dtype_ok(int dt) { return dt == PT2Q_F32 || dt == PT2Q_F16 || dt == PT2Q_BF16; }
+
+}  // namespace
+
+extern "C" const char* pt2q_version(void) { return "pt2q-mi355x 0.1.0 (gfx950)"; }
+
+extern "C" const char* pt2q_strerror(int status) {
+  switch (status) {
+    case PT2Q_OK: return "ok";
+    case PT2Q_E_ARG: return "invalid argument";
+    case PT2Q_E_NOT_SPD: return "Hessian not positive definite (Cholesky breakdown)";
+    case PT2Q_E_UNSUPPORTED: return "unsupported shape/configuration";
+    case PT2Q_E_HIP: return "HIP runtime error";
+    case PT2Q_E_WORKSPACE: return "workspace too small";
+  }
+  return "unknown status";
+}
+
+extern "C" size_t pt2q_cholesky_workspace_bytes(int m) {
+  return 2 * (((size_t)m * m * 4 + 255) & ~(size_t)255);
+}
+
+extern "C" size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags) {
+  (void)flags;
+  if (n <= 0 || m <= 0 || b <= 0) return 0;
+  size_t mm = ((size_t)m * m * 4 + 255) & ~(size_t)255;
+  return blocks_bytes(n, m, b) + 4 * mm + 2 * 256;
+}
+
+extern "C" size_t pt2q_ssr_workspace_bytes(int n, int m) {
+  return blocks_bytes(n, m, 128);
+}
+
+extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G,
+                         int64_t ldg, int accumulate, void* stream) {
+  if (!X || !G || N < 0 || m <= 0 || !dtype_ok(xdtype) || ldx < m || ldg < m) return PT2Q_E_ARG;
+  GemmDesc g{};
+  g.M = m; g.N = m; g.K = (int)N;
+  g.A = X; g.lda = ldx; g.a_layout = LAY_KMAJOR;
+  g.B = X; g.ldb = ldx; g.b_layout = LAY_KMAJOR;
+  g.in_dtype = xdtype;
+  g.C = G; g.ldc = ldg;
+  g.mode = accumulate ? GEMM_ADD : GEMM_STORE;
+  g.upper = 1; g.mirror = 1;
+  return pt2q_launch_gemm(g, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples,
+                                    float percdamp, float* H, int64_t ldh, float* damp_dev,
+                                    void* stream) {
+  if (!G || !H || m <= 0 || nsamples <= 0) return PT2Q_E_ARG;
+  return pt2q_launch_prepare_hessian(G, ldg, m, nsamples, percdamp, H, ldh, damp_dev,
+                                     (hipStream_t)stream);
+}
+
+extern "C" int pt2q_cholesky_inverse(const float* H, int64_t ldh, int m, float* Hinv,
+                                     int64_t ldhi, void* workspace, size_t workspace_bytes,
+                                     int* info_dev, void* stream) {
+  if (!H || !Hinv || !info_dev || m <= 0) return PT2Q_E_ARG;
+  Carve c{(char*)workspace, workspace_bytes};
+  float* U = c.take<float>((size_t)m * m);
+  float* Ui = c.take<float>((size_t)m * m);
+  if (!c.ok) return PT2Q_E_WORKSPACE;
+  return pt2q_launch_cholesky_inverse(H, ldh, m, Hinv, ldhi, U, Ui, info_dev, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int n, int m, int b,
+                                    int flags, const float* A, int64_t lda, const float* Hinv,
+                                    int64_t ldhi, int max_iter, float* alpha, float* mu, void* T,
+                                    int tdtype, int64_t* perm, int* iters_dev, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  if (!W || !Hinv || !alpha || !mu || !T || !perm || n <= 0 || m <= 0 || b <= 0 ||
+      !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0)
+    return PT2Q_E_ARG;
+  int aga = flags & PT2Q_AGA_MASK;
+  if (aga != PT2Q_AGA_NONE && !A) return PT2Q_E_ARG;
+  if (aga == PT2Q_AGA_HESS && (b < m ? b : m) > 128) return PT2Q_E_UNSUPPORTED;
+  if ((b < m ? b : m) > 512) return PT2Q_E_UNSUPPORTED;
+  Carve c{(char*)workspace, workspace_bytes};
+  BlockWs w;
+  if (!carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
+  return run_blocks(W, wdtype, ldw, n, m, b, flags, A, lda, Hinv, ldhi, max_iter, alpha, mu, T,
+                    tdtype, perm, iters_dev, w, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n, int m,
+                                   const void* X, int xdtype, int64_t N, int64_t ldx, int b,
+                                   int flags, float percdamp, int max_iter, float* alpha,
+                                   float* mu, void* T, int tdtype, int64_t* perm, int* iters_dev,
+                                   int* info_dev, void* workspace, size_t workspace_bytes,
+                                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!W || !X || !info_dev || N <= 0 || m <= 0 || n <= 0 || b <= 0 || !dtype_ok(xdtype))
+    return PT2Q_E_ARG;
+  if ((b < m ? b : m) > 512) return PT2Q_E_UNSUPPORTED;
+  Carve c{(char*)workspace, workspace_bytes};
+  float* G = c.take<float>((size_t)m * m);
+  float* H = c.take<float>((size_t)m * m);
+  float* Ui = c.take<float>((size_t)m * m);
+  float* Hinv = c.take<float>((size_t)m * m);
+  float* damp = c.take<float>(1);
+  BlockWs w;
+  if (!c.ok || !carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
+  int rc;
+  if ((rc = pt2q_gram(X, xdtype, N, m, ldx, G, m, 0, stream)) != PT2Q_OK) return rc;
+  if ((rc = pt2q_launch_prepare_hessian(G, m, m, N, percdamp, H, m, damp, st)) != PT2Q_OK) return rc;
+  // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G)
+  if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st)) != PT2Q_OK) return rc;
+  int f = (flags & ~PT2Q_AGA_MASK) | PT2Q_AGA_ACT;
+  return run_blocks(W, wdtype, ldw, n, m, b, f, G, m, Hinv, m, max_iter, alpha, mu, T, tdtype,
+                    perm, iters_dev, w, st);
+}
+
+extern "C" int pt2q_s1_from_gram(const float* S, int64_t lds, int b, float* S1, float* d_dev,
+                                 void* stream) {
+  if (!S || !S1 || !d_dev || b <= 0) return PT2Q_E_ARG;
+  return pt2q_launch_aga_s1(1, S, lds, nullptr, b, S1, d_dev, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const int64_t* rem, int r,
+                               int b, int64_t* blk, int64_t* newrem, float* sim, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!W || !rem || !blk || n <= 0 || m <= 0 || r <= 0 || r > m || b <= 0) return PT2Q_E_ARG;
+  if (r > b && !newrem) return PT2Q_E_ARG;
+  Carve c{(char*)workspace, workspace_bytes};
+  BlockWs w;
+  if (!carve_blocks(c, n, m, 128, w)) return PT2Q_E_WORKSPACE;
+  int rc;
+  if ((rc = pt2q_launch_transpose_to_f32(W, PT2Q_F32, ldw, n, m, w.Wt, w.ldw, st)) != PT2Q_OK) return rc;
+  hipLaunchKernelGGL(i64_to_i32_kernel, dim3(ceil_div(r, 256)), dim3(256), 0, st, rem, r, w.rem[0]);
+  PT2Q_LAUNCH_CHECK();
+  const int bs = r < b ? r : b;
+  // blk indices (int32) are staged in rem[1] (capacity m >= b); newrem in the Tt scratch
+  int* blk32 = w.rem[1];
+  int* nrem32 = (int*)w.Tt;  // m*ldw bytes >= 4m
+  if (sim || r > b) {
+    float* part = w.ssr;
+    float* wn = part + (size_t)ceil_div(m, 128) * n;
+    float* simb = sim ? sim : wn + n;
+    if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, w.rem[0], r, part, wn, simb, st)) != PT2Q_OK)
+      return rc;
+    if (r > b) {
+      if ((rc = pt2q_launch_ssr_topk(simb, w.rem[0], r, b, blk32, nrem32, nullptr, st)) != PT2Q_OK)
+        return rc;
+      hipLaunchKernelGGL(i32_to_i64_kernel, dim3(ceil_div(r - bs, 256)), dim3(256), 0, st, nrem32,
+                         r - bs, newrem);
+      PT2Q_LAUNCH_CHECK();
+    }
+  }
+  if (r <= b) blk32 = w.rem[0];
+  hipLaunchKernelGGL(i32_to_i64_kernel, dim3(ceil_div(bs, 256)), dim3(256), 0, st, blk32, bs, blk);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}

@@ -1,0 +1,386 @@
+// Asymmetric Ternary Quantizer (ATQ) kernels: init + ITF + AGA + error term, one pass.
+//
+// Reference: quantizer.py:32-293 (AsymmetricTernaryQuantizer), main.py:176-189 (per-block use).
+//
+// Mapping: a wave64 holds 4 weight rows; the 16 lanes of a row own the block columns
+// k = l + 16 s (l = lane & 15, s = 0..NS-1), keeping w and the ternary codes in registers.
+// Every row reduction is the canonical SUM16 (lane-sequential over s, then an xor-8/4/2/1
+// butterfly), the same order oracle/pt2q_oracle.c uses, so codes AND scales are bit-identical
+// to the oracle.  The reference's whole-block ITF stop (torch.equal over the block,
+// quantizer.py:164) is evaluated per wave: rows that have converged are fixed points of
+// grid+round, so continuing them reproduces the block loop exactly; the one block-level case
+// that differs (every row's T_init == 0 -> the block loop returns the init grid untouched) is
+// detected with a per-block counter and repaired by the last workgroup to finish.
+#include <type_traits>
+
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+constexpr int ROWS_PER_WAVE = 4;
+constexpr int WAVES = 4;
+constexpr int ROWS_PER_WG = ROWS_PER_WAVE * WAVES;
+
+template <int NS>
+struct Row {
+  float w[NS];
+  float t[NS];
+  int l, b;
+  PT2Q_DEV bool has(int s) const { return l + 16 * s < b; }
+};
+
+template <int NS>
+PT2Q_DEV float row_sum_w(const Row<NS>& R) {
+  float p = 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) p = p + R.w[s];
+  return bfly16(p);
+}
+
+// ternary_init, quantizer.py:32-69. Returns alpha0, mu0; sets R.t; returns whether all t == 0.
+template <int NS>
+PT2Q_DEV bool row_init(Row<NS>& R, float wsum, float* alpha0, float* mu0) {
+  const float fb = (float)R.b;
+  float mu = wsum / fb;
+  float p = 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) p = p + fabsf(R.w[s] - mu);
+  float delta = 0.75f * (bfly16(p) / fb);
+  float pn = 0.0f, pd = 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float t = 0.0f;
+    if (R.has(s)) {
+      float wc = R.w[s] - mu;
+      t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
+      pn = pn + t * wc;
+      pd = pd + fabsf(t);
+    }
+    R.t[s] = t;
+  }
+  float num = bfly16(pn);
+  float cnt = bfly16(pd);
+  *alpha0 = num / clampmin(cnt);
+  *mu0 = mu;
+  return cnt == 0.0f;
+}
+
+// build_optimal_grid, quantizer.py:71-108.
+template <int NS>
+PT2Q_DEV void row_grid(const Row<NS>& R, float wsum, float* a, float* m) {
+  float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) {
+      pwt = pwt + R.w[s] * R.t[s];
+      pt = pt + R.t[s];
+      pt2 = pt2 + R.t[s] * R.t[s];
+    }
+  float swt = bfly16(pwt), ts = bfly16(pt), t2 = bfly16(pt2);
+  const float fb = (float)R.b;
+  float den = clampmin(fb * t2 - ts * ts);
+  *a = (fb * swt - ts * wsum) / den;
+  *m = (t2 * wsum - ts * swt) / den;
+}
+
+// flexible_round, quantizer.py:110-134. Returns true if this lane changed a code.
+template <int NS>
+PT2Q_DEV bool row_round(Row<NS>& R, float a, float m) {
+  float as = clampmin(a);
+  bool changed = false;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) {
+      float z = (R.w[s] - m) / as;
+      float nt = (z > 0.5f) ? 1.0f : ((z < -0.5f) ? -1.0f : 0.0f);
+      changed |= (nt != R.t[s]);
+      R.t[s] = nt;
+    }
+  return changed;
+}
+
+// iterative_ternary_fitting, quantizer.py:136-175, wave-level stop (see file header).
+// Assumes the block is not all-zero at init (iteration 0 never stops).
+template <int NS>
+PT2Q_DEV int row_itf(Row<NS>& R, float wsum, int max_iter, float* a, float* m) {
+  int it = 0;
+  bool any = true;
+  for (; it < max_iter; ++it) {
+    if (!any) break;
+    row_grid(R, wsum, a, m);
+    bool ch = row_round(R, *a, *m);
+    any = __any(ch);
+  }
+  return it;
+}
+
+// activation_aware_grid_alignment, quantizer.py:177-248, given S1 (per lane) and d.
+template <int NS>
+PT2Q_DEV void row_aga(const Row<NS>& R, const float (&S1)[NS], float d, float* a, float* m) {
+  float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) {
+      float t = R.t[s], w = R.w[s], c = S1[s];
+      pv = fmaf(t, c, pv);
+      pws = fmaf(w, c, pws);
+      pwts = fmaf(w * t, c, pwts);
+      pt2s = fmaf(t * t, c, pt2s);
+    }
+  float v = bfly16(pv), ws1 = bfly16(pws), wts1 = bfly16(pwts), t2s1 = bfly16(pt2s);
+  float v2 = v * v;
+  float den = clampmin(d * t2s1 - v2);
+  *a = (d * wts1 - v * ws1) / den;
+  *m = (t2s1 * ws1 - v * wts1) / den;
+}
+
+struct BlockArgs {
+  const float* Wt;   // m x ldw feature-major working weights
+  long ldw;
+  int n, b;
+  const int* blk;    // b column indices (selection order)
+  const float* S1;   // b, or nullptr (no AGA)
+  const float* d;    // device scalar
+  int max_iter;
+  float* alpha;      // n   (row kb of alpha_t)
+  float* mu;         // n
+  int8_t* Tt;        // m x ldt int8 codes (feature-major, original order)
+  long ldt;
+  float* Et;         // b x lde error term E[k][i] = w - (alpha*t + mu)
+  long lde;
+  int* iters;        // 1 int (atomicMax), nullable
+  int* counters;     // [0] zero-init rows, [1] workgroups done
+};
+
+template <int NS>
+PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_zero) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane >> 4, l = lane & 15;
+  const int i = row0 + r;
+  const bool valid = i < A.n;
+  Row<NS> R;
+  R.l = l;
+  R.b = A.b;
+  int colrow[NS];
+  float S1[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int k = l + 16 * s;
+    colrow[s] = (k < A.b) ? A.blk[k] : 0;
+    R.w[s] = (valid && k < A.b) ? A.Wt[(long)colrow[s] * A.ldw + i] : 0.0f;
+    S1[s] = (A.S1 && k < A.b) ? A.S1[k] : 0.0f;
+  }
+  float wsum = row_sum_w(R);
+  float a, m;
+  bool zero = row_init(R, wsum, &a, &m);
+  if (count_zero && valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
+  int it = 0;
+  if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
+  if (A.S1) row_aga(R, S1, *A.d, &a, &m);
+  if (A.iters && lane == 0 && !skip_itf) atomicMax(A.iters, it);
+  if (!valid) return;
+  if (l == 0) {
+    A.alpha[i] = a;
+    A.mu[i] = m;
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (R.has(s)) {
+      int k = l + 16 * s;
+      A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
+      A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
+    }
+}
+
+template <int NS>
+__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
+  const int wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE;
+  block_rows<NS>(A, row0, false, true);
+  // Last-arriving workgroup repairs the whole-block T_init == 0 case (quantizer.py:164 breaks
+  // at iteration 0 and returns the init grid).  Release/acquire per cdna_hip_programming §6 G16.
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = __hip_atomic_fetch_add(&A.counters[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (ticket == (int)gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  int zero_rows = __hip_atomic_load(&A.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (zero_rows != A.n) return;
+  if (A.iters && threadIdx.x == 0) *A.iters = 0;
+  for (int row0b = wave * ROWS_PER_WAVE; row0b < A.n; row0b += ROWS_PER_WG)
+    block_rows<NS>(A, row0b, true, false);
+}
+
+// ----------------------------------------------------------------- per-stage kernel (row-major)
+
+struct StageArgs {
+  int mode;
+  const float* W;
+  long ldw;
+  int n, b;
+  float* alpha;
+  float* mu;
+  float* T;
+  long ldt;
+  const float* S1;
+  const float* d;
+  int max_iter;
+  int* iters;
+  int* zero_rows;  // FULL / ITF: block all-zero detection (two-pass)
+  int pass;        // FULL: 0 = init + count, 1 = finish
+};
+
+template <int NS>
+__global__ __launch_bounds__(256) void atq_stage_kernel(StageArgs A) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane >> 4, l = lane & 15;
+  const int i = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE + r;
+  const bool valid = i < A.n;
+  Row<NS> R;
+  R.l = l;
+  R.b = A.b;
+  float S1[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    int k = l + 16 * s;
+    R.w[s] = (valid && k < A.b) ? A.W[(long)i * A.ldw + k] : 0.0f;
+    R.t[s] = (valid && k < A.b && A.mode != PT2Q_STAGE_INIT && A.mode != PT2Q_STAGE_ROUND &&
+              A.mode != PT2Q_STAGE_FULL)
+                 ? A.T[(long)i * A.ldt + k]
+                 : 0.0f;
+    S1[s] = (A.S1 && k < A.b) ? A.S1[k] : 0.0f;
+  }
+  float wsum = row_sum_w(R);
+  float a = valid ? A.alpha[i] : 0.0f, m = valid ? A.mu[i] : 0.0f;
+  int it = 0;
+  bool write_t = true;
+  switch (A.mode) {
+    case PT2Q_STAGE_INIT:
+      row_init(R, wsum, &a, &m);
+      break;
+    case PT2Q_STAGE_GRID:
+      row_grid(R, wsum, &a, &m);
+      write_t = false;
+      break;
+    case PT2Q_STAGE_ROUND:
+      row_round(R, a, m);
+      break;
+    case PT2Q_STAGE_ITF: {
+      // Caller passes init (alpha, mu, T); zero_rows[0] holds the count of all-zero T rows.
+      bool block_zero = (*A.zero_rows == A.n);
+      if (!block_zero) it = row_itf(R, wsum, A.max_iter, &a, &m);
+      break;
+    }
+    case PT2Q_STAGE_AGA:
+      row_aga(R, S1, *A.d, &a, &m);
+      write_t = false;
+      break;
+    case PT2Q_STAGE_FULL: {
+      bool zero = row_init(R, wsum, &a, &m);
+      if (A.pass == 0) {
+        if (valid && l == 0 && zero) atomicAdd(A.zero_rows, 1);
+        return;
+      }
+      bool block_zero = (*A.zero_rows == A.n);
+      if (!block_zero) it = row_itf(R, wsum, A.max_iter, &a, &m);
+      if (A.S1) row_aga(R, S1, *A.d, &a, &m);
+      break;
+    }
+  }
+  if (A.iters && lane == 0) atomicMax(A.iters, it);
+  if (!valid) return;
+  if (l == 0 && A.mode != PT2Q_STAGE_ROUND) {
+    A.alpha[i] = a;
+    A.mu[i] = m;
+  }
+  if (write_t) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (R.has(s)) A.T[(long)i * A.ldt + l + 16 * s] = R.t[s];
+  }
+}
+
+// count of all-zero T rows (for the ITF stage's iteration-0 block check)
+__global__ void count_zero_rows_kernel(const float* T, long ldt, int n, int b, int* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool z = true;
+  for (int k = 0; k < b; ++k) z &= (T[(long)i * ldt + k] == 0.0f);
+  if (z) atomicAdd(out, 1);
+}
+
+template <typename F>
+int dispatch_ns(int b, F&& f) {
+  if (b <= 128) return f(std::integral_constant<int, 8>{});
+  if (b <= 256) return f(std::integral_constant<int, 16>{});
+  if (b <= 512) return f(std::integral_constant<int, 32>{});
+  return PT2Q_E_UNSUPPORTED;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- internal launchers
+
+int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
+                          const float* S1, const float* d, int max_iter, float* alpha, float* mu,
+                          int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
+                          hipStream_t st) {
+  BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters};
+  int grid = ceil_div(n, ROWS_PER_WG);
+  return dispatch_ns(b, [&](auto ns) {
+    constexpr int NS = decltype(ns)::value;
+    hipLaunchKernelGGL(atq_block_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  });
+}
+
+extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int b, float* alpha,
+                              float* mu, float* T, int64_t ldt, const float* S1,
+                              const float* d_dev, int max_iter, int* iters_dev, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n <= 0 || b <= 0 || !W || !alpha || !mu || !T) return PT2Q_E_ARG;
+  if ((mode == PT2Q_STAGE_AGA) && (!S1 || !d_dev)) return PT2Q_E_ARG;
+  if ((mode == PT2Q_STAGE_ITF || mode == PT2Q_STAGE_FULL) &&
+      (!workspace || workspace_bytes < sizeof(int)))
+    return PT2Q_E_WORKSPACE;
+  int* zero_rows = (int*)workspace;
+  int grid = ceil_div(n, ROWS_PER_WG);
+  StageArgs A{mode, W, ldw, n, b, alpha, mu, T, ldt, S1, d_dev, max_iter, iters_dev, zero_rows, 0};
+  if (iters_dev && (mode == PT2Q_STAGE_ITF || mode == PT2Q_STAGE_FULL))
+    if (hipMemsetAsync(iters_dev, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+  if (mode == PT2Q_STAGE_ITF) {
+    if (hipMemsetAsync(zero_rows, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+    hipLaunchKernelGGL(count_zero_rows_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, T, ldt,
+                       n, b, zero_rows);
+    PT2Q_LAUNCH_CHECK();
+  }
+  return dispatch_ns(b, [&](auto ns) {
+    constexpr int NS = decltype(ns)::value;
+    if (mode == PT2Q_STAGE_FULL) {
+      if (hipMemsetAsync(zero_rows, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+      StageArgs A0 = A;
+      A0.pass = 0;
+      hipLaunchKernelGGL(atq_stage_kernel<NS>, dim3(grid), dim3(256), 0, st, A0);
+      PT2Q_LAUNCH_CHECK();
+      A.pass = 1;
+    }
+    hipLaunchKernelGGL(atq_stage_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  });
+}

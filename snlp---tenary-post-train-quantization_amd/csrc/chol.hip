@@ -1,0 +1,177 @@
+// Cholesky factorisation and inverse of the damped Hessian (main.py:136-139, gptq.py:101-103:
+// torch.linalg.cholesky + torch.cholesky_inverse) under the PT2Q contract:
+//
+//   U (upper, H = UᵀU):  acc = H[k][i]; for j < k ascending: acc = fmaf(-U[j][k], U[j][i], acc);
+//                        U[k][k] = sqrt(acc) (breakdown if !(acc > 0)); U[k][i] = acc / U[k][k]
+//   Uinv = U⁻¹:          Uinv[k][k] = 1/U[k][k]; Uinv[k][i] = -(j-ascending chain over
+//                        j in [k,i) of Uinv[k][j]*U[j][i]) / U[i][i]
+//   Hinv = Uinv·Uinvᵀ:   Hinv[i][k] = j-ascending chain over j >= max(i,k) of Uinv[i][j]*Uinv[k][j]
+//
+// Blocked right-looking with NB = 64 panels; the trailing updates and the triangular products
+// run on the f32-MFMA GEMM (gemm.hip) whose k-ordered chains keep every element bit-identical
+// to the unblocked definition above (oracle/pt2q_oracle.c).
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+constexpr int NB = 64;
+
+// Factor the nb x nb diagonal block at (p0, p0) in place (upper triangle), right-looking.
+__global__ __launch_bounds__(1024) void chol_diag_kernel(float* A, long lda, int p0, int nb,
+                                                         int* info) {
+  __shared__ float D[NB][NB + 1];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < nb * nb; q += blockDim.x) {
+    int r = q / nb, c = q % nb;
+    D[r][c] = A[(long)(p0 + r) * lda + p0 + c];
+  }
+  __syncthreads();
+  for (int k = 0; k < nb; ++k) {
+    if (tid == 0) {
+      float akk = D[k][k];
+      if (!(akk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
+      D[k][k] = sqrtf(akk);
+    }
+    __syncthreads();
+    const float ukk = D[k][k];
+    for (int i = k + 1 + tid; i < nb; i += blockDim.x) D[k][i] = D[k][i] / ukk;
+    __syncthreads();
+    const int w = nb - k - 1;  // rows/cols k+1 .. nb-1
+    for (int q = tid; q < w * w; q += blockDim.x) {
+      int r = k + 1 + q / w, i = k + 1 + q % w;
+      if (i >= r) D[r][i] = fmaf(-D[k][r], D[k][i], D[r][i]);
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < nb * nb; q += blockDim.x) {
+    int r = q / nb, c = q % nb;
+    if (c >= r) A[(long)(p0 + r) * lda + p0 + c] = D[r][c];
+  }
+}
+
+// Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution with the factored
+// diagonal block (chains continue from the already-updated A values).
+__global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int p0, int nb,
+                                                         int m) {
+  __shared__ float D[NB][NB + 1];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < nb * nb; q += blockDim.x) {
+    int r = q / nb, c = q % nb;
+    D[r][c] = A[(long)(p0 + r) * lda + p0 + c];
+  }
+  __syncthreads();
+  const int i = p0 + nb + blockIdx.x * blockDim.x + tid;
+  if (i >= m) return;
+  float x[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) x[k] = (k < nb) ? A[(long)(p0 + k) * lda + i] : 0.0f;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    if (k < nb) {
+      x[k] = x[k] / D[k][k];
+#pragma unroll
+      for (int r = k + 1; r < NB; ++r)
+        if (r < nb) x[r] = fmaf(-D[k][r], x[k], x[r]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+    if (k < nb) A[(long)(p0 + k) * lda + i] = x[k];
+}
+
+// In-block part of the triangular inverse for column block [c0, c0+nb): rows k < c0+nb.
+// Ui[k][c0..] holds the GEMM partial chains for k < c0 (zero otherwise).
+__global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long ldu, float* Ui,
+                                                            long ldi, int c0, int nb) {
+  __shared__ float D[NB][NB + 1];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < nb * nb; q += blockDim.x) {
+    int r = q / nb, c = q % nb;
+    D[r][c] = U[(long)(c0 + r) * ldu + c0 + c];
+  }
+  __syncthreads();
+  const int k = blockIdx.x * blockDim.x + tid;
+  if (k >= c0 + nb) return;
+  float acc[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) acc[q] = (k < c0 && q < nb) ? Ui[(long)k * ldi + c0 + q] : 0.0f;
+  const int jb = (k > c0) ? k - c0 : 0;  // first in-block j (local)
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (j < nb && j >= jb) {
+      float xj = (c0 + j == k) ? 1.0f / D[j][j] : -acc[j] / D[j][j];
+      acc[j] = xj;
+#pragma unroll
+      for (int q = j + 1; q < NB; ++q)
+        if (q < nb) acc[q] = fmaf(xj, D[j][q], acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q)
+    if (q < nb) Ui[(long)k * ldi + c0 + q] = (q >= jb) ? acc[q] : 0.0f;
+}
+
+__global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m) {
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long)m * m) return;
+  int r = (int)(q / m), c = (int)(q % m);
+  A[(long)r * lda + c] = (c >= r) ? H[(long)r * ldh + c] : 0.0f;
+}
+
+}  // namespace
+
+int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
+                                 float* U, float* Ui, int* info, hipStream_t st) {
+  const long ld = m;  // U and Ui are packed m x m
+  if (hipMemsetAsync(info, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+  hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
+                     U, ld, m);
+  PT2Q_LAUNCH_CHECK();
+  int rc;
+  for (int p0 = 0; p0 < m; p0 += NB) {
+    int nb = (m - p0 < NB) ? m - p0 : NB;
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(1024), 0, st, U, ld, p0, nb, info);
+    PT2Q_LAUNCH_CHECK();
+    int rest = m - p0 - nb;
+    if (rest <= 0) break;
+    hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div(rest, 256)), dim3(256), 0, st, U, ld, p0,
+                       nb, m);
+    PT2Q_LAUNCH_CHECK();
+    GemmDesc g{};
+    g.M = rest; g.N = rest; g.K = nb;
+    g.A = U + (long)p0 * ld + p0 + nb; g.lda = ld; g.a_layout = LAY_KMAJOR;
+    g.B = U + (long)p0 * ld + p0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;
+    g.in_dtype = PT2Q_F32;
+    g.C = U + (long)(p0 + nb) * ld + p0 + nb; g.ldc = ld;
+    g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
+    if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
+  }
+  // Uinv = U^-1 by column blocks
+  if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
+  for (int c0 = 0; c0 < m; c0 += NB) {
+    int nb = (m - c0 < NB) ? m - c0 : NB;
+    if (c0 > 0) {
+      GemmDesc g{};
+      g.M = c0; g.N = nb; g.K = c0;
+      g.A = Ui; g.lda = ld; g.a_layout = LAY_ROWMAJOR;      // (k, j) = Ui[k][j]
+      g.B = U + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;     // (j, i) = U[j][c0+i]
+      g.in_dtype = PT2Q_F32;
+      g.C = Ui + c0; g.ldc = ld;
+      g.mode = GEMM_STORE; g.kstart_diag = 1;
+      if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
+    }
+    hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div(c0 + nb, 256)), dim3(256), 0, st, U, ld,
+                       Ui, ld, c0, nb);
+    PT2Q_LAUNCH_CHECK();
+  }
+  // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
+  GemmDesc g{};
+  g.M = m; g.N = m; g.K = m;
+  g.A = Ui; g.lda = ld; g.a_layout = LAY_ROWMAJOR;   // (i, j) = Ui[i][j]
+  g.B = Ui; g.ldb = ld; g.b_layout = LAY_ROWMAJOR;   // (j, k) = Ui[k][j]
+  g.in_dtype = PT2Q_F32;
+  g.C = Hinv; g.ldc = ldhi;
+  g.mode = GEMM_STORE; g.upper = 1; g.mirror = 1; g.kstart_diag = 2;
+  return pt2q_launch_gemm(g, st);
+}

@@ -1,0 +1,59 @@
+// Internal (non-exported) launchers shared between the libpt2q translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// ---- ATQ (atq.hip)
+int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
+                          const float* S1, const float* d, int max_iter, float* alpha, float* mu,
+                          int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
+                          hipStream_t st);
+
+// ---- SSR / selection (ssr.hip)
+int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
+                               float* part, float* wn, float* sim, hipStream_t st);
+int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
+                         int64_t* perm_out, hipStream_t st);
+int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
+                           int* newrem, int64_t* perm_out, hipStream_t st);
+int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
+                       float* d, hipStream_t st);
+int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, const int* rem,
+                          int nr, float* C, long ldc, hipStream_t st);
+size_t pt2q_ssr_scratch_floats(int n, int m);
+
+// ---- GEMM (gemm.hip)
+enum GemmMode { GEMM_STORE = 0, GEMM_ADD = 1, GEMM_SUB = 2, GEMM_CHAIN_NEG = 3 };
+enum GemmLayout { LAY_KMAJOR = 0, LAY_ROWMAJOR = 1 };
+struct GemmDesc {
+  int M, N, K;
+  const void* A;  // element (i,k): KMAJOR A[k*lda + i], ROWMAJOR A[i*lda + k]
+  long lda;
+  int a_layout;
+  const void* B;  // element (k,j): KMAJOR B[k*ldb + j], ROWMAJOR B[j*ldb + k]
+  long ldb;
+  int b_layout;
+  int in_dtype;   // PT2Q_F32 / PT2Q_F16 / PT2Q_BF16 (applies to both A and B)
+  float* C;       // C[crow(i)*ldc + j]
+  long ldc;
+  const int* crow;  // nullable output-row gather
+  int mode;
+  int upper;        // compute only tiles with tile_i <= tile_j
+  int mirror;       // with upper: also write C[j][i] (full symmetric output)
+  int kstart_diag;  // skip K below min(tile row start): exact for triangular operands (zeros)
+};
+int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
+
+// ---- misc (misc.hip)
+int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,
+                                 float* dst, long ldd, hipStream_t st);
+int pt2q_launch_transpose_i8(const int8_t* src, long lds, int rows, int cols, void* dst, int ddtype,
+                             long ldd, hipStream_t st);
+int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, float* dst, long ldd,
+                              hipStream_t st);
+int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
+                                float* H, long ldh, float* damp, hipStream_t st);
+
+// ---- Cholesky (chol.hip)
+int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
+                                 float* U, float* Ui, int* info, hipStream_t st);

@@ -1,0 +1,227 @@
+// Layout changes, Hessian damping, dequantisation, 2-bit packing and synthetic inputs.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+template <typename T>
+PT2Q_DEV float ld_f32(const T* p);
+template <>
+PT2Q_DEV float ld_f32<float>(const float* p) { return *p; }
+template <>
+PT2Q_DEV float ld_f32<_Float16>(const _Float16* p) { return (float)*p; }
+template <>
+PT2Q_DEV float ld_f32<uint16_t>(const uint16_t* p) { return __uint_as_float(((uint32_t)*p) << 16); }
+template <>
+PT2Q_DEV float ld_f32<int8_t>(const int8_t* p) { return (float)*p; }
+
+// dst[c][r] = src[r][c] through a 32x33 LDS tile (coalesced on both sides).
+template <typename TS, typename TD>
+__global__ __launch_bounds__(256) void transpose_kernel(const TS* src, long lds, int rows, int cols,
+                                                        TD* dst, long ldd) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
+  for (int y = ty; y < 32; y += 8) {
+    int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < rows && c < cols) ? (float)ld_f32<TS>(src + (long)r * lds + c) : 0.0f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    int c = c0 + y, r = r0 + tx;
+    if (c < cols && r < rows) dst[(long)c * ldd + r] = (TD)tile[tx][y];
+  }
+}
+
+__global__ void hess_scale_kernel(const float* G, long ldg, int m, float fn, float* H, long ldh) {
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long)m * m) return;
+  int r = (int)(q / m), c = (int)(q % m);
+  H[(long)r * ldh + c] = G[(long)r * ldg + c] / fn;
+}
+
+// damp = percdamp * (SUMN(diag H) / m); H_ii += damp   (main.py:132-133, gptq.py:97-98)
+__global__ __launch_bounds__(1024) void hess_damp_kernel(float* H, long ldh, int m, float percdamp,
+                                                         float* damp_out) {
+  __shared__ float dmp;
+  if (threadIdx.x < 64) {
+    float p = sumn_lane<false>(H, m, ldh + 1, threadIdx.x);
+    p = bfly64(p);
+    if (threadIdx.x == 0) {
+      dmp = percdamp * (p / (float)m);
+      if (damp_out) *damp_out = dmp;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < m; i += blockDim.x) H[(long)i * ldh + i] = H[(long)i * ldh + i] + dmp;
+}
+
+// gptq.py:213-228: out[:, perm[k*b + t]] = alpha[:,k] * T[:, col] + mu[:,k]
+template <typename TT>
+__global__ void dequant_kernel(const float* alpha, const float* mu, const TT* T,
+                               const int64_t* perm, int n, int m, int b, int B, float* out) {
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long)n * m) return;
+  int i = (int)(q / m), pos = (int)(q % m);
+  int k = pos / b;
+  long col = perm ? perm[pos] : pos;
+  float t = (float)T[(long)i * m + col];
+  out[(long)i * m + col] = alpha[(long)i * B + k] * t + mu[(long)i * B + k];
+}
+
+__global__ void pack_kernel(const int8_t* T, long count, uint8_t* out) {
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long nb = (count + 3) / 4;
+  if (q >= nb) return;
+  uint8_t v = 0;
+  for (int s = 0; s < 4; ++s) {
+    long i = 4 * q + s;
+    uint8_t c = (i < count) ? (uint8_t)(T[i] + 1) : 0;
+    v |= (uint8_t)(c << (2 * s));
+  }
+  out[q] = v;
+}
+
+__global__ void unpack_kernel(const uint8_t* in, long count, int8_t* T) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  T[i] = (int8_t)((in[i >> 2] >> (2 * (i & 3))) & 3) - 1;
+}
+
+PT2Q_DEV uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_kernel(float* out, long count, uint64_t base, float scale, long cols,
+                            int every, uint64_t obase, float oscale) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < count; i += (long)gridDim.x * blockDim.x) {
+    uint64_t h = splitmix64(base + (uint64_t)i);
+    float c = (float)((int64_t)(h >> 40) - (1ll << 23));
+    float s = scale;
+    if (every > 0) {
+      uint64_t col = (uint64_t)(i % cols);
+      if (splitmix64(obase + col) % (uint64_t)every == 0) s = oscale;
+    }
+    out[i] = c * s;
+  }
+}
+
+}  // namespace
+
+int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,
+                                 float* dst, long ldd, hipStream_t st) {
+  dim3 grid(ceil_div(cols, 32), ceil_div(rows, 32));
+  switch (dtype) {
+    case PT2Q_F32:
+      hipLaunchKernelGGL((transpose_kernel<float, float>), grid, dim3(256), 0, st,
+                         (const float*)src, lds, rows, cols, dst, ldd);
+      break;
+    case PT2Q_F16:
+      hipLaunchKernelGGL((transpose_kernel<_Float16, float>), grid, dim3(256), 0, st,
+                         (const _Float16*)src, lds, rows, cols, dst, ldd);
+      break;
+    case PT2Q_BF16:
+      hipLaunchKernelGGL((transpose_kernel<uint16_t, float>), grid, dim3(256), 0, st,
+                         (const uint16_t*)src, lds, rows, cols, dst, ldd);
+      break;
+    default:
+      return PT2Q_E_ARG;
+  }
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_transpose_i8(const int8_t* src, long lds, int rows, int cols, void* dst,
+                             int ddtype, long ldd, hipStream_t st) {
+  dim3 grid(ceil_div(cols, 32), ceil_div(rows, 32));
+  if (ddtype == PT2Q_I8)
+    hipLaunchKernelGGL((transpose_kernel<int8_t, int8_t>), grid, dim3(256), 0, st, src, lds, rows,
+                       cols, (int8_t*)dst, ldd);
+  else if (ddtype == PT2Q_F32)
+    hipLaunchKernelGGL((transpose_kernel<int8_t, float>), grid, dim3(256), 0, st, src, lds, rows,
+                       cols, (float*)dst, ldd);
+  else
+    return PT2Q_E_ARG;
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, float* dst, long ldd,
+                              hipStream_t st) {
+  return pt2q_launch_transpose_to_f32(src, PT2Q_F32, lds, rows, cols, dst, ldd, st);
+}
+
+int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
+                                float* H, long ldh, float* damp, hipStream_t st) {
+  hipLaunchKernelGGL(hess_scale_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg,
+                     m, (float)nsamples, H, ldh);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(hess_damp_kernel, dim3(1), dim3(1024), 0, st, H, ldh, m, percdamp, damp);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_dequantize(const float* alpha, const float* mu, const void* T, int tdtype,
+                               const int64_t* perm, int n, int m, int b, float* out,
+                               void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n <= 0 || m <= 0 || b <= 0 || !alpha || !mu || !T || !out) return PT2Q_E_ARG;
+  int B = (b < m) ? ceil_div(m, b) : 1;
+  int bb = (b < m) ? b : m;
+  long tot = (long)n * m;
+  if (tdtype == PT2Q_I8)
+    hipLaunchKernelGGL((dequant_kernel<int8_t>), dim3(ceil_div(tot, 256)), dim3(256), 0, st, alpha,
+                       mu, (const int8_t*)T, perm, n, m, bb, B, out);
+  else if (tdtype == PT2Q_F32)
+    hipLaunchKernelGGL((dequant_kernel<float>), dim3(ceil_div(tot, 256)), dim3(256), 0, st, alpha,
+                       mu, (const float*)T, perm, n, m, bb, B, out);
+  else
+    return PT2Q_E_ARG;
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_pack_ternary(const int8_t* T, int64_t count, uint8_t* packed, void* stream) {
+  if (count < 0 || !T || !packed) return PT2Q_E_ARG;
+  long nb = (count + 3) / 4;
+  if (nb == 0) return PT2Q_OK;
+  hipLaunchKernelGGL(pack_kernel, dim3(ceil_div(nb, 256)), dim3(256), 0, (hipStream_t)stream, T,
+                     (long)count, packed);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_unpack_ternary(const uint8_t* packed, int64_t count, int8_t* T, void* stream) {
+  if (count < 0 || !T || !packed) return PT2Q_E_ARG;
+  if (count == 0) return PT2Q_OK;
+  hipLaunchKernelGGL(unpack_kernel, dim3(ceil_div(count, 256)), dim3(256), 0, (hipStream_t)stream,
+                     packed, (long)count, T);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_fill_synthetic(float* out, int64_t count, uint64_t seed, float scale,
+                                   int64_t cols, int outlier_every, float scale_outlier,
+                                   void* stream) {
+  if (count < 0 || !out || (outlier_every > 0 && cols <= 0)) return PT2Q_E_ARG;
+  if (count == 0) return PT2Q_OK;
+  // host-side splitmix64 of the seeds (same function as device)
+  auto sm = [](uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  uint64_t base = sm(seed);
+  uint64_t obase = sm(seed ^ 0x5BD1E995ull);
+  long grid = ceil_div(count, 256);
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(fill_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, out,
+                     (long)count, base, scale, (long)cols, outlier_every, obase, scale_outlier);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}

@@ -1,0 +1,283 @@
+// SSR (structural-similarity reordering) block selection and the error-feedback coefficients.
+//
+// Reference: reorder.py:36-61 (compute_column_similarity_to_mean), reorder.py:107-143
+// (select_next_block_ssr), main.py:176-177 / gptq.py:142-150 (block operands),
+// main.py:199-209 (coefficients Hinv[blk][:,rem] / diag).
+//
+// Weights live feature-major (Wt[j] = column j of W, contiguous over the n rows), so every
+// "column" gather of the reference is a gather of whole contiguous rows here.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+constexpr int CHUNK = 128;  // canonical wbar chunk (rem entries per partial sum)
+
+// part[c][i] = sum over rem[c*128 .. c*128+127] (ascending) of Wt[rem[e]][i]
+__global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, long ldw, int n,
+                                                               const int* rem, int r,
+                                                               float* part) {
+  const int c = blockIdx.x;
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int e0 = c * CHUNK, e1 = min(r, e0 + CHUNK);
+  float p = 0.0f;
+  for (int e = e0; e < e1; ++e) p = p + Wt[(long)rem[e] * ldw + i];
+  part[(long)c * n + i] = p;
+}
+
+// wbar = (sum_c part[c]) / r ; nw = clamp(sqrt(SUMN fma wbar^2)) ; wn = wbar / nw
+__global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(const float* part, int nchunks,
+                                                              int n, int r, float* wn) {
+  extern __shared__ float lds[];  // n floats + 1
+  float* wbar = lds;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float t = 0.0f;
+    for (int c = 0; c < nchunks; ++c) t = t + part[(long)c * n + i];
+    wbar[i] = t / (float)r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float p = sumn_lane<true>(wbar, n, 1, threadIdx.x);
+    p = bfly64(p);
+    if (threadIdx.x == 0) lds[n] = clampmin(sqrtf(p));
+  }
+  __syncthreads();
+  const float nw = lds[n];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = wbar[i] / nw;
+}
+
+// One wave per remaining column: nj = clamp(sqrt(SUMN fma x^2)); s = SUMN fma (x/nj) * wn.
+__global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw, int n,
+                                                      const int* rem, int r, const float* wn,
+                                                      float* sim) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int t = threadIdx.x & 63;
+  if (e >= r) return;
+  const float* x = Wt + (long)rem[e] * ldw;
+  float ss = bfly64(sumn_lane<true>(x, n, 1, t));
+  const float nj = clampmin(sqrtf(ss));
+  float p = 0.0f;
+  for (long base = 4 * t; base < n; base += 256) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      long i = base + q;
+      if (i < n) p = fmaf(x[i] / nj, wn[i], p);
+    }
+  }
+  p = bfly64(p);
+  if (t == 0) sim[e] = p;
+}
+
+PT2Q_DEV uint32_t orderable(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Ordered top-b of r similarities: keys (value desc, position asc), bitonic sort in LDS.
+// Writes blk (selection order), newrem (ascending), perm_out (int64, nullable).
+__global__ __launch_bounds__(1024) void ssr_topk_kernel(const float* sim, const int* rem, int r,
+                                                        int b, int P, int* blk, int* newrem,
+                                                        int64_t* perm_out) {
+  extern __shared__ unsigned long long keys[];  // P keys, then r flag bytes, then scan ints
+  unsigned char* sel = (unsigned char*)(keys + P);
+  int* scan = (int*)(sel + ((r + 15) & ~15));
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int e = tid; e < P; e += nt)
+    keys[e] = (e < r) ? (((unsigned long long)orderable(sim[e]) << 32) |
+                         (unsigned long long)(0xFFFFFFFFu - (uint32_t)e))
+                      : 0ull;
+  for (int e = tid; e < r; e += nt) sel[e] = 0;
+  __syncthreads();
+  // bitonic sort, descending
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int idx = tid; idx < P / 2; idx += nt) {
+        int lo = 2 * idx - (idx & (stride - 1));
+        int hi = lo + stride;
+        bool desc = ((lo & size) == 0);
+        unsigned long long a = keys[lo], c = keys[hi];
+        if ((a < c) == desc) {
+          keys[lo] = c;
+          keys[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = tid; t < b; t += nt) {
+    int e = (int)(0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFull));
+    int j = rem[e];
+    blk[t] = j;
+    if (perm_out) perm_out[t] = j;
+    sel[e] = 1;
+  }
+  __syncthreads();
+  // stable compaction of the unselected positions (ascending)
+  const int per = (r + nt - 1) / nt;
+  const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
+  int cnt = 0;
+  for (int e = e0; e < e1; ++e) cnt += !sel[e];
+  // block exclusive scan of cnt: wave-inclusive scan by shuffles, then wave totals
+  const int lane = tid & 63, wv = tid >> 6;
+  int incl = cnt;
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) scan[wv] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int q = 0; q < (nt >> 6); ++q) {
+      int v = scan[q];
+      scan[q] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  int o = scan[wv] + incl - cnt;
+  for (int e = e0; e < e1; ++e)
+    if (!sel[e]) newrem[o++] = rem[e];
+}
+
+// Sequential block (use_ssr=False: main.py:167-169, gptq.py:135-137) or "take the rest"
+// (reorder.py:125-126 when |rem| <= b).
+__global__ void select_seq_kernel(int mode, int p0, int bs, int m, const int* rem, int* blk,
+                                  int* newrem, int64_t* perm_out) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < bs) {
+    int j = (mode == 0) ? p0 + t : rem[t];
+    blk[t] = j;
+    if (perm_out) perm_out[t] = j;
+  }
+  if (mode == 0) {
+    int nr = m - p0 - bs;
+    for (int e = t; e < nr; e += gridDim.x * blockDim.x) newrem[e] = p0 + bs + e;
+  }
+}
+
+// S1 = S·1 and d = 1ᵀS1 for the AGA of one block.
+//   src 1 (variant M): S[j][l] = A[blk_j][blk_l], A = raw Gram XᵀX (== X_bᵀX_b).
+//   src 2 (variant G): S = Hbbᵀ Hbb with Hbb = A[blk][:,blk] (k-ascending fmaf chains).
+// S1[j] = l-ascending sum; d = j-ascending sum (oracle s1_from_gram / s1_from_hess_block).
+__global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, long lda,
+                                                     const int* blk, int b, float* S1,
+                                                     float* d) {
+  extern __shared__ float sm[];
+  const int tid = threadIdx.x;
+  float* s1 = sm;  // b
+  if (src == 1) {
+    for (int j = tid; j < b; j += blockDim.x) {
+      const float* row = A + (long)(blk ? blk[j] : j) * lda;
+      float s = 0.0f;
+      for (int l = 0; l < b; ++l) s = s + row[blk ? blk[l] : l];
+      s1[j] = s;
+    }
+  } else {
+    float* hb = sm + b;          // b x (b+1)
+    float* S = hb + b * (b + 1); // b x (b+1)
+    const int ld = b + 1;
+    for (int q = tid; q < b * b; q += blockDim.x) {
+      int t = q / b, j = q % b;
+      hb[t * ld + j] = A[(long)(blk ? blk[t] : t) * lda + (blk ? blk[j] : j)];
+    }
+    __syncthreads();
+    for (int q = tid; q < b * b; q += blockDim.x) {
+      int j = q / b, l = q % b;
+      float acc = 0.0f;
+      for (int t = 0; t < b; ++t) acc = fmaf(hb[t * ld + j], hb[t * ld + l], acc);
+      S[j * ld + l] = acc;
+    }
+    __syncthreads();
+    for (int j = tid; j < b; j += blockDim.x) {
+      float s = 0.0f;
+      for (int l = 0; l < b; ++l) s = s + S[j * ld + l];
+      s1[j] = s;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < b; j += blockDim.x) S1[j] = s1[j];
+  if (tid == 0) {
+    float dd = 0.0f;
+    for (int j = 0; j < b; ++j) dd = dd + s1[j];
+    *d = dd;
+  }
+}
+
+// C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k])   (main.py:201-209)
+__global__ __launch_bounds__(256) void ef_coeff_kernel(const float* Hinv, long ldh,
+                                                       const int* blk, const int* rem, int nr,
+                                                       float* C, long ldc) {
+  const int k = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= nr) return;
+  const long rowb = (long)blk[k] * ldh;
+  const float dg = clampmin(Hinv[rowb + blk[k]]);
+  C[(long)k * ldc + e] = Hinv[rowb + rem[e]] / dg;
+}
+
+}  // namespace
+
+size_t pt2q_ssr_scratch_floats(int n, int m) {
+  // part (ceil(m/128) x n) + wn (n) + sim (m)
+  return (size_t)ceil_div(m, CHUNK) * n + (size_t)n + (size_t)m;
+}
+
+int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
+                               float* part, float* wn, float* sim, hipStream_t st) {
+  if (r <= 0 || n <= 0) return PT2Q_E_ARG;
+  if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
+  int nchunks = ceil_div(r, CHUNK);
+  hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
+                     Wt, ldw, n, rem, r, part);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), (n + 1) * sizeof(float), st,
+                     part, nchunks, n, r, wn);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ssr_sim_kernel, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r,
+                     wn, sim);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
+                         int64_t* perm_out, hipStream_t st) {
+  int P = 1;
+  while (P < r) P <<= 1;
+  size_t lds = (size_t)P * 8 + (size_t)((r + 15) & ~15) + 1024 * sizeof(int);
+  if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
+  hipLaunchKernelGGL(ssr_topk_kernel, dim3(1), dim3(1024), lds, st, sim, rem, r, b, P, blk,
+                     newrem, perm_out);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
+                           int* newrem, int64_t* perm_out, hipStream_t st) {
+  int work = (mode == 0) ? (m - p0) : bs;
+  int grid = ceil_div(work > 0 ? work : 1, 256);
+  if (grid > 64) grid = 64;
+  hipLaunchKernelGGL(select_seq_kernel, dim3(grid), dim3(256), 0, st, mode, p0, bs, m, rem, blk,
+                     newrem, perm_out);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
+                       float* d, hipStream_t st) {
+  size_t lds = (size_t)b * sizeof(float);
+  if (src == 2) lds += 2 * (size_t)b * (b + 1) * sizeof(float);
+  if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
+  hipLaunchKernelGGL(aga_s1_kernel, dim3(1), dim3(256), lds, st, src, A, lda, blk, b, S1, d);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, const int* rem,
+                          int nr, float* C, long ldc, hipStream_t st) {
+  hipLaunchKernelGGL(ef_coeff_kernel, dim3(ceil_div(nr, 256), bs), dim3(256), 0, st, Hinv, ldh,
+                     blk, rem, nr, C, ldc);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}

@@ -1,0 +1,284 @@
+"""HIP path (libpt2q via the pt2q package) vs the CPU oracle (bit-exact) and vs the reference's
+golden fixtures (codes/perm exact, scales within 1e-5).  Runs on an MI355X: `pytest -m gpu`."""
+import numpy as np
+import pytest
+import torch
+
+import synth
+from conftest import golden_names, layer_inputs, load_golden
+from oracle import oracle as orc
+from test_oracle_golden import check_scales
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def bits_equal(a, b):
+    a = np.ascontiguousarray(a, np.float32).view(np.uint32)
+    b = np.ascontiguousarray(b, np.float32).view(np.uint32)
+    # +0 and -0 compare equal (torch.equal semantics); everything else bitwise
+    z = (a & 0x7FFFFFFF) == 0
+    return np.array_equal(np.where(z, 0, a), np.where(z, 0, b))
+
+
+# ------------------------------------------------------------------ building blocks
+
+@pytest.mark.parametrize("N,m,dt", [(300, 200, torch.float32), (1024, 384, torch.float32),
+                                    (2048, 256, torch.float16), (512, 130, torch.bfloat16)])
+def test_gram_bitexact(pt2q, N, m, dt):
+    X = synth.activations(7 + m, N, m)
+    Xd = cuda(X).to(dt)
+    G = pt2q.gram(Xd)
+    ref = orc.gram(host(Xd.float()))
+    assert bits_equal(host(G), ref)
+    # accumulate (gptq.py add_batch): H = H + XᵀX
+    G2 = pt2q.gram(Xd[: N // 2], G.clone(), accumulate=True)
+    ref2 = ref.copy()
+    orc.gram_accumulate(ref2, host(Xd[: N // 2].float()))
+    assert bits_equal(host(G2), ref2)
+
+
+@pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500)])
+def test_hessian_cholesky_inverse_bitexact(pt2q, m, N):
+    X = synth.activations(11 + m, N, m)
+    G = orc.gram(X)
+    H, damp = pt2q.prepare_hessian(cuda(G), N, 0.01)
+    Hr, dr = orc.prepare_hessian(G, N, 0.01)
+    assert bits_equal(host(H), Hr) and np.float32(host(damp)[0]) == np.float32(dr)
+    Hinv, spd = pt2q.cholesky_inverse(H)
+    Hinv_r, spd_r = orc.cholesky_inverse(Hr)
+    assert spd and spd_r
+    assert bits_equal(host(Hinv), Hinv_r)
+
+
+def test_cholesky_breakdown_reports_and_falls_back(pt2q):
+    H = np.eye(80, dtype=np.float32)
+    H[37, 37] = -1.0
+    Hinv, spd = pt2q.cholesky_inverse(cuda(H))
+    assert not spd
+    np.testing.assert_allclose(host(Hinv), np.linalg.pinv(H), atol=1e-6)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_atq_stages_vs_oracle_and_reference(pt2q, seed):
+    g = load_golden(f"atq_4096x128_s{seed}")
+    W = synth.weights(int(g["wseed"]), 4096, 128)
+    X = synth.activations(int(g["xseed"]), 512, 128)
+    q = pt2q.AsymmetricTernaryQuantizer()
+    Wd = cuda(W)
+    a0, m0, T0 = q.ternary_init(Wd)
+    ra0, rm0, rT0 = orc.ternary_init(W)
+    assert bits_equal(host(a0), ra0) and bits_equal(host(m0), rm0) and np.array_equal(host(T0), rT0)
+    np.testing.assert_array_equal(host(T0).astype(np.int8), g["T_init"])
+    a1, m1, T1 = q.iterative_ternary_fitting(Wd, a0, m0, T0)
+    ra1, rm1, rT1, rit = orc.iterative_ternary_fitting(W, ra0, rm0, rT0)
+    assert bits_equal(host(a1), ra1) and bits_equal(host(m1), rm1) and np.array_equal(host(T1), rT1)
+    assert int(q.last_itf_iters.item()) == rit
+    np.testing.assert_array_equal(host(T1).astype(np.int8), g["T_itf"])
+    check_scales(host(a1).ravel(), g["a_itf"], "a_itf")
+    ga, gm = q.build_optimal_grid(Wd, T1)
+    rga, rgm = orc.build_optimal_grid(W, rT1)
+    assert bits_equal(host(ga), rga) and bits_equal(host(gm), rgm)
+    Tr = q.flexible_round(Wd, ga, gm)
+    assert np.array_equal(host(Tr), orc.flexible_round(W, rga, rgm))
+    a2, m2 = q.activation_aware_grid_alignment(Wd, T1, cuda(X))
+    ra2, rm2 = orc.activation_aware_grid_alignment(W, rT1, X)
+    assert bits_equal(host(a2), ra2) and bits_equal(host(m2), rm2)
+    check_scales(host(a2).ravel(), g["a_aga"], "a_aga")
+    af, mf, Tf = q.quantize(Wd, cuda(X))
+    raf, rmf, rTf, _ = orc.atq_quantize(W, X)
+    assert bits_equal(host(af), raf) and bits_equal(host(mf), rmf) and np.array_equal(host(Tf), rTf)
+
+
+def test_atq_edges_vs_reference(pt2q):
+    g = load_golden("atq_edges")
+    q = pt2q.AsymmetricTernaryQuantizer()
+    Z = torch.zeros(64, 128, device=DEV)
+    a, m, T = q.quantize(Z)
+    np.testing.assert_array_equal(host(T).astype(np.int8), g["zero_T"])
+    np.testing.assert_array_equal(host(a).ravel(), g["zero_alpha"])
+    np.testing.assert_array_equal(host(m).ravel(), g["zero_mu"])
+    assert int(q.last_itf_iters.item()) == 0
+    a, m, T = q.quantize(Z, cuda(synth.activations(220, 64, 128)))
+    np.testing.assert_array_equal(host(T).astype(np.int8), g["zerox_T"])
+    np.testing.assert_array_equal(host(a).ravel(), g["zerox_alpha"])
+    Wc = g["const_W"]
+    a, m, T = q.quantize(cuda(Wc))
+    np.testing.assert_array_equal(host(T).astype(np.int8), g["const_T"])
+    ra, rm, rT, _ = orc.atq_quantize(Wc)
+    assert bits_equal(host(a), ra) and bits_equal(host(m), rm)
+    Wr = synth.weights(130, 32, 128)
+    T = q.flexible_round(cuda(Wr), cuda(g["round_alpha"]), cuda(g["round_mu"]))
+    np.testing.assert_array_equal(host(T).astype(np.int8), g["round_T"])
+
+
+def test_atq_wide_block_vs_oracle(pt2q):
+    """b = 512 (the widest register-resident block; per-channel runs use the same kernel)."""
+    W = synth.weights(110, 256, 512)
+    X = synth.activations(210, 300, 512)
+    q = pt2q.AsymmetricTernaryQuantizer()
+    a, m, T = q.quantize(cuda(W), cuda(X))
+    ra, rm, rT, _ = orc.atq_quantize(W, X)
+    assert bits_equal(host(a), ra) and bits_equal(host(m), rm) and np.array_equal(host(T), rT)
+
+
+@pytest.mark.parametrize("name", ["ssr_4096x4096", "ssr_1024x1000_subset"])
+def test_ssr_vs_oracle_and_reference(pt2q, name):
+    g = load_golden(name)
+    n, m = int(g["n"]), int(g["m"])
+    W = synth.weights(int(g["wseed"]), n, m)
+    rem = g["rem"] if "rem" in g else np.arange(m, dtype=np.int64)
+    Wd = cuda(W)
+    sim = pt2q.compute_column_similarity_to_mean(Wd, cuda(rem))
+    assert bits_equal(host(sim), orc.ssr_similarity(W, rem))
+    blk, newrem = pt2q.select_next_block_ssr(Wd, cuda(rem), 128)
+    np.testing.assert_array_equal(host(blk), g["blk"])
+    np.testing.assert_array_equal(host(newrem), g["newrem"])
+
+
+def test_fill_synthetic_matches_numpy(pt2q):
+    a = pt2q.fill_synthetic((300, 257), 1234, std=0.02)
+    np.testing.assert_array_equal(host(a), synth.weights(1234, 300, 257))
+    b = pt2q.fill_synthetic((64, 1000), 99, std=1.0, outliers=True)
+    np.testing.assert_array_equal(host(b), synth.activations(99, 64, 1000))
+
+
+def test_pack_unpack_matches_reference_layout(pt2q):
+    T = (synth.centered24(5, 1001).astype(np.int64) % 3 - 1).astype(np.int8)
+    packed, shape = pt2q.pack_ternary(cuda(T))
+    # utils.py:202-217 layout: {-1,0,1} -> {0,1,2}, element 4q+s at bits 2s of byte q
+    flat = np.concatenate([T + 1, np.zeros((-len(T)) % 4, np.int8)]).astype(np.uint8).reshape(-1, 4)
+    want = flat[:, 0] | (flat[:, 1] << 2) | (flat[:, 2] << 4) | (flat[:, 3] << 6)
+    np.testing.assert_array_equal(host(packed), want)
+    np.testing.assert_array_equal(host(pt2q.unpack_ternary(packed, shape)), T)
+
+
+# ------------------------------------------------------------------ whole layers
+
+def _oracle_m(W, X, bs, ssr, percdamp=0.01):
+    return orc.quantize_layer_m(W, X, block_size=bs, use_ssr=ssr, percdamp=percdamp)
+
+
+def _assert_layer_bitexact(out, ref):
+    np.testing.assert_array_equal(host(out.perm), ref["perm"])
+    np.testing.assert_array_equal(host(out.T), ref["T"])
+    assert bits_equal(host(out.alpha), ref["alpha"])
+    assert bits_equal(host(out.mu), ref["mu"])
+    np.testing.assert_array_equal(host(out.iters), ref["iters"])
+
+
+@pytest.mark.parametrize("name", [n for n in golden_names("layer_m_") if n != "layer_m_notspd"])
+def test_layer_m_vs_reference_and_oracle(pt2q, name):
+    g = load_golden(name)
+    W, X = layer_inputs(g)
+    bs, ssr = int(g["block_size"]), bool(g["use_ssr"])
+    out = pt2q.quantize_layer(cuda(W), cuda(X), block_size=bs, use_ssr=ssr)
+    assert out.spd
+    _assert_layer_bitexact(out, _oracle_m(W, X, bs, ssr))
+    np.testing.assert_array_equal(host(out.perm), g["perm"])
+    np.testing.assert_array_equal(host(out.T), g["T"])
+    check_scales(host(out.alpha), g["alpha"], "alpha")
+
+
+def test_pt2llm_quantizer_surface(pt2q):
+    """main.py:102-230 call shape: nn.Linear + 3-D activations -> CPU dict."""
+    g = load_golden("layer_m_c1_ssr")
+    W, X = layer_inputs(g)
+    lin = torch.nn.Linear(W.shape[1], W.shape[0], bias=False)
+    lin.weight.data = torch.from_numpy(W.copy())
+    q = pt2q.PT2LLMQuantizer(model=None, tokenizer=None, device="cuda")
+    res = q.quantize_layer(lin, "layer_0.q_proj", torch.from_numpy(X.reshape(2, -1, X.shape[1])))
+    assert set(res) == {"alpha", "mu", "T", "perm"}
+    assert res["T"].dtype == torch.int8 and res["perm"].dtype == torch.int64
+    assert res["T"].device.type == "cpu"
+    np.testing.assert_array_equal(res["T"].numpy(), g["T"])
+    np.testing.assert_array_equal(res["perm"].numpy(), g["perm"])
+
+
+@pytest.mark.parametrize("name", golden_names("layer_g_"))
+def test_layer_g_vs_reference_and_oracle(pt2q, name):
+    g = load_golden(name)
+    W, X = layer_inputs(g)
+    m = W.shape[1]
+    lin = torch.nn.Linear(m, W.shape[0], bias=False).to(DEV)
+    lin.weight.data = cuda(W)
+    gq = pt2q.GPTQ(lin, int(g["block_size"]), 0.01)
+    for c in np.array_split(X, int(g["nbatch"])):
+        gq.add_batch(cuda(c))
+    alpha, mu, T, perm = gq.quantize(use_ssr=bool(g["use_ssr"]))
+    Hs = np.zeros((m, m), np.float32)
+    for c in np.array_split(X, int(g["nbatch"])):
+        orc.gram_accumulate(Hs, c)
+    ref = orc.quantize_layer_g(W, Hs, X.shape[0], block_size=int(g["block_size"]),
+                               use_ssr=bool(g["use_ssr"]))
+    np.testing.assert_array_equal(host(perm), ref["perm"])
+    np.testing.assert_array_equal(host(T), ref["T"])
+    assert bits_equal(host(alpha), ref["alpha"]) and bits_equal(host(mu), ref["mu"])
+    np.testing.assert_array_equal(host(T).astype(np.int8), g["T"])
+    np.testing.assert_array_equal(host(perm), g["perm"])
+    # gptq.py:201-230 reconstruction
+    Wq = gq.get_quantized_weight()
+    bs = int(g["block_size"])
+    want = np.empty_like(W)
+    for k in range(ref["alpha"].shape[1]):
+        cols = ref["perm"][k * bs:(k + 1) * bs]
+        want[:, cols] = ref["alpha"][:, k:k + 1] * ref["T"][:, cols] + ref["mu"][:, k:k + 1]
+    assert bits_equal(host(Wq), want)
+
+
+def test_layer_not_spd_pinv_fallback(pt2q):
+    g = load_golden("layer_m_notspd")
+    W, X = layer_inputs(g)
+    out = pt2q.quantize_layer(cuda(W), cuda(X), block_size=128, use_ssr=True,
+                              percdamp=float(g["percdamp"]))
+    assert not out.spd
+    np.testing.assert_array_equal(host(out.perm), g["perm"])
+    b0 = g["perm"][:128]
+    np.testing.assert_array_equal(host(out.T)[:, b0], g["T"][:, b0])
+
+
+@pytest.mark.parametrize("n,m,N,ssr,bs", [
+    (1024, 1024, 2048, True, 128),
+    (768, 3072, 512, True, 128),     # GPT-2 mlp.c_proj shape, 24 blocks
+    (2304, 768, 1024, False, 128),   # GPT-2 c_attn shape, sequential blocks
+    (640, 1000, 700, True, 256),     # ragged m, wider blocks
+])
+def test_layer_m_bitexact_larger(pt2q, n, m, N, ssr, bs):
+    W = synth.weights(1000 + n, n, m)
+    X = synth.activations(2000 + m, N, m)
+    out = pt2q.quantize_layer(cuda(W), cuda(X), block_size=bs, use_ssr=ssr)
+    _assert_layer_bitexact(out, _oracle_m(W, X, bs, ssr))
+
+
+def test_layer_m_fp16_inputs_equal_upcast(pt2q):
+    """fp16 layer + activations (configs C3/C4): the engine computes on the exact fp32 upcast."""
+    W = synth.weights(31, 512, 640)
+    X = synth.activations(32, 1024, 640)
+    Wh, Xh = cuda(W).half(), cuda(X).half()
+    out = pt2q.quantize_layer(Wh, Xh)
+    ref = _oracle_m(host(Wh.float()), host(Xh.float()), 128, True)
+    _assert_layer_bitexact(out, ref)
+
+
+def test_layer_headline_shape_bitexact(pt2q):
+    """Llama-2-7B q_proj shape (4096x4096, 32 blocks), N=2048: GPU == oracle bit-for-bit."""
+    orc.set_threads(16)
+    W = synth.weights(4096, 4096, 4096)
+    X = synth.activations(4097, 2048, 4096)
+    out = pt2q.quantize_layer(cuda(W), cuda(X))
+    ref = _oracle_m(W, X, 128, True)
+    _assert_layer_bitexact(out, ref)
+    # size-independent properties
+    p = host(out.perm)
+    assert np.array_equal(np.sort(p), np.arange(4096))
+    T = host(out.T)
+    assert set(np.unique(T)) <= {-1, 0, 1}
