@@ -9,8 +9,12 @@
 // oracle's sequential fmaf chains bit-for-bit.  Zero-padding K is an exact no-op (the chain
 // never holds -0 when it starts from +0).
 //
-// Tile: BM x BN x 16, 256 threads = 4 waves in a 2x2 grid, each wave (BM/2)x(BN/2) as
-// 32x32 MFMA sub-tiles; LDS double-buffered with register prefetch of the next K-tile.
+// Tile: BM x BN x 32, 256 threads = 4 waves in a 2x2 grid, each wave (BM/2)x(BN/2) as 32x32
+// MFMA sub-tiles.  Operands stream global -> registers (16-byte vector loads, fp16/bf16
+// converted to fp32 on the way) -> LDS [k][d] (double-buffered); the next K-tile's loads are
+// issued before the current tile's MFMAs so their latency hides under the MFMA work.
+#include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -19,7 +23,9 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int BK = 16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int BK = 32;
+constexpr int PAD = 4;
 
 template <typename T>
 PT2Q_DEV float to_f32(T v);
@@ -30,51 +36,102 @@ PT2Q_DEV float to_f32<_Float16>(_Float16 v) { return (float)v; }
 template <>
 PT2Q_DEV float to_f32<uint16_t>(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-// Loads a BK x BDIM tile of a matrix into registers (as f32) and writes it to LDS as
-// lds[k][d] (k-major).  KMAJOR: element (d,k) at base[k*ld + d]; ROWMAJOR: base[d*ld + k].
-template <typename TIn, int BDIM>
+// Raw 16-byte vector of TIn kept in registers between the load and the LDS store, so the
+// load's latency overlaps the MFMA work of the current K-tile (no wait at the load site).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename TIn>
+PT2Q_DEV void unpack16(u32x4 raw, float* out) {
+  if constexpr (sizeof(TIn) == 4) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = __uint_as_float(raw[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      uint16_t u = (uint16_t)(raw[e >> 1] >> (16 * (e & 1)));
+      TIn t;
+      __builtin_memcpy(&t, &u, 2);
+      out[e] = to_f32<TIn>(t);
+    }
+  }
+}
+
+// Loads a BK x BDIM tile (element (d, k)) into registers, then stores it to lds[k][d].
+//   KMAJOR: element (d,k) at base[k*ld + d]   (vectors run along d)
+//   ROWMAJOR: element (d,k) at base[d*ld + k] (vectors run along k)
+// VEC requires 16-byte aligned rows and the vector dimension to be a multiple of the vector
+// width (checked at launch), so a vector is either wholly inside or wholly outside the matrix;
+// outside vectors load from the (valid) base address and are zeroed at store time.
+template <typename TIn, int BDIM, bool VEC>
 struct TileLoader {
-  static constexpr int ELEMS = BK * BDIM / 256;  // per thread
-  float v[ELEMS];
+  static constexpr int VW = VEC ? 16 / (int)sizeof(TIn) : 1;
+  static constexpr int NV = BK * BDIM / VW / 256;  // vectors per thread
+  static_assert(NV >= 1, "tile too small");
+  u32x4 raw[VEC ? NV : 1];
+  bool ok[NV];
+  float v[VEC ? 1 : NV];
+
+  PT2Q_DEV void coords(int q, int layout, int& d, int& k) const {
+    if (layout == LAY_KMAJOR) {
+      k = q / (BDIM / VW);
+      d = (q % (BDIM / VW)) * VW;
+    } else {
+      d = q / (BK / VW);
+      k = (q % (BK / VW)) * VW;
+    }
+  }
+
   PT2Q_DEV void load(const TIn* base, long ld, int layout, int d0, int k0, int DMAX, int KMAX) {
     const int tid = threadIdx.x;
-    if (layout == LAY_KMAJOR) {
-      // thread -> (k, d): consecutive threads along d
 #pragma unroll
-      for (int e = 0; e < ELEMS; ++e) {
-        int q = tid + e * 256;
-        int k = q / BDIM, d = q % BDIM;
-        int gk = k0 + k, gd = d0 + d;
-        v[e] = (gk < KMAX && gd < DMAX) ? to_f32<TIn>(base[(long)gk * ld + gd]) : 0.0f;
-      }
-    } else {
-      // thread -> (d, k): consecutive threads along k
-#pragma unroll
-      for (int e = 0; e < ELEMS; ++e) {
-        int q = tid + e * 256;
-        int d = q / BK, k = q % BK;
-        int gk = k0 + k, gd = d0 + d;
-        v[e] = (gk < KMAX && gd < DMAX) ? to_f32<TIn>(base[(long)gd * ld + gk]) : 0.0f;
+    for (int e = 0; e < NV; ++e) {
+      int d, k;
+      coords(tid + e * 256, layout, d, k);
+      const int gd = d0 + d, gk = k0 + k;
+      ok[e] = gk < KMAX && gd < DMAX;
+      const long off = (layout == LAY_KMAJOR) ? (long)gk * ld + gd : (long)gd * ld + gk;
+      const TIn* p = base + (ok[e] ? off : 0);
+      if constexpr (VEC) {
+        raw[e] = *(const u32x4*)p;
+      } else {
+        float x = to_f32<TIn>(*p);
+        v[e] = ok[e] ? x : 0.0f;
       }
     }
   }
-  PT2Q_DEV void store(float (*lds)[BDIM + 4], int layout) {
+
+  PT2Q_DEV void store(float (*lds)[BDIM + PAD], int layout) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int e = 0; e < ELEMS; ++e) {
-      int q = tid + e * 256;
-      if (layout == LAY_KMAJOR)
-        lds[q / BDIM][q % BDIM] = v[e];
-      else
-        lds[q % BK][q / BK] = v[e];
+    for (int e = 0; e < NV; ++e) {
+      int d, k;
+      coords(tid + e * 256, layout, d, k);
+      if constexpr (VEC) {
+        float f[VW];
+        unpack16<TIn>(raw[e], f);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) f[w] = ok[e] ? f[w] : 0.0f;
+        if (layout == LAY_KMAJOR) {
+#pragma unroll
+          for (int w = 0; w < VW; w += 4) {
+            f32x4 x = {f[w], f[w + 1], f[w + 2], f[w + 3]};
+            *(f32x4*)&lds[k][d + w] = x;
+          }
+        } else {
+#pragma unroll
+          for (int w = 0; w < VW; ++w) lds[k + w][d] = f[w];
+        }
+      } else {
+        lds[k][d] = v[e];
+      }
     }
   }
 };
 
-template <int BM, int BN, typename TIn>
+template <int BM, int BN, typename TIn, bool VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
-  __shared__ float As[2][BK][BM + 4];
-  __shared__ float Bs[2][BK][BN + 4];
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
   constexpr int RM = BM / 64, RN = BN / 64;
 
   int ti, tj;
@@ -104,16 +161,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
     for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float c0 = 0.0f;
+        acc[rm][rn][r] = 0.0f;
         if (g.mode == GEMM_CHAIN_NEG) {
           int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
           int col = j0 + wc * (BN / 2) + rn * 32 + li;
-          if (row < g.M && col < g.N) {
-            long crow = g.crow ? g.crow[row] : row;
-            c0 = g.C[crow * g.ldc + col];
-          }
+          bool in = row < g.M && col < g.N;
+          long crow = g.crow ? g.crow[in ? row : 0] : row;
+          float c0 = g.C[in ? crow * g.ldc + col : 0];
+          acc[rm][rn][r] = in ? c0 : 0.0f;
         }
-        acc[rm][rn][r] = c0;
       }
 
   int kbeg = 0;
@@ -123,8 +179,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
   const TIn* Bb = (const TIn*)g.B;
   const float sgn = (g.mode == GEMM_CHAIN_NEG) ? -1.0f : 1.0f;
 
-  TileLoader<TIn, BM> la;
-  TileLoader<TIn, BN> lb;
+  TileLoader<TIn, BM, VEC> la;
+  TileLoader<TIn, BN, VEC> lb;
   if (kbeg < g.K) {
     la.load(Ab, g.lda, g.a_layout, i0, kbeg, g.M, g.K);
     lb.load(Bb, g.ldb, g.b_layout, j0, kbeg, g.N, g.K);
@@ -191,17 +247,40 @@ int launch_t(const GemmDesc& g, hipStream_t st) {
     ntiles = (long)tm * tn;
   }
   if (ntiles <= 0) return PT2Q_OK;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn>), dim3((unsigned)ntiles), dim3(256), 0, st, g, tm,
-                     tn);
+  const int vw = 16 / (int)sizeof(TIn);
+  auto ok_vec = [&](const void* p, long ld, int layout, int dim) {
+    int vdim = (layout == LAY_KMAJOR) ? dim : g.K;
+    return ((uintptr_t)p % 16 == 0) && (ld % vw == 0) && (vdim % vw == 0);
+  };
+  const bool vec = ok_vec(g.A, g.lda, g.a_layout, g.M) && ok_vec(g.B, g.ldb, g.b_layout, g.N);
+  if (vec)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, true>), dim3((unsigned)ntiles), dim3(256), 0, st, g,
+                       tm, tn);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, false>), dim3((unsigned)ntiles), dim3(256), 0, st,
+                       g, tm, tn);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
 
+// Pick the tile so that the grid balances over the 256 CUs: every workgroup carries the same
+// work, so the makespan is ceil(tiles / slots); prefer 128x128 (higher operand reuse) unless
+// 64x64 packs the chip clearly better.
 template <typename TIn>
 int launch_dt(const GemmDesc& g, hipStream_t st) {
-  // small problems: 64x64 tiles for more workgroups
-  long big = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128);
-  if (big >= 256) return launch_t<128, 128, TIn>(g, st);
+  auto count = [&](int t) -> long {
+    long tm = ceil_div(g.M, t), tn = ceil_div(g.N, t);
+    return g.upper ? tm * (tm + 1) / 2 : tm * tn;
+  };
+  const double slots = 256.0;
+  long c128 = count(128), c64 = count(64);
+  static const char* force = std::getenv("PT2Q_GEMM_TILE");
+  if (force && force[0] == '1') return launch_t<128, 128, TIn>(g, st);
+  if (force && force[0] == '6') return launch_t<64, 64, TIn>(g, st);
+  // efficiency = useful tiles / (rounds * slots); 64x64 tiles cost 1/4 of a 128x128 tile
+  double r128 = std::ceil(c128 / slots), r64 = std::ceil(c64 / slots);
+  double t128 = r128 * 4.0, t64 = r64 * 1.0 * 1.15;  // 64x64: ~15% lower per-tile efficiency
+  if (c128 >= 64 && t128 <= t64) return launch_t<128, 128, TIn>(g, st);
   return launch_t<64, 64, TIn>(g, st);
 }
 
