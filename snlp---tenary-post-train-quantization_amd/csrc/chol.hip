@@ -50,6 +50,33 @@ __global__ __launch_bounds__(1024) void chol_diag_kernel(float* A, long lda, int
   }
 }
 
+// The same factorisation in ONE wave with no barriers: lane c keeps column c of the block in
+// registers (col[r] = D[r][c]); row k is broadcast lane-to-lane with readlane.  The entries
+// below the diagonal are scratch (never written back).  Padding (nb < NB) is an identity block.
+__global__ __launch_bounds__(64) void chol_diag_wave_kernel(float* A, long lda, int p0, int nb,
+                                                            int* info) {
+  const int c = threadIdx.x;
+  float col[NB];
+#pragma unroll
+  for (int r = 0; r < NB; ++r)
+    col[r] = (r < nb && c < nb) ? A[(long)(p0 + r) * lda + p0 + c] : ((r == c) ? 1.0f : 0.0f);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[k]), k));
+    if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
+    const float ukk = sqrtf(dkk);
+    col[k] = (c == k) ? ukk : ((c > k) ? col[k] / ukk : col[k]);
+#pragma unroll
+    for (int r = k + 1; r < NB; ++r) {
+      const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[k]), r));
+      col[r] = fmaf(-s, col[k], col[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NB; ++r)
+    if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[r];
+}
+
 // Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution with the factored
 // diagonal block (chains continue from the already-updated A values).
 __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int p0, int nb,
@@ -131,7 +158,7 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   int rc;
   for (int p0 = 0; p0 < m; p0 += NB) {
     int nb = (m - p0 < NB) ? m - p0 : NB;
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(1024), 0, st, U, ld, p0, nb, info);
+    hipLaunchKernelGGL(chol_diag_wave_kernel, dim3(1), dim3(64), 0, st, U, ld, p0, nb, info);
     PT2Q_LAUNCH_CHECK();
     int rest = m - p0 - nb;
     if (rest <= 0) break;
@@ -147,23 +174,25 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
     if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
   }
-  // Uinv = U^-1 by column blocks
+  // Uinv = U^-1 by column blocks, right-looking: Ui[k][i] holds the running chain of every
+  // not-yet-final column; after block J is final, one CHAIN GEMM extends the chains of all
+  // later columns by the terms j in J (ascending), so each element keeps its canonical order.
   if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
   for (int c0 = 0; c0 < m; c0 += NB) {
     int nb = (m - c0 < NB) ? m - c0 : NB;
-    if (c0 > 0) {
-      GemmDesc g{};
-      g.M = c0; g.N = nb; g.K = c0;
-      g.A = Ui; g.lda = ld; g.a_layout = LAY_ROWMAJOR;      // (k, j) = Ui[k][j]
-      g.B = U + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;     // (j, i) = U[j][c0+i]
-      g.in_dtype = PT2Q_F32;
-      g.C = Ui + c0; g.ldc = ld;
-      g.mode = GEMM_STORE; g.kstart_diag = 1;
-      if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
-    }
     hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div(c0 + nb, 256)), dim3(256), 0, st, U, ld,
                        Ui, ld, c0, nb);
     PT2Q_LAUNCH_CHECK();
+    int rest = m - c0 - nb;
+    if (rest <= 0) break;
+    GemmDesc g{};
+    g.M = c0 + nb; g.N = rest; g.K = nb;
+    g.A = Ui + c0; g.lda = ld; g.a_layout = LAY_ROWMAJOR;            // (k, j) = Ui[k][c0+j]
+    g.B = U + (long)c0 * ld + c0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;  // (j, i) = U[c0+j][c0+nb+i]
+    g.in_dtype = PT2Q_F32;
+    g.C = Ui + c0 + nb; g.ldc = ld;
+    g.mode = GEMM_CHAIN_POS;
+    if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
   }
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
   GemmDesc g{};

@@ -160,17 +160,31 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
 #pragma unroll
     for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        acc[rm][rn][r] = 0.0f;
-        if (g.mode == GEMM_CHAIN_NEG) {
+      for (int r = 0; r < 16; ++r) acc[rm][rn][r] = 0.0f;
+  if (g.mode == GEMM_CHAIN_NEG || g.mode == GEMM_CHAIN_POS) {
+    // chains continue from C (no output-row gather in this mode); all loads issued before use
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
           int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
           int col = j0 + wc * (BN / 2) + rn * 32 + li;
           bool in = row < g.M && col < g.N;
-          long crow = g.crow ? g.crow[in ? row : 0] : row;
-          float c0 = g.C[in ? crow * g.ldc + col : 0];
-          acc[rm][rn][r] = in ? c0 : 0.0f;
+          acc[rm][rn][r] = g.C[in ? (long)row * g.ldc + col : 0];
         }
-      }
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          int col = j0 + wc * (BN / 2) + rn * 32 + li;
+          if (!(row < g.M && col < g.N)) acc[rm][rn][r] = 0.0f;
+        }
+  }
 
   int kbeg = 0;
   if (g.kstart_diag == 1) kbeg = i0 - (i0 % BK);

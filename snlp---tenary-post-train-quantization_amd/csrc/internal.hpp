@@ -23,7 +23,7 @@ int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, c
 size_t pt2q_ssr_scratch_floats(int n, int m);
 
 // ---- GEMM (gemm.hip)
-enum GemmMode { GEMM_STORE = 0, GEMM_ADD = 1, GEMM_SUB = 2, GEMM_CHAIN_NEG = 3 };
+enum GemmMode { GEMM_STORE = 0, GEMM_ADD = 1, GEMM_SUB = 2, GEMM_CHAIN_NEG = 3, GEMM_CHAIN_POS = 4 };
 enum GemmLayout { LAY_KMAJOR = 0, LAY_ROWMAJOR = 1 };
 struct GemmDesc {
   int M, N, K;

@@ -17,34 +17,47 @@ constexpr int CHUNK = 128;  // canonical wbar chunk (rem entries per partial sum
 __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, long ldw, int n,
                                                                const int* rem, int r,
                                                                float* part) {
+  __shared__ long rows[CHUNK];
   const int c = blockIdx.x;
+  const int e0 = c * CHUNK, cnt = min(r, e0 + CHUNK) - e0;
+  for (int e = threadIdx.x; e < cnt; e += blockDim.x) rows[e] = (long)rem[e0 + e] * ldw;
+  __syncthreads();
   const int i = blockIdx.y * 256 + threadIdx.x;
   if (i >= n) return;
-  const int e0 = c * CHUNK, e1 = min(r, e0 + CHUNK);
   float p = 0.0f;
-  for (int e = e0; e < e1; ++e) p = p + Wt[(long)rem[e] * ldw + i];
+  int e = 0;
+  for (; e + 8 <= cnt; e += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = Wt[rows[e + u] + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p = p + v[u];
+  }
+  for (; e < cnt; ++e) p = p + Wt[rows[e] + i];
   part[(long)c * n + i] = p;
 }
 
-// wbar = (sum_c part[c]) / r ; nw = clamp(sqrt(SUMN fma wbar^2)) ; wn = wbar / nw
-__global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(const float* part, int nchunks,
-                                                              int n, int r, float* wn) {
-  extern __shared__ float lds[];  // n floats + 1
-  float* wbar = lds;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    float t = 0.0f;
-    for (int c = 0; c < nchunks; ++c) t = t + part[(long)c * n + i];
-    wbar[i] = t / (float)r;
-  }
-  __syncthreads();
+// wbar[i] = (chunk partials summed in chunk order) / r
+__global__ __launch_bounds__(256) void ssr_wbar_sum_kernel(const float* part, int nchunks, int n,
+                                                           int r, float* wbar) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float t = 0.0f;
+  for (int c = 0; c < nchunks; ++c) t = t + part[(long)c * n + i];
+  wbar[i] = t / (float)r;
+}
+
+// nw = clamp(sqrt(SUMN fma wbar^2)) ; wn = wbar / nw   (in place)
+__global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) {
+  __shared__ float nws;
   if (threadIdx.x < 64) {
-    float p = sumn_lane<true>(wbar, n, 1, threadIdx.x);
+    float p = sumn_lane<true>(wn, n, 1, threadIdx.x);
     p = bfly64(p);
-    if (threadIdx.x == 0) lds[n] = clampmin(sqrtf(p));
+    if (threadIdx.x == 0) nws = clampmin(sqrtf(p));
   }
   __syncthreads();
-  const float nw = lds[n];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = wbar[i] / nw;
+  const float nw = nws;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = wn[i] / nw;
 }
 
 // One wave per remaining column: nj = clamp(sqrt(SUMN fma x^2)); s = SUMN fma (x/nj) * wn.
@@ -167,11 +180,39 @@ __global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, lo
   extern __shared__ float sm[];
   const int tid = threadIdx.x;
   float* s1 = sm;  // b
-  if (src == 1) {
+  if (src == 1 && b <= 128) {
+    // gather the b x b sub-block cooperatively (independent loads), then row sums in order
+    float* gb = sm + b;  // b x (b+1)
+    int* idx = (int*)(gb + b * (b + 1));
+    const int ld = b + 1;
+    for (int j = tid; j < b; j += blockDim.x) idx[j] = blk ? blk[j] : j;
+    __syncthreads();
+    for (int q = tid; q < b * b; q += blockDim.x) {
+      int j = q / b, l = q % b;
+      gb[j * ld + l] = A[(long)idx[j] * lda + idx[l]];
+    }
+    __syncthreads();
     for (int j = tid; j < b; j += blockDim.x) {
-      const float* row = A + (long)(blk ? blk[j] : j) * lda;
       float s = 0.0f;
-      for (int l = 0; l < b; ++l) s = s + row[blk ? blk[l] : l];
+      for (int l = 0; l < b; ++l) s = s + gb[j * ld + l];
+      s1[j] = s;
+    }
+  } else if (src == 1) {
+    int* idx = (int*)(sm + b);
+    for (int j = tid; j < b; j += blockDim.x) idx[j] = blk ? blk[j] : j;
+    __syncthreads();
+    for (int j = tid; j < b; j += blockDim.x) {
+      const float* row = A + (long)idx[j] * lda;
+      float s = 0.0f;
+      int l = 0;
+      for (; l + 8 <= b; l += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = row[idx[l + u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = s + v[u];
+      }
+      for (; l < b; ++l) s = s + row[idx[l]];
       s1[j] = s;
     }
   } else {
@@ -232,8 +273,10 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
                      Wt, ldw, n, rem, r, part);
   PT2Q_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), (n + 1) * sizeof(float), st,
-                     part, nchunks, n, r, wn);
+  hipLaunchKernelGGL(ssr_wbar_sum_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, nchunks,
+                     n, r, wn);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), 0, st, wn, n);
   PT2Q_LAUNCH_CHECK();
   hipLaunchKernelGGL(ssr_sim_kernel, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r,
                      wn, sim);
@@ -268,6 +311,8 @@ int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b,
                        float* d, hipStream_t st) {
   size_t lds = (size_t)b * sizeof(float);
   if (src == 2) lds += 2 * (size_t)b * (b + 1) * sizeof(float);
+  else if (b <= 128) lds += (size_t)b * (b + 1) * sizeof(float) + (size_t)b * sizeof(int);
+  else lds += (size_t)b * sizeof(int);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   hipLaunchKernelGGL(aga_s1_kernel, dim3(1), dim3(256), lds, st, src, A, lda, blk, b, S1, d);
   PT2Q_LAUNCH_CHECK();
