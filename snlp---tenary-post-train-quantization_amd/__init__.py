@@ -13,7 +13,7 @@ from .quantizer import AsymmetricTernaryQuantizer, compute_output_error, compute
 from .reorder import compute_column_similarity_to_mean, select_next_block_ssr
 from .gptq import GPTQ, GPTQQuantizer
 from .pt2llm import PT2LLMQuantizer
-from .engine import (LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
+from .engine import (LayerGraph, LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
                      gram, pack_ternary, prepare_hessian, quantize_blocks, quantize_layer,
                      unpack_ternary)
 
@@ -21,7 +21,7 @@ __version__ = "0.1.0"
 __all__ = [
     "AsymmetricTernaryQuantizer", "compute_quantization_error", "compute_output_error",
     "compute_column_similarity_to_mean", "select_next_block_ssr", "GPTQ", "GPTQQuantizer",
-    "PT2LLMQuantizer", "LayerOutput", "LayerWorkspace", "gram", "prepare_hessian",
+    "PT2LLMQuantizer", "LayerGraph", "LayerOutput", "LayerWorkspace", "gram", "prepare_hessian",
     "cholesky_inverse", "quantize_blocks", "quantize_layer", "dequantize", "pack_ternary",
     "unpack_ternary", "fill_synthetic",
 ]

@@ -17,44 +17,13 @@ namespace {
 
 constexpr int NB = 64;
 
-// Factor the nb x nb diagonal block at (p0, p0) in place (upper triangle), right-looking.
-__global__ __launch_bounds__(1024) void chol_diag_kernel(float* A, long lda, int p0, int nb,
-                                                         int* info) {
-  __shared__ float D[NB][NB + 1];
-  const int tid = threadIdx.x;
-  for (int q = tid; q < nb * nb; q += blockDim.x) {
-    int r = q / nb, c = q % nb;
-    D[r][c] = A[(long)(p0 + r) * lda + p0 + c];
-  }
-  __syncthreads();
-  for (int k = 0; k < nb; ++k) {
-    if (tid == 0) {
-      float akk = D[k][k];
-      if (!(akk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
-      D[k][k] = sqrtf(akk);
-    }
-    __syncthreads();
-    const float ukk = D[k][k];
-    for (int i = k + 1 + tid; i < nb; i += blockDim.x) D[k][i] = D[k][i] / ukk;
-    __syncthreads();
-    const int w = nb - k - 1;  // rows/cols k+1 .. nb-1
-    for (int q = tid; q < w * w; q += blockDim.x) {
-      int r = k + 1 + q / w, i = k + 1 + q % w;
-      if (i >= r) D[r][i] = fmaf(-D[k][r], D[k][i], D[r][i]);
-    }
-    __syncthreads();
-  }
-  for (int q = tid; q < nb * nb; q += blockDim.x) {
-    int r = q / nb, c = q % nb;
-    if (c >= r) A[(long)(p0 + r) * lda + p0 + c] = D[r][c];
-  }
-}
-
-// The same factorisation in ONE wave with no barriers: lane c keeps column c of the block in
-// registers (col[r] = D[r][c]); row k is broadcast lane-to-lane with readlane.  The entries
-// below the diagonal are scratch (never written back).  Padding (nb < NB) is an identity block.
+// The same factorisation in ONE wave: lane c keeps column c of the block in registers
+// (col[r] = D[r][c]); each step publishes row k through LDS (one 64-float row, read back as
+// broadcasts).  Entries below the diagonal are scratch, never written back.  Padding
+// (nb < NB) is an identity block, which leaves the real entries untouched.
 __global__ __launch_bounds__(64) void chol_diag_wave_kernel(float* A, long lda, int p0, int nb,
                                                             int* info) {
+  __shared__ __attribute__((aligned(16))) float row[2][NB];
   const int c = threadIdx.x;
   float col[NB];
 #pragma unroll
@@ -66,77 +35,106 @@ __global__ __launch_bounds__(64) void chol_diag_wave_kernel(float* A, long lda, 
     if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
     const float ukk = sqrtf(dkk);
     col[k] = (c == k) ? ukk : ((c > k) ? col[k] / ukk : col[k]);
+    row[k & 1][c] = col[k];
+    __syncthreads();
 #pragma unroll
-    for (int r = k + 1; r < NB; ++r) {
-      const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[k]), r));
-      col[r] = fmaf(-s, col[k], col[r]);
-    }
+    for (int r = k + 1; r < NB; ++r) col[r] = fmaf(-row[k & 1][r], col[k], col[r]);
   }
 #pragma unroll
   for (int r = 0; r < NB; ++r)
     if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[r];
 }
 
-// Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution with the factored
-// diagonal block (chains continue from the already-updated A values).
+constexpr int LPR = 4;           // lanes cooperating on one panel column / inverse row
+constexpr int SEG = NB / LPR;    // entries owned per lane
+
+// Loads the nb x nb diagonal block at (r0, r0) into D (identity padding beyond nb).
+PT2Q_DEV void load_diag_block(float (*D)[NB + 4], const float* A, long lda, int r0, int nb) {
+  for (int q = threadIdx.x; q < NB * NB; q += blockDim.x) {
+    int r = q / NB, c = q % NB;
+    D[r][c] = (r < nb && c < nb) ? A[(long)(r0 + r) * lda + r0 + c] : ((r == c) ? 1.0f : 0.0f);
+  }
+}
+
+// Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution against the factored
+// diagonal block, continuing each element's chain from the already-updated A value.  Four
+// lanes share a column (16 rows each); the lane owning row k divides and broadcasts x_k.
 __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int p0, int nb,
                                                          int m) {
-  __shared__ float D[NB][NB + 1];
-  const int tid = threadIdx.x;
-  for (int q = tid; q < nb * nb; q += blockDim.x) {
-    int r = q / nb, c = q % nb;
-    D[r][c] = A[(long)(p0 + r) * lda + p0 + c];
-  }
+  __shared__ __attribute__((aligned(16))) float D[NB][NB + 4];
+  load_diag_block(D, A, lda, p0, nb);
   __syncthreads();
-  const int i = p0 + nb + blockIdx.x * blockDim.x + tid;
-  if (i >= m) return;
-  float x[NB];
+  const int i = p0 + nb + (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int sub = threadIdx.x & (LPR - 1), base = threadIdx.x & 63 & ~(LPR - 1);
+  const bool valid = i < m;
+  float x[SEG];
 #pragma unroll
-  for (int k = 0; k < NB; ++k) x[k] = (k < nb) ? A[(long)(p0 + k) * lda + i] : 0.0f;
+  for (int s = 0; s < SEG; ++s) {
+    int k = sub * SEG + s;
+    x[s] = (valid && k < nb) ? A[(long)(p0 + k) * lda + i] : 0.0f;
+  }
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     if (k < nb) {
-      x[k] = x[k] / D[k][k];
+      const int owner = k / SEG, ks = k % SEG;
+      const float mine = x[ks] / D[k][k];
+      const float xk = __shfl(mine, base | owner);
+      if (sub == owner) x[ks] = xk;
 #pragma unroll
-      for (int r = k + 1; r < NB; ++r)
-        if (r < nb) x[r] = fmaf(-D[k][r], x[k], x[r]);
+      for (int s = 0; s < SEG; ++s) {
+        const int r = sub * SEG + s;
+        const float nv = fmaf(-D[k][r], xk, x[s]);
+        x[s] = (r > k) ? nv : x[s];
+      }
     }
   }
+  if (!valid) return;
 #pragma unroll
-  for (int k = 0; k < NB; ++k)
-    if (k < nb) A[(long)(p0 + k) * lda + i] = x[k];
+  for (int s = 0; s < SEG; ++s) {
+    int k = sub * SEG + s;
+    if (k < nb) A[(long)(p0 + k) * lda + i] = x[s];
+  }
 }
 
 // In-block part of the triangular inverse for column block [c0, c0+nb): rows k < c0+nb.
-// Ui[k][c0..] holds the GEMM partial chains for k < c0 (zero otherwise).
+// Ui[k][c0..] holds the running chains for k < c0 (zero otherwise).  Four lanes share a row.
 __global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long ldu, float* Ui,
                                                             long ldi, int c0, int nb) {
-  __shared__ float D[NB][NB + 1];
-  const int tid = threadIdx.x;
-  for (int q = tid; q < nb * nb; q += blockDim.x) {
-    int r = q / nb, c = q % nb;
-    D[r][c] = U[(long)(c0 + r) * ldu + c0 + c];
-  }
+  __shared__ __attribute__((aligned(16))) float D[NB][NB + 4];
+  load_diag_block(D, U, ldu, c0, nb);
   __syncthreads();
-  const int k = blockIdx.x * blockDim.x + tid;
-  if (k >= c0 + nb) return;
-  float acc[NB];
+  const int k = (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int sub = threadIdx.x & (LPR - 1), base = threadIdx.x & 63 & ~(LPR - 1);
+  const bool valid = k < c0 + nb;
+  float acc[SEG];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) acc[q] = (k < c0 && q < nb) ? Ui[(long)k * ldi + c0 + q] : 0.0f;
+  for (int s = 0; s < SEG; ++s) {
+    int q = sub * SEG + s;
+    acc[s] = (valid && k < c0 && q < nb) ? Ui[(long)k * ldi + c0 + q] : 0.0f;
+  }
   const int jb = (k > c0) ? k - c0 : 0;  // first in-block j (local)
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    if (j < nb && j >= jb) {
-      float xj = (c0 + j == k) ? 1.0f / D[j][j] : -acc[j] / D[j][j];
-      acc[j] = xj;
+    if (j < nb) {
+      const int owner = j / SEG, js = j % SEG;
+      const bool active = j >= jb;
+      const float mine = (c0 + j == k) ? 1.0f / D[j][j] : -acc[js] / D[j][j];
+      const float xj = __shfl(mine, base | owner);
+      if (sub == owner && active) acc[js] = xj;
 #pragma unroll
-      for (int q = j + 1; q < NB; ++q)
-        if (q < nb) acc[q] = fmaf(xj, D[j][q], acc[q]);
+      for (int s = 0; s < SEG; ++s) {
+        const int q = sub * SEG + s;
+        const float nv = fmaf(xj, D[j][q], acc[s]);
+        acc[s] = (active && q > j) ? nv : acc[s];
+      }
     }
   }
+  if (!valid) return;
 #pragma unroll
-  for (int q = 0; q < NB; ++q)
-    if (q < nb) Ui[(long)k * ldi + c0 + q] = (q >= jb) ? acc[q] : 0.0f;
+  for (int s = 0; s < SEG; ++s) {
+    int q = sub * SEG + s;
+    if (q < nb) Ui[(long)k * ldi + c0 + q] = (q >= jb) ? acc[s] : 0.0f;
+  }
 }
 
 __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m) {
@@ -162,8 +160,8 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     PT2Q_LAUNCH_CHECK();
     int rest = m - p0 - nb;
     if (rest <= 0) break;
-    hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div(rest, 256)), dim3(256), 0, st, U, ld, p0,
-                       nb, m);
+    hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div((long)rest * LPR, 256)), dim3(256), 0, st, U,
+                       ld, p0, nb, m);
     PT2Q_LAUNCH_CHECK();
     GemmDesc g{};
     g.M = rest; g.N = rest; g.K = nb;
@@ -180,8 +178,8 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
   for (int c0 = 0; c0 < m; c0 += NB) {
     int nb = (m - c0 < NB) ? m - c0 : NB;
-    hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div(c0 + nb, 256)), dim3(256), 0, st, U, ld,
-                       Ui, ld, c0, nb);
+    hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div((long)(c0 + nb) * LPR, 256)), dim3(256), 0,
+                       st, U, ld, Ui, ld, c0, nb);
     PT2Q_LAUNCH_CHECK();
     int rest = m - c0 - nb;
     if (rest <= 0) break;

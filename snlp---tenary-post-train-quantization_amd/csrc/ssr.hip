@@ -68,14 +68,36 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
   const int t = threadIdx.x & 63;
   if (e >= r) return;
   const float* x = Wt + (long)rem[e] * ldw;
-  float ss = bfly64(sumn_lane<true>(x, n, 1, t));
-  const float nj = clampmin(sqrtf(ss));
   float p = 0.0f;
-  for (long base = 4 * t; base < n; base += 256) {
+  if ((n & 3) == 0 && (ldw & 3) == 0) {
+    // float4 path (same per-lane element order {256u + 4t + q})
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    float ss = 0.0f;
+    for (long base = 4 * t; base < n; base += 256) {
+      f4 v = *(const f4*)(x + base);
+      ss = fmaf(v[0], v[0], ss);
+      ss = fmaf(v[1], v[1], ss);
+      ss = fmaf(v[2], v[2], ss);
+      ss = fmaf(v[3], v[3], ss);
+    }
+    const float nj = clampmin(sqrtf(bfly64(ss)));
+    for (long base = 4 * t; base < n; base += 256) {
+      f4 v = *(const f4*)(x + base);
+      f4 w = *(const f4*)(wn + base);
+      p = fmaf(v[0] / nj, w[0], p);
+      p = fmaf(v[1] / nj, w[1], p);
+      p = fmaf(v[2] / nj, w[2], p);
+      p = fmaf(v[3] / nj, w[3], p);
+    }
+  } else {
+    float ss = bfly64(sumn_lane<true>(x, n, 1, t));
+    const float nj = clampmin(sqrtf(ss));
+    for (long base = 4 * t; base < n; base += 256) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      long i = base + q;
-      if (i < n) p = fmaf(x[i] / nj, wn[i], p);
+      for (int q = 0; q < 4; ++q) {
+        long i = base + q;
+        if (i < n) p = fmaf(x[i] / nj, wn[i], p);
+      }
     }
   }
   p = bfly64(p);
@@ -187,9 +209,20 @@ __global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, lo
     const int ld = b + 1;
     for (int j = tid; j < b; j += blockDim.x) idx[j] = blk ? blk[j] : j;
     __syncthreads();
-    for (int q = tid; q < b * b; q += blockDim.x) {
-      int j = q / b, l = q % b;
-      gb[j * ld + l] = A[(long)idx[j] * lda + idx[l]];
+    const int tot = b * b, step = blockDim.x;
+    for (int q0 = 0; q0 < tot; q0 += 8 * step) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {  // 8 independent gathers in flight per thread
+        int q = q0 + u * step + tid;
+        int qq = q < tot ? q : 0;
+        v[u] = A[(long)idx[qq / b] * lda + idx[qq % b]];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        int q = q0 + u * step + tid;
+        if (q < tot) gb[(q / b) * ld + (q % b)] = v[u];
+      }
     }
     __syncthreads();
     for (int j = tid; j < b; j += blockDim.x) {

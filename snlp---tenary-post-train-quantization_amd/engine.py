@@ -155,6 +155,45 @@ def quantize_layer(W: torch.Tensor, X: torch.Tensor, block_size: int = 128, use_
     return outputs
 
 
+class LayerGraph:
+    """One whole layer (pt2q_quantize_layer: ~600 kernel launches at d=4096) captured into a
+    hipGraph and replayed; W and X are captured by address, so update them in place between
+    replays.  The Cholesky status is read with `spd()` after a replay (one host read)."""
+
+    def __init__(self, W: torch.Tensor, X: torch.Tensor, block_size: int = 128,
+                 use_ssr: bool = True, percdamp: float = 0.01, max_iter: int = 100,
+                 t_dtype=torch.int8):
+        self.W = _float_input(W)
+        self.X = _float_input(X.reshape(-1, X.shape[-1]))
+        n, m = self.W.shape
+        dev = self.W.device
+        B = num_blocks(m, block_size)
+        self.args = (block_size, use_ssr, percdamp, max_iter, t_dtype)
+        self.ws = LayerWorkspace(n, m, block_size, dev)
+        self.out = LayerOutput(torch.empty((n, B), dtype=torch.float32, device=dev),
+                               torch.empty((n, B), dtype=torch.float32, device=dev),
+                               torch.empty((n, m), dtype=t_dtype, device=dev),
+                               torch.empty(m, dtype=torch.int64, device=dev),
+                               torch.zeros(B, dtype=torch.int32, device=dev))
+        self._run()  # eager warm-up: loads every kernel before capture
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._run()
+
+    def _run(self):
+        bs, ssr, pd, mi, td = self.args
+        return quantize_layer(self.W, self.X, bs, ssr, pd, mi, td, workspace=self.ws,
+                              check_spd=False, outputs=self.out)
+
+    def replay(self) -> LayerOutput:
+        self.graph.replay()
+        return self.out
+
+    def spd(self) -> bool:
+        return int(self.out.info.item()) == 0
+
+
 def dequantize(alpha, mu, T, perm, block_size):
     """Correct reconstruction W_q[:, perm[k*b:(k+1)*b]] = alpha[:,k]*T + mu[:,k] (gptq.py:201-230)."""
     n, m = T.shape

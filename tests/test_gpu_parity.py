@@ -235,6 +235,25 @@ def test_layer_g_vs_reference_and_oracle(pt2q, name):
     assert bits_equal(host(Wq), want)
 
 
+def test_layer_graph_replay_matches_eager(pt2q):
+    """The hipGraph-captured layer (bench path) replays to the same bits as the oracle."""
+    W = synth.weights(41, 1024, 768)
+    X = synth.activations(42, 1536, 768)
+    Wd, Xd = cuda(W), cuda(X)
+    lg = pt2q.LayerGraph(Wd, Xd)
+    out = lg.replay()
+    torch.cuda.synchronize()
+    assert lg.spd()
+    ref = _oracle_m(W, X, 128, True)
+    _assert_layer_bitexact(out, ref)
+    # new inputs in place -> replay recomputes
+    W2 = synth.weights(43, 1024, 768)
+    Wd.copy_(cuda(W2))
+    out = lg.replay()
+    torch.cuda.synchronize()
+    _assert_layer_bitexact(out, _oracle_m(W2, X, 128, True))
+
+
 def test_layer_not_spd_pinv_fallback(pt2q):
     g = load_golden("layer_m_notspd")
     W, X = layer_inputs(g)
