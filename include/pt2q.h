@@ -66,9 +66,11 @@ size_t pt2q_cholesky_workspace_bytes(int m);
 
 /* G = XᵀX (accumulate=0) or G = G + XᵀX (accumulate=1).  X: N x m of type xdtype.
  * Replaces main.py:128 (H = X.T @ X) and gptq.py:59-76 (GPTQ.add_batch). Writes the full
- * symmetric matrix. */
+ * symmetric matrix.  workspace (nullable, pt2q_gram_workspace_bytes(m)) enables the balanced
+ * persistent kernel for long K. */
+size_t pt2q_gram_workspace_bytes(int m);
 int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G, int64_t ldg,
-              int accumulate, void* stream);
+              int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
 /* H = G / nsamples; H_ii += percdamp * mean(diag H).  Replaces main.py:129-133 and
  * gptq.py:94-98.  damp_dev (nullable) receives the damping value. */

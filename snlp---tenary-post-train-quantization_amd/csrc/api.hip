@@ -201,15 +201,20 @@ extern "C" size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags) {
   (void)flags;
   if (n <= 0 || m <= 0 || b <= 0) return 0;
   size_t mm = ((size_t)m * m * 4 + 255) & ~(size_t)255;
-  return blocks_bytes(n, m, b) + 4 * mm + 2 * 256;
+  return blocks_bytes(n, m, b) + 4 * mm + 2 * 256 + pt2q_gram_workspace_bytes(m);
 }
 
 extern "C" size_t pt2q_ssr_workspace_bytes(int n, int m) {
   return blocks_bytes(n, m, 128);
 }
 
+extern "C" size_t pt2q_gram_workspace_bytes(int m) {
+  return m > 0 ? (pt2q_gram_flags_ints(m) * sizeof(int) + 255) & ~(size_t)255 : 0;
+}
+
 extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G,
-                         int64_t ldg, int accumulate, void* stream) {
+                         int64_t ldg, int accumulate, void* workspace, size_t workspace_bytes,
+                         void* stream) {
   if (!X || !G || N < 0 || m <= 0 || !dtype_ok(xdtype) || ldx < m || ldg < m) return PT2Q_E_ARG;
   GemmDesc g{};
   g.M = m; g.N = m; g.K = (int)N;
@@ -219,7 +224,9 @@ extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ld
   g.C = G; g.ldc = ldg;
   g.mode = accumulate ? GEMM_ADD : GEMM_STORE;
   g.upper = 1; g.mirror = 1;
-  return pt2q_launch_gemm(g, (hipStream_t)stream);
+  int* flags = (workspace && workspace_bytes >= pt2q_gram_flags_ints(m) * sizeof(int))
+                   ? (int*)workspace : nullptr;
+  return pt2q_launch_gram(g, flags, (hipStream_t)stream);
 }
 
 extern "C" int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples,
@@ -276,10 +283,13 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
   float* Ui = c.take<float>((size_t)m * m);
   float* Hinv = c.take<float>((size_t)m * m);
   float* damp = c.take<float>(1);
+  int* gflags = c.take<int>(pt2q_gram_flags_ints(m));
   BlockWs w;
   if (!c.ok || !carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
   int rc;
-  if ((rc = pt2q_gram(X, xdtype, N, m, ldx, G, m, 0, stream)) != PT2Q_OK) return rc;
+  if ((rc = pt2q_gram(X, xdtype, N, m, ldx, G, m, 0, gflags,
+                     pt2q_gram_flags_ints(m) * sizeof(int), stream)) != PT2Q_OK)
+    return rc;
   if ((rc = pt2q_launch_prepare_hessian(G, m, m, N, percdamp, H, m, damp, st)) != PT2Q_OK) return rc;
   // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G)
   if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st)) != PT2Q_OK) return rc;

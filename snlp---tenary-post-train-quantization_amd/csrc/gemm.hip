@@ -128,41 +128,53 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, typename TIn, bool VEC>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
-  constexpr int RM = BM / 64, RN = BN / 64;
-
-  int ti, tj;
-  {
-    int bid = blockIdx.x;
-    if (g.upper) {
-      ti = 0;
-      while (bid >= tiles_n - ti) {
-        bid -= tiles_n - ti;
-        ++ti;
+// Upper-triangle tile order: 8x8-tile supertiles, row-major over the super-triangle, row-major
+// (i <= j) inside a supertile.  L is a logical tile index in [0, T(T+1)/2).
+PT2Q_DEV void upper_tile(int L, int T, int& ti, int& tj) {
+  constexpr int S = 8;
+  const int Ts = (T + S - 1) / S;
+  int I = 0, J = 0;
+  for (;;) {
+    const int h = min(S, T - I * S), w = min(S, T - J * S);
+    const int cnt = (I == J) ? h * (h + 1) / 2 : h * w;
+    if (L < cnt) {
+      if (I == J) {
+        int rr = 0;
+        while (L >= h - rr) {
+          L -= h - rr;
+          ++rr;
+        }
+        ti = I * S + rr;
+        tj = I * S + rr + L;
+      } else {
+        ti = I * S + L / w;
+        tj = J * S + L % w;
       }
-      tj = ti + bid;
-    } else {
-      ti = bid / tiles_n;
-      tj = bid % tiles_n;
+      return;
+    }
+    L -= cnt;
+    if (++J == Ts) {
+      ++I;
+      J = I;
     }
   }
-  const int i0 = ti * BM, j0 = tj * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int li = lane & 31, lk = lane >> 5;
+}
 
+// Bijective XCD-aware remap: blocks b, b+8, ... (one XCD under round-robin dispatch) get a
+// contiguous range of logical ids.  Speed only; any placement is correct.
+PT2Q_DEV int xcd_remap(int b, int nwg) {
+  const int xcd = b % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+template <int BM, int BN>
+struct Frag {
+  static constexpr int RM = BM / 64, RN = BN / 64;
   f32x16 acc[RM][RN];
-#pragma unroll
-  for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-    for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[rm][rn][r] = 0.0f;
-  if (g.mode == GEMM_CHAIN_NEG || g.mode == GEMM_CHAIN_POS) {
-    // chains continue from C (no output-row gather in this mode); all loads issued before use
+  template <typename F>
+  PT2Q_DEV void for_each(int i0, int j0, F&& f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm)
 #pragma unroll
@@ -171,83 +183,200 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
         for (int r = 0; r < 16; ++r) {
           int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
           int col = j0 + wc * (BN / 2) + rn * 32 + li;
-          bool in = row < g.M && col < g.N;
-          acc[rm][rn][r] = g.C[in ? (long)row * g.ldc + col : 0];
-        }
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          int col = j0 + wc * (BN / 2) + rn * 32 + li;
-          if (!(row < g.M && col < g.N)) acc[rm][rn][r] = 0.0f;
+          float v = acc[rm][rn][r];
+          f(v, row, col);
+          acc[rm][rn][r] = v;
         }
   }
+};
 
-  int kbeg = 0;
-  if (g.kstart_diag == 1) kbeg = i0 - (i0 % BK);
-  if (g.kstart_diag == 2) kbeg = j0 - (j0 % BK);
+// Extend the chains of one output tile over K-range [kbeg, kend) (k ascending).
+template <int BM, int BN, typename TIn, bool VEC>
+PT2Q_DEV void tile_mma(Frag<BM, BN>& F, const GemmDesc& g, int i0, int j0, int kbeg, int kend,
+                       float (*As)[BK][BM + PAD], float (*Bs)[BK][BN + PAD]) {
+  constexpr int RM = BM / 64, RN = BN / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
   const TIn* Ab = (const TIn*)g.A;
   const TIn* Bb = (const TIn*)g.B;
   const float sgn = (g.mode == GEMM_CHAIN_NEG) ? -1.0f : 1.0f;
-
-  TileLoader<TIn, BM, VEC> la;
-  TileLoader<TIn, BN, VEC> lb;
-  if (kbeg < g.K) {
-    la.load(Ab, g.lda, g.a_layout, i0, kbeg, g.M, g.K);
-    lb.load(Bb, g.ldb, g.b_layout, j0, kbeg, g.N, g.K);
-    la.store(As[0], g.a_layout);
-    lb.store(Bs[0], g.b_layout);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int k0 = kbeg; k0 < g.K; k0 += BK) {
-    const bool more = (k0 + BK < g.K);
-    if (more) {
-      la.load(Ab, g.lda, g.a_layout, i0, k0 + BK, g.M, g.K);
-      lb.load(Bb, g.ldb, g.b_layout, j0, k0 + BK, g.N, g.K);
+  // Two register stages (loop unrolled by 2, so no dynamic register indexing): while the MFMAs
+  // of K-tile t run from LDS, the loads of tiles t+1 and t+2 are in flight.
+  TileLoader<TIn, BM, VEC> la0, la1;
+  TileLoader<TIn, BN, VEC> lb0, lb1;
+  auto compute = [&](int buf) {
+    float a[BK / 2][RM], b[BK / 2][RN];
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+#pragma unroll
+      for (int rm = 0; rm < RM; ++rm) a[s][rm] = As[buf][2 * s + lk][wr * (BM / 2) + rm * 32 + li];
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn) b[s][rn] = Bs[buf][2 * s + lk][wc * (BN / 2) + rn * 32 + li];
     }
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float a[RM], b[RN];
-#pragma unroll
-      for (int rm = 0; rm < RM; ++rm) a[rm] = sgn * As[cur][kk + lk][wr * (BM / 2) + rm * 32 + li];
-#pragma unroll
-      for (int rn = 0; rn < RN; ++rn) b[rn] = Bs[cur][kk + lk][wc * (BN / 2) + rn * 32 + li];
+    for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
       for (int rm = 0; rm < RM; ++rm)
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn)
-          acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[rm], b[rn], acc[rm][rn], 0, 0, 0);
+          F.acc[rm][rn] =
+              __builtin_amdgcn_mfma_f32_32x32x2f32(sgn * a[s][rm], b[s][rn], F.acc[rm][rn], 0, 0, 0);
+  };
+  // elements with k >= kend are zero-filled: an exact no-op for the chains
+  if (kbeg < kend) {
+    la0.load(Ab, g.lda, g.a_layout, i0, kbeg, g.M, kend);
+    lb0.load(Bb, g.ldb, g.b_layout, j0, kbeg, g.N, kend);
+    la0.store(As[0], g.a_layout);
+    lb0.store(Bs[0], g.b_layout);
+    if (kbeg + BK < kend) {
+      la1.load(Ab, g.lda, g.a_layout, i0, kbeg + BK, g.M, kend);
+      lb1.load(Bb, g.ldb, g.b_layout, j0, kbeg + BK, g.N, kend);
     }
-    if (more) {
-      la.store(As[cur ^ 1], g.a_layout);
-      lb.store(Bs[cur ^ 1], g.b_layout);
-    }
-    __syncthreads();
-    cur ^= 1;
   }
+  __syncthreads();
+  for (int k0 = kbeg; k0 < kend; k0 += 2 * BK) {
+    if (k0 + 2 * BK < kend) {
+      la0.load(Ab, g.lda, g.a_layout, i0, k0 + 2 * BK, g.M, kend);
+      lb0.load(Bb, g.ldb, g.b_layout, j0, k0 + 2 * BK, g.N, kend);
+    }
+    compute(0);
+    if (k0 + BK >= kend) break;
+    la1.store(As[1], g.a_layout);
+    lb1.store(Bs[1], g.b_layout);
+    __syncthreads();
+    if (k0 + 3 * BK < kend) {
+      la1.load(Ab, g.lda, g.a_layout, i0, k0 + 3 * BK, g.M, kend);
+      lb1.load(Bb, g.ldb, g.b_layout, j0, k0 + 3 * BK, g.N, kend);
+    }
+    compute(1);
+    if (k0 + 2 * BK >= kend) break;
+    la0.store(As[0], g.a_layout);
+    lb0.store(Bs[0], g.b_layout);
+    __syncthreads();
+  }
+  __syncthreads();  // LDS is reused by the next tile / epilogue
+}
 
+template <int BM, int BN, typename TIn, bool VEC>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  int ti, tj;
+  if (g.upper) {
+    upper_tile(xcd_remap(blockIdx.x, gridDim.x), tiles_n, ti, tj);
+  } else {
+    ti = blockIdx.x / tiles_n;
+    tj = blockIdx.x % tiles_n;
+  }
+  const int i0 = ti * BM, j0 = tj * BN;
+  Frag<BM, BN> F;
+  F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
+  if (g.mode == GEMM_CHAIN_NEG || g.mode == GEMM_CHAIN_POS) {
+    // chains continue from C (no output-row gather in this mode); all loads issued before use
+    F.for_each(i0, j0, [&](float& a, int row, int col) {
+      bool in = row < g.M && col < g.N;
+      a = g.C[in ? (long)row * g.ldc + col : 0];
+    });
+    F.for_each(i0, j0, [&](float& a, int row, int col) {
+      if (!(row < g.M && col < g.N)) a = 0.0f;
+    });
+  }
+  int kbeg = 0;
+  if (g.kstart_diag == 1) kbeg = i0 - (i0 % BK);
+  if (g.kstart_diag == 2) kbeg = j0 - (j0 % BK);
+  tile_mma<BM, BN, TIn, VEC>(F, g, i0, j0, kbeg, g.K, As, Bs);
   const bool mirror = g.upper && g.mirror && (ti != tj);
-#pragma unroll
-  for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-    for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        int col = j0 + wc * (BN / 2) + rn * 32 + li;
-        if (row >= g.M || col >= g.N) continue;
-        long crow = g.crow ? g.crow[row] : row;
-        float* p = g.C + crow * g.ldc + col;
-        float v = acc[rm][rn][r];
-        if (g.mode == GEMM_ADD) v = *p + v;
-        else if (g.mode == GEMM_SUB) v = *p - v;
-        *p = v;
-        if (mirror) g.C[(long)col * g.ldc + row] = v;
+  F.for_each(i0, j0, [&](float& a, int row, int col) {
+    if (row >= g.M || col >= g.N) return;
+    long crow = g.crow ? g.crow[row] : row;
+    float* p = g.C + crow * g.ldc + col;
+    float v = a;
+    if (g.mode == GEMM_ADD) v = *p + v;
+    else if (g.mode == GEMM_SUB) v = *p - v;
+    *p = v;
+    if (mirror) g.C[(long)col * g.ldc + row] = v;
+  });
+}
+
+// Persistent, balanced ("stream-K with exact chain continuation") symmetric Gram, STORE mode:
+// the K range is cut into nseg segments and unit u = seg * T + tile.  Workgroups take units in
+// increasing u from a global counter.  A unit with seg > 0 waits for the tile's previous segment
+// (flag), continues the chains from the partial tile stored in C (plain fp32, so the fmaf chain
+// is exactly the unsplit one), and stores the partial back; the last segment writes the final
+// tile and its mirror.  A unit only waits on a smaller unit, which was taken earlier by a
+// workgroup that is already running, so progress never depends on how many workgroups are
+// resident.  Units taken together share a K range, so the X panels they read are shared in L2.
+template <typename TIn, bool VEC>
+__global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, int nseg, int seglen,
+                                                           int* flags, int* timeout) {
+  constexpr int BM = 128, BN = 128;
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  __shared__ long s_unit;
+  const int ntile = T * (T + 1) / 2;
+  const long units = (long)ntile * nseg;
+  int* counter = timeout + 1;
+  for (;;) {
+    if (threadIdx.x == 0) s_unit = atomicAdd(counter, 1);
+    __syncthreads();
+    const long u = s_unit;
+    __syncthreads();
+    if (u >= units) break;
+    const int seg = (int)(u / ntile), tl = (int)(u % ntile);
+    int ti, tj;
+    upper_tile(tl, T, ti, tj);
+    const int i0 = ti * BM, j0 = tj * BN;
+    Frag<BM, BN> F;
+    if (seg == 0) {
+      F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
+    } else {
+      if (threadIdx.x == 0) {
+        long spins = 0;
+        while (__hip_atomic_load(&flags[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seg) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1l << 28)) {
+            atomicExch(timeout, 1);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      __syncthreads();
+      F.for_each(i0, j0, [&](float& a, int row, int col) {
+        bool in = row < g.M && col < g.N;
+        a = g.C[in ? (long)row * g.ldc + col : 0];
+      });
+    }
+    const int kbeg = seg * seglen, kend = min(g.K, kbeg + seglen);
+    tile_mma<BM, BN, TIn, VEC>(F, g, i0, j0, kbeg, kend, As, Bs);
+    const bool last = (seg == nseg - 1);
+    const bool mirror = last && (ti != tj);
+    F.for_each(i0, j0, [&](float& a, int row, int col) {
+      if (row >= g.M || col >= g.N) return;
+      g.C[(long)row * g.ldc + col] = a;
+      if (mirror) g.C[(long)col * g.ldc + row] = a;
+    });
+    if (!last) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[tl], seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, typename TIn>
+bool vec_ok(const GemmDesc& g) {
+  const int vw = 16 / (int)sizeof(TIn);
+  auto ok_vec = [&](const void* p, long ld, int layout, int dim) {
+    int vdim = (layout == LAY_KMAJOR) ? dim : g.K;
+    return ((uintptr_t)p % 16 == 0) && (ld % vw == 0) && (vdim % vw == 0);
+  };
+  return ok_vec(g.A, g.lda, g.a_layout, g.M) && ok_vec(g.B, g.ldb, g.b_layout, g.N);
 }
 
 template <int BM, int BN, typename TIn>
@@ -261,13 +390,7 @@ int launch_t(const GemmDesc& g, hipStream_t st) {
     ntiles = (long)tm * tn;
   }
   if (ntiles <= 0) return PT2Q_OK;
-  const int vw = 16 / (int)sizeof(TIn);
-  auto ok_vec = [&](const void* p, long ld, int layout, int dim) {
-    int vdim = (layout == LAY_KMAJOR) ? dim : g.K;
-    return ((uintptr_t)p % 16 == 0) && (ld % vw == 0) && (vdim % vw == 0);
-  };
-  const bool vec = ok_vec(g.A, g.lda, g.a_layout, g.M) && ok_vec(g.B, g.ldb, g.b_layout, g.N);
-  if (vec)
+  if (vec_ok<BM, BN, TIn>(g))
     hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, true>), dim3((unsigned)ntiles), dim3(256), 0, st, g,
                        tm, tn);
   else
@@ -298,6 +421,30 @@ int launch_dt(const GemmDesc& g, hipStream_t st) {
   return launch_t<64, 64, TIn>(g, st);
 }
 
+template <typename TIn>
+int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
+  const int T = ceil_div(g.M, 128);
+  const int ntile = T * (T + 1) / 2;
+  if (ntile > nflags) return PT2Q_E_WORKSPACE;
+  int dev = 0, cus = 256, per_cu = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  auto kern = vec_ok<128, 128, TIn>(g) ? gram_streamk_kernel<TIn, true> : gram_streamk_kernel<TIn, false>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const int P = cus * per_cu;  // one resident wave of workgroups (correctness does not need it)
+  // segments: enough units for >= 12 rounds, segment >= 2048 rows, multiple of 2*BK
+  int nseg = (int)std::ceil(12.0 * P / ntile);
+  int seglen = ceil_div(g.K, nseg);
+  if (seglen < 2048) seglen = 2048;
+  seglen = ceil_div(seglen, 2 * BK) * 2 * BK;
+  nseg = ceil_div(g.K, seglen);
+  if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2), st) != hipSuccess) return PT2Q_E_HIP;
+  int* timeout = flags + ntile;
+  hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
 }  // namespace
 
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
@@ -312,4 +459,30 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
       return launch_dt<uint16_t>(g, st);
   }
   return PT2Q_E_ARG;
+}
+
+size_t pt2q_gram_flags_ints(int m) {
+  long T = ceil_div(m, 128);
+  return (size_t)(T * (T + 1) / 2 + 2);  // tile flags, timeout, unit counter
+}
+
+// Symmetric Gram C = XᵀX (STORE): balanced persistent kernel when it pays (big K, enough
+// tiles), else the one-tile-per-workgroup GEMM.  flags: pt2q_gram_flags_ints(m) ints or NULL.
+int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st) {
+  const int T = ceil_div(g.M, 128);
+  const long ntile = (long)T * (T + 1) / 2;
+  static const char* mode = std::getenv("PT2Q_GRAM_STREAMK");
+  const bool allow = !(mode && mode[0] == '0');
+  if (flags && allow && g.mode == GEMM_STORE && g.upper && g.mirror && g.M == g.N &&
+      ntile >= 128 && g.K >= 16384) {
+    switch (g.in_dtype) {
+      case PT2Q_F32:
+        return launch_streamk<float>(g, flags, (int)ntile, st);
+      case PT2Q_F16:
+        return launch_streamk<_Float16>(g, flags, (int)ntile, st);
+      case PT2Q_BF16:
+        return launch_streamk<uint16_t>(g, flags, (int)ntile, st);
+    }
+  }
+  return pt2q_launch_gemm(g, st);
 }

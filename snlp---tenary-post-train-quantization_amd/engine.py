@@ -43,8 +43,10 @@ def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate: bool = F
     if G is None:
         G = torch.empty((m, m), dtype=torch.float32, device=X.device)
         accumulate = False
+    ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), X.device)
     _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), N, m, m, _lib.ptr(G), m,
-                                    int(accumulate), _lib.stream_of(X.device)), "pt2q_gram")
+                                    int(accumulate), _lib.ptr(ws), ws.numel(),
+                                    _lib.stream_of(X.device)), "pt2q_gram")
     return G
 
 

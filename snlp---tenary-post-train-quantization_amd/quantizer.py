@@ -65,7 +65,7 @@ class AsymmetricTernaryQuantizer:
         S = torch.empty((b, b), dtype=torch.float32, device=dev)
         st = _lib.stream_of(dev)
         _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), X.shape[0], b, b,
-                                        _lib.ptr(S), b, 0, st), "pt2q_gram")
+                                        _lib.ptr(S), b, 0, None, 0, st), "pt2q_gram")
         S1 = torch.empty(b, dtype=torch.float32, device=dev)
         d = torch.empty(1, dtype=torch.float32, device=dev)
         _lib.check(_lib.lib().pt2q_s1_from_gram(_lib.ptr(S), b, b, _lib.ptr(S1), _lib.ptr(d), st),

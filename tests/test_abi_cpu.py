@@ -48,7 +48,7 @@ def test_host_only_entry_points(pt2q):
 def test_argument_errors_without_device(pt2q):
     lib = pt2q._lib.lib()
     E_ARG = 1
-    assert lib.pt2q_gram(None, 0, 10, 10, 10, None, 10, 0, None) == E_ARG
+    assert lib.pt2q_gram(None, 0, 10, 10, 10, None, 10, 0, None, 0, None) == E_ARG
     assert lib.pt2q_quantize_layer(None, 0, 1, 1, 1, None, 0, 1, 1, 128, 0, 0.01, 100, None, None,
                                    None, 3, None, None, None, None, 0, None) == E_ARG
     assert lib.pt2q_atq_stage(0, None, 1, 1, 1, None, None, None, 1, None, None, 100, None, None, 0,

@@ -47,6 +47,18 @@ def test_gram_bitexact(pt2q, N, m, dt):
     assert bits_equal(host(G2), ref2)
 
 
+@pytest.mark.parametrize("N,m,dt", [(16384, 2048, torch.float16), (20000, 2100, torch.float16),
+                                     (17000, 2048, torch.float32), (16448, 2176, torch.bfloat16)])
+def test_gram_streamk_bitexact(pt2q, N, m, dt):
+    """The balanced persistent Gram (segmented K, chains continued through fp32 partials) is
+    taken for K >= 16384 and >= 128 tiles of 128x128; it must equal the oracle bit-for-bit,
+    including ragged m / N (scalar-load path for m % 8 != 0)."""
+    X = synth.activations(13 + m, N, m)
+    Xd = cuda(X).to(dt)
+    G = pt2q.gram(Xd)
+    assert bits_equal(host(G), orc.gram(host(Xd.float())))
+
+
 @pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500)])
 def test_hessian_cholesky_inverse_bitexact(pt2q, m, N):
     X = synth.activations(11 + m, N, m)
