@@ -64,9 +64,11 @@ const char* pt2q_strerror(int status);
 size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags);
 size_t pt2q_cholesky_workspace_bytes(int m);
 
-/* G = XᵀX (accumulate=0) or G = G + XᵀX (accumulate=1).  X: N x m of type xdtype.
- * Replaces main.py:128 (H = X.T @ X) and gptq.py:59-76 (GPTQ.add_batch). Writes the full
- * symmetric matrix.  workspace (nullable, pt2q_gram_workspace_bytes(m)) enables the balanced
+/* G = XᵀX (accumulate=0), G = G + XᵀX (accumulate=1), or continue (accumulate=2): every
+ * entry's k-ascending chain resumes from G, so Grams streamed batch by batch are bit-identical
+ * to one Gram of the concatenated rows.  X: N x m of type xdtype.
+ * Replaces main.py:128 (H = X.T @ X over the captured activations, main.py:293),
+ * gptq.py:59-76 (GPTQ.add_batch, accumulate=1). Writes the full symmetric matrix.  workspace (nullable, pt2q_gram_workspace_bytes(m)) enables the balanced
  * persistent kernel for long K. */
 size_t pt2q_gram_workspace_bytes(int m);
 int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G, int64_t ldg,

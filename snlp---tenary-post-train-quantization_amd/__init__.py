@@ -13,9 +13,11 @@ from .quantizer import AsymmetricTernaryQuantizer, compute_output_error, compute
 from .reorder import compute_column_similarity_to_mean, select_next_block_ssr
 from .gptq import GPTQ, GPTQQuantizer
 from .pt2llm import PT2LLMQuantizer
+from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_llm_layers,
+                          quantize_decoder_layer)
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
-                     gram, pack_ternary, prepare_hessian, quantize_blocks, quantize_layer,
-                     unpack_ternary)
+                     gram, hessian_inverse, pack_ternary, prepare_hessian, quantize_blocks,
+                     quantize_layer, quantize_shared, unpack_ternary)
 
 __version__ = "0.1.0"
 __all__ = [
@@ -23,5 +25,6 @@ __all__ = [
     "compute_column_similarity_to_mean", "select_next_block_ssr", "GPTQ", "GPTQQuantizer",
     "PT2LLMQuantizer", "LayerGraph", "LayerOutput", "LayerWorkspace", "gram", "prepare_hessian",
     "cholesky_inverse", "quantize_blocks", "quantize_layer", "dequantize", "pack_ternary",
-    "unpack_ternary", "fill_synthetic",
+    "unpack_ternary", "fill_synthetic", "hessian_inverse", "quantize_shared", "GramAccumulator",
+    "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
 ]

@@ -1,0 +1,198 @@
+"""Calibration capture with on-the-fly Grams — the caller of the hot path.
+
+The reference (main.py:257-299) registers forward hooks on every nn.Linear of one decoder layer,
+keeps every captured input (128 samples x 2048 tokens x d fp32 = 4 GB per linear at d=4096),
+concatenates them and calls quantize_layer(linear, X) once per linear.  Only the Gram of X is
+ever needed by the layer loop (H = XᵀX/N, and the AGA statistics S1 = G[blk,blk]·1 of
+main.py:177 come from the raw Gram), so here each hook streams its batch straight into an
+m x m fp32 Gram with the chain-continuing Gram kernel (pt2q_gram accumulate=2).  The result is
+bit-identical to the Gram of the concatenated activations, memory is O(m²) instead of O(N·m),
+and linears that read the same tensor (q/k/v, gate/up) share one Gram and one Cholesky
+inverse.
+
+Reference helpers mirrored: find_linear_layers (model.py:162-171), get_llm_layers
+(model.py:139-159), the per-layer loop of PT2LLMQuantizer.quantize (main.py:232-308) and its
+weight write-back _dequantize_weight (main.py:313-335).
+"""
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import engine
+
+
+def find_linear_layers(module: nn.Module, prefix: str = "") -> Dict[str, nn.Linear]:
+    """model.py:162-171: recursive name -> nn.Linear map (children order)."""
+    out = {}
+    for name, child in module.named_children():
+        full = f"{prefix}.{name}" if prefix else name
+        if isinstance(child, nn.Linear):
+            out[full] = child
+        else:
+            out.update(find_linear_layers(child, full))
+    return out
+
+
+def get_llm_layers(model: nn.Module, model_type: str = "llama"):
+    """model.py:139-159: the decoder-layer list of the supported architectures."""
+    if model_type in ("llama", "llama2", "llama3", "qwen", "qwen3"):
+        return model.model.layers
+    if model_type in ("gemma", "gemma3"):
+        if hasattr(model, "language_model") and hasattr(model.language_model, "layers"):
+            return model.language_model.layers
+        if hasattr(model, "model") and hasattr(model.model, "layers"):
+            return model.model.layers
+        raise AttributeError("Cannot find layers in Gemma model")
+    if model_type == "opt":
+        return model.model.decoder.layers
+    if model_type == "bloom":
+        return model.transformer.h
+    raise ValueError(f"Unknown model type: {model_type}")
+
+
+class GramAccumulator:
+    """An m x m fp32 Gram fed batch by batch; bit-identical to XᵀX of the concatenated rows."""
+
+    def __init__(self, m: int, device):
+        self.m = m
+        self.device = torch.device(device)
+        self.G = torch.zeros((m, m), dtype=torch.float32, device=self.device)
+        self.nsamples = 0
+        self._ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), self.device)
+
+    def add(self, X: torch.Tensor):
+        X = X.reshape(-1, X.shape[-1])
+        if X.shape[-1] != self.m:
+            raise ValueError(f"GramAccumulator: expected {self.m} features, got {X.shape[-1]}")
+        X = X.to(self.device)
+        if X.shape[0] == 0:
+            return
+        mode = "continue" if self.nsamples else False
+        engine.gram(X, self.G, accumulate=mode, workspace=self._ws)
+        self.nsamples += X.shape[0]
+
+
+class GramCapture:
+    """Forward hooks on a set of linears (main.py:262-275) that stream each input batch into a
+    Gram.  Linears whose input is the very same tensor in a forward pass share one accumulator
+    (grouping is fixed at the first pass and checked afterwards)."""
+
+    def __init__(self, linears: Dict[str, nn.Linear], device=None):
+        self.linears = linears
+        self.device = device
+        self.group_of: Dict[str, int] = {}
+        self.accs: List[GramAccumulator] = []
+        self.members: List[List[str]] = []
+        self._last_key: Dict[int, tuple] = {}
+        # the last input of each group is held until the next pass, so its storage cannot be
+        # recycled for another tensor of the same shape within the pass (that would alias keys)
+        self._held: Dict[int, torch.Tensor] = {}
+        self._pass = 0
+        self._hooks = []
+
+    @staticmethod
+    def _key(t: torch.Tensor, pass_id: int):
+        return (pass_id, t.data_ptr(), tuple(t.shape), tuple(t.stride()), t._version)
+
+    def _hook(self, name):
+        def hook(module, inp, out):
+            x = inp[0] if isinstance(inp, tuple) else inp
+            x = x.detach()
+            key = self._key(x, self._pass)
+            if name not in self.group_of:
+                gid = None
+                for g, k in self._last_key.items():
+                    if k == key and self.accs[g].m == x.shape[-1]:
+                        gid = g
+                        break
+                if gid is None:
+                    dev = self.device if self.device is not None else x.device
+                    self.accs.append(GramAccumulator(x.shape[-1], dev))
+                    self.members.append([])
+                    gid = len(self.accs) - 1
+                self.group_of[name] = gid
+                self.members[gid].append(name)
+            gid = self.group_of[name]
+            if self._last_key.get(gid) == key:
+                return  # same tensor already added by a group partner in this pass
+            if self._last_key.get(gid, (None,))[0] == self._pass:
+                raise RuntimeError(f"GramCapture: linears {self.members[gid]} were grouped on a "
+                                   "shared input but received different inputs")
+            self._last_key[gid] = key
+            self._held[gid] = x
+            self.accs[gid].add(x)
+        return hook
+
+    def __enter__(self):
+        for name, lin in self.linears.items():
+            self._hooks.append(lin.register_forward_hook(self._hook(name)))
+        return self
+
+    def __exit__(self, *exc):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self._held.clear()
+        return False
+
+    def next_pass(self):
+        """Call between forward passes (one per calibration sample)."""
+        self._pass += 1
+        self._held.clear()
+
+    def groups(self):
+        """[(accumulator, [linear names])] in first-seen order."""
+        return list(zip(self.accs, self.members))
+
+
+def dequantize_weight_reference(params, block_size: int) -> torch.Tensor:
+    """main.py:313-335 exactly as the reference writes weights back between layers: blocks are
+    taken as contiguous column ranges of T (which is in ORIGINAL order) and then the inverse
+    permutation is applied, which mis-assigns scales when SSR reorders.  Kept for
+    reference-compatible model propagation; `engine.dequantize` is the correct reconstruction."""
+    T = params["T"].float()
+    alpha, mu, perm = params["alpha"], params["mu"], params["perm"]
+    n, m = T.shape
+    W = torch.zeros(n, m, dtype=alpha.dtype, device=T.device)
+    for b in range(alpha.shape[1]):
+        s, e = b * block_size, min((b + 1) * block_size, m)
+        W[:, s:e] = alpha[:, b:b + 1] * T[:, s:e] + mu[:, b:b + 1]
+    return W[:, torch.argsort(perm)]
+
+
+@torch.no_grad()
+def quantize_decoder_layer(layer: nn.Module, run_forward, block_size: int = 128,
+                           use_ssr: bool = True, percdamp: float = 0.01, layer_idx: int = 0,
+                           writeback: str = "reference", device=None):
+    """One iteration of main.py:258-303 for decoder layer `layer`.
+
+    run_forward(capture) must run the calibration forwards (calling capture.next_pass() between
+    samples).  Returns {"layer_<i>.<name>": {alpha, mu, T int8, perm}} (device tensors) and
+    writes the quantised weights back into the linears ("reference": main.py:297-299 semantics,
+    "correct": gptq.py:201-230 reconstruction, "none": leave weights untouched)."""
+    linears = find_linear_layers(layer)
+    cap = GramCapture(linears, device)
+    with cap:
+        run_forward(cap)
+    results = {}
+    for acc, names in cap.groups():
+        Ws = [linears[nm].weight.data.to(acc.device) for nm in names]
+        outs = engine.quantize_shared(Ws, acc.G, acc.nsamples, block_size, use_ssr, percdamp)
+        for nm, out in zip(names, outs):
+            lin = linears[nm]
+            dt = lin.weight.dtype
+            params = {"alpha": out.alpha.to(dt), "mu": out.mu.to(dt), "T": out.T, "perm": out.perm}
+            results[f"layer_{layer_idx}.{nm}"] = params
+            if writeback == "reference":
+                Wq = dequantize_weight_reference(params, block_size)
+            elif writeback == "correct":
+                bs = block_size if block_size < out.T.shape[1] else out.T.shape[1]
+                Wq = engine.dequantize(out.alpha, out.mu, out.T, out.perm, bs)
+            elif writeback == "none":
+                continue
+            else:
+                raise ValueError(f"writeback must be reference|correct|none, got {writeback}")
+            lin.weight.data = Wq.to(lin.weight.device, dt)
+    return results

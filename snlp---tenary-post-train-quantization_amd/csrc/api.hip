@@ -222,7 +222,8 @@ extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ld
   g.B = X; g.ldb = ldx; g.b_layout = LAY_KMAJOR;
   g.in_dtype = xdtype;
   g.C = G; g.ldc = ldg;
-  g.mode = accumulate ? GEMM_ADD : GEMM_STORE;
+  if (accumulate < 0 || accumulate > 2) return PT2Q_E_ARG;
+  g.mode = accumulate == 2 ? GEMM_CHAIN_POS : accumulate ? GEMM_ADD : GEMM_STORE;
   g.upper = 1; g.mirror = 1;
   int* flags = (workspace && workspace_bytes >= pt2q_gram_flags_ints(m) * sizeof(int))
                    ? (int*)workspace : nullptr;

@@ -327,8 +327,17 @@ __global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, in
     upper_tile(tl, T, ti, tj);
     const int i0 = ti * BM, j0 = tj * BN;
     Frag<BM, BN> F;
-    if (seg == 0) {
+    if (seg == 0 && g.mode != GEMM_CHAIN_POS) {
       F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
+    } else if (seg == 0) {
+      // continue mode: segment 0 extends the chains already held in C
+      F.for_each(i0, j0, [&](float& a, int row, int col) {
+        bool in = row < g.M && col < g.N;
+        a = g.C[in ? (long)row * g.ldc + col : 0];
+      });
+      F.for_each(i0, j0, [&](float& a, int row, int col) {
+        if (!(row < g.M && col < g.N)) a = 0.0f;
+      });
     } else {
       if (threadIdx.x == 0) {
         long spins = 0;
@@ -432,12 +441,21 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
   const int P = cus * per_cu;  // one resident wave of workgroups (correctness does not need it)
-  // segments: enough units for >= 12 rounds, segment >= 2048 rows, multiple of 2*BK
-  int nseg = (int)std::ceil(12.0 * P / ntile);
-  int seglen = ceil_div(g.K, nseg);
-  if (seglen < 2048) seglen = 2048;
-  seglen = ceil_div(seglen, 2 * BK) * 2 * BK;
-  nseg = ceil_div(g.K, seglen);
+  // segment length (>= 2048 rows, multiple of 2*BK): minimise the makespan estimate
+  // rounds(units / P) * (seglen + per-unit overhead of ~256 rows: partial reload/store, wait)
+  int nseg = 1, seglen = ceil_div(g.K, 2 * BK) * 2 * BK;
+  double best = 1e300;
+  for (int s = 1; s <= 256; ++s) {
+    int len = ceil_div(ceil_div(g.K, s), 2 * BK) * 2 * BK;
+    if (s > 1 && len < 2048) break;
+    const int ns = ceil_div(g.K, len);
+    const double cost = std::ceil((double)ntile * ns / P) * (len + 256.0);
+    if (cost < best * 0.999) {
+      best = cost;
+      nseg = ns;
+      seglen = len;
+    }
+  }
   if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2), st) != hipSuccess) return PT2Q_E_HIP;
   int* timeout = flags + ntile;
   hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
@@ -473,7 +491,7 @@ int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st) {
   const long ntile = (long)T * (T + 1) / 2;
   static const char* mode = std::getenv("PT2Q_GRAM_STREAMK");
   const bool allow = !(mode && mode[0] == '0');
-  if (flags && allow && g.mode == GEMM_STORE && g.upper && g.mirror && g.M == g.N &&
+  if (flags && allow && (g.mode == GEMM_STORE || g.mode == GEMM_CHAIN_POS) && g.upper && g.mirror && g.M == g.N &&
       ntile >= 128 && g.K >= 16384) {
     switch (g.in_dtype) {
       case PT2Q_F32:

@@ -36,16 +36,24 @@ class LayerOutput:
     spd: bool = True
 
 
-def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
-    """XᵀX (main.py:128) or G += XᵀX (gptq.py:75), X (N, m) or (B, L, m)."""
+def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate=False,
+         workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """XᵀX (main.py:128), X (N, m) or (B, L, m).
+
+    accumulate=False: G = XᵀX.  True: G = G + XᵀX (gptq.py:75 add_batch).  "continue": every
+    entry's fp32 chain resumes from G, so a Gram streamed batch by batch is bit-identical to one
+    Gram of the concatenated rows (the captured-and-concatenated X of main.py:293)."""
     X = _float_input(X.reshape(-1, X.shape[-1]))
     N, m = X.shape
     if G is None:
         G = torch.empty((m, m), dtype=torch.float32, device=X.device)
         accumulate = False
-    ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), X.device)
+    mode = 2 if accumulate == "continue" else int(bool(accumulate))
+    ws = workspace
+    if ws is None or ws.numel() < _lib.lib().pt2q_gram_workspace_bytes(m):
+        ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), X.device)
     _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), N, m, m, _lib.ptr(G), m,
-                                    int(accumulate), _lib.ptr(ws), ws.numel(),
+                                    mode, _lib.ptr(ws), ws.numel(),
                                     _lib.stream_of(X.device)), "pt2q_gram")
     return G
 
@@ -99,6 +107,31 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: torch.Tens
         _lib.stream_of(dev))
     _lib.check(rc, "pt2q_quantize_blocks")
     return LayerOutput(alpha, mu, T, perm, iters)
+
+
+def hessian_inverse(G: torch.Tensor, nsamples: int, percdamp: float = 0.01):
+    """main.py:129-141 on a raw Gram: damped H, then Hinv (pinv on Cholesky breakdown).
+    Returns (Hinv, spd)."""
+    H, _ = prepare_hessian(G, nsamples, percdamp)
+    Hinv, spd = cholesky_inverse(H)
+    if not spd:
+        Hinv = torch.linalg.pinv(H)
+    return Hinv, spd
+
+
+def quantize_shared(Ws, G: torch.Tensor, nsamples: int, block_size: int = 128,
+                    use_ssr: bool = True, percdamp: float = 0.01, max_iter: int = 100,
+                    t_dtype=torch.int8):
+    """Variant M for several linears that read the same activations (q/k/v, gate/up): one Gram
+    G = XᵀX and one Cholesky inverse, then the block loop per weight.  Each result is
+    bit-identical to quantize_layer(W, X) on that linear alone (same kernels, same inputs)."""
+    Hinv, spd = hessian_inverse(G, nsamples, percdamp)
+    outs = []
+    for W in Ws:
+        out = quantize_blocks(W, G, Hinv, block_size, use_ssr, _lib.AGA_ACT, max_iter, t_dtype)
+        out.spd = spd
+        outs.append(out)
+    return outs
 
 
 class LayerWorkspace:

@@ -1,15 +1,16 @@
 """PT2LLMQuantizer.quantize_layer on MI355X — the reference's CLI hot path (main.py:102-230).
 
-Only the per-layer engine is in scope.  The model-level calibration loop, HF model
-loading and the CLI (main.py:232-433, model.py, utils.py) need network access in the reference
-and are out of scope for this engine; `quantize()` says so instead of silently doing nothing.
+quantize() runs the model-level loop of main.py:232-308 on caller-supplied calibration samples
+(the reference downloads them; there is no network here), streaming each linear's inputs into
+shared Grams (calibration.py).  HF model loading and the CLI (model.py:228-260, main.py:338)
+stay out of scope.
 """
 from typing import Dict
 
 import torch
 import torch.nn as nn
 
-from . import engine
+from . import calibration, engine
 
 
 class PT2LLMQuantizer:
@@ -56,7 +57,32 @@ class PT2LLMQuantizer:
             "perm": out.perm.cpu(),
         }
 
-    def quantize(self):
-        raise NotImplementedError(
-            "model-level calibration (main.py:232-311) needs HF models/datasets over the network and "
-            "is outside this engine's scope; call quantize_layer per linear (see INTEGRATION.md)")
+    def get_calibration_data(self):
+        """main.py:89-99 downloads wikitext through `datasets`; there is no network here, so
+        calibration token tensors must be passed to quantize() explicitly."""
+        raise RuntimeError("pass calibration_samples (list of token-id tensors) to quantize(); "
+                           "dataset download (utils.py:47-60) is not available offline")
+
+    @torch.no_grad()
+    def quantize(self, calibration_samples=None, writeback: str = "reference"):
+        """main.py:232-308: decoder layer by decoder layer, capture the linears' inputs over the
+        calibration forwards, quantise every linear, write the weights back.  The captured
+        inputs go straight into per-input Grams (calibration.GramCapture), so q/k/v and gate/up
+        share one Gram and one Cholesky inverse; results equal quantize_layer on the
+        concatenated activations bit-for-bit.  Returns {name: {alpha, mu, T, perm}} on CPU."""
+        if self.model is None:
+            raise RuntimeError("PT2LLMQuantizer.quantize needs a model")
+        if calibration_samples is None:
+            calibration_samples = self.get_calibration_data()
+        layers = calibration.get_llm_layers(self.model, self.model_type)
+        self.model.eval()
+        for idx, layer in enumerate(layers):
+            def run(cap):
+                for sample in calibration_samples:
+                    self.model(sample.to(self.device))
+                    cap.next_pass()
+            res = calibration.quantize_decoder_layer(layer, run, self.block_size, self.use_ssr,
+                                                     self.percdamp, idx, writeback, self.device)
+            for name, p in res.items():
+                self.quantized_params[name] = {k: v.cpu() for k, v in p.items()}
+        return self.quantized_params

@@ -1,0 +1,88 @@
+"""Calibration capture + shared Grams (reference main.py:232-308).
+
+The streamed Gram must equal the Gram of the concatenated rows bit-for-bit (oracle), shared
+quantisation must equal per-linear quantize_layer, and the model-level loop must reproduce the
+reference's capture-concatenate-quantise-writeback loop exactly (emulated here with the same
+hooks the reference registers, main.py:262-275, and per-linear quantize_layer)."""
+import numpy as np
+import pytest
+import torch
+
+import synth
+from test_gpu_parity import bits_equal, cuda, host
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("splits,m,dt", [((100, 37, 200), 96, torch.float32),
+                                         ((1000, 3000, 16384), 2048, torch.float16)])
+def test_gram_continue_equals_concatenated(pt2q, splits, m, dt):
+    X = synth.activations(21 + m, sum(splits), m)
+    Xd = cuda(X).to(dt)
+    acc = pt2q.GramAccumulator(m, "cuda")
+    s = 0
+    for k in splits:
+        acc.add(Xd[s:s + k])
+        s += k
+    assert acc.nsamples == X.shape[0]
+    assert bits_equal(host(acc.G), orc.gram(host(Xd.float())))
+
+
+def test_quantize_shared_equals_per_linear(pt2q):
+    n1, n2, m, N = 384, 256, 320, 600
+    X = cuda(synth.activations(31, N, m))
+    Ws = [cuda(synth.weights(32, n1, m)), cuda(synth.weights(33, n2, m))]
+    G = pt2q.gram(X)
+    outs = pt2q.quantize_shared(Ws, G, N, 128, True)
+    for W, o in zip(Ws, outs):
+        r = pt2q.quantize_layer(W, X, 128, True)
+        for a, b in ((o.alpha, r.alpha), (o.mu, r.mu), (o.T, r.T), (o.perm, r.perm)):
+            assert bits_equal(host(a), host(b))
+
+
+def _tiny_llama():
+    transformers = pytest.importorskip("transformers")
+    cfg = transformers.LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=384,
+                                   num_hidden_layers=2, num_attention_heads=4,
+                                   num_key_value_heads=4, max_position_embeddings=256)
+    torch.manual_seed(0)
+    return transformers.LlamaForCausalLM(cfg).cuda().eval()
+
+
+def test_model_loop_matches_reference_loop(pt2q):
+    """PT2LLMQuantizer.quantize (Gram capture, shared Hessians) vs the reference's loop shape:
+    capture every input, torch.cat, quantize_layer per linear, _dequantize_weight write-back."""
+    torch.manual_seed(1)
+    samples = [torch.randint(0, 512, (1, 64)) for _ in range(3)]
+
+    model_a = _tiny_llama()
+    q = pt2q.PT2LLMQuantizer(model_a, None, "llama", block_size=128, use_ssr=True)
+    got = q.quantize(samples)
+
+    model_b = _tiny_llama()
+    want = {}
+    with torch.no_grad():
+        for idx, layer in enumerate(model_b.model.layers):
+            acts, hooks = {}, []
+            lins = pt2q.find_linear_layers(layer)
+            for name, lin in lins.items():
+                hooks.append(lin.register_forward_hook(
+                    lambda mod, inp, out, name=name: acts.setdefault(name, []).append(inp[0].detach())))
+            for s in samples:
+                model_b(s.cuda())
+            for h in hooks:
+                h.remove()
+            for name, lin in lins.items():
+                X = torch.cat(acts[name], dim=0)
+                out = pt2q.quantize_layer(lin.weight.data, X, 128, True)
+                p = {"alpha": out.alpha, "mu": out.mu, "T": out.T, "perm": out.perm}
+                want[f"layer_{idx}.{name}"] = p
+                lin.weight.data = pt2q.calibration.dequantize_weight_reference(p, 128).to(lin.weight.dtype)
+    assert set(got) == set(want) and len(got) == 14
+    for k in want:
+        for f in ("alpha", "mu", "T", "perm"):
+            assert bits_equal(host(got[k][f]), host(want[k][f])), (k, f)
+    # the model was written back identically
+    for pa, pb in zip(model_a.parameters(), model_b.parameters()):
+        assert torch.equal(pa, pb)
