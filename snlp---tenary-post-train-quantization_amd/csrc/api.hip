@@ -52,8 +52,9 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
   w.ldw = ldw;
   w.Wt = c.take<float>((size_t)m * ldw);
   w.Tt = c.take<int8_t>((size_t)m * ldw);
-  w.Et = c.take<float>((size_t)bb * ldw);
-  w.Ck = c.take<float>((size_t)bb * m);
+  // E and the feedback coefficients exist only when a block leaves columns behind (B > 1)
+  w.Et = c.take<float>(B > 1 ? (size_t)bb * ldw : 1);
+  w.Ck = c.take<float>(B > 1 ? (size_t)bb * m : 1);
   w.alpha_t = c.take<float>((size_t)B * n);
   w.mu_t = c.take<float>((size_t)B * n);
   w.S1 = c.take<float>((size_t)bb);
@@ -77,8 +78,8 @@ size_t blocks_bytes(int n, int m, int b) {
   const int B = b < m ? ceil_div(m, b) : 1;
   add((size_t)m * ldw * 4);
   add((size_t)m * ldw);
-  add((size_t)bb * ldw * 4);
-  add((size_t)bb * m * 4);
+  add(B > 1 ? (size_t)bb * ldw * 4 : 4);
+  add(B > 1 ? (size_t)bb * m * 4 : 4);
   add((size_t)B * n * 4);
   add((size_t)B * n * 4);
   add((size_t)bb * 4);
@@ -150,7 +151,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     }
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
                                     w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
-                                    w.Et, w.ldw, iters + k, w.counters + 2 * k, st)) != PT2Q_OK)
+                                    nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
+                                    st)) != PT2Q_OK)
       return rc;
     if (nr > 0) {
       if ((rc = pt2q_launch_ef_coeffs(Hinv, ldhi, w.blk, bs, nrem, nr, w.Ck, m, st)) != PT2Q_OK)
@@ -260,7 +262,6 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
   int aga = flags & PT2Q_AGA_MASK;
   if (aga != PT2Q_AGA_NONE && !A) return PT2Q_E_ARG;
   if (aga == PT2Q_AGA_HESS && (b < m ? b : m) > 128) return PT2Q_E_UNSUPPORTED;
-  if ((b < m ? b : m) > 512) return PT2Q_E_UNSUPPORTED;
   Carve c{(char*)workspace, workspace_bytes};
   BlockWs w;
   if (!carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
@@ -277,7 +278,6 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
   hipStream_t st = (hipStream_t)stream;
   if (!W || !X || !info_dev || N <= 0 || m <= 0 || n <= 0 || b <= 0 || !dtype_ok(xdtype))
     return PT2Q_E_ARG;
-  if ((b < m ? b : m) > 512) return PT2Q_E_UNSUPPORTED;
   Carve c{(char*)workspace, workspace_bytes};
   float* G = c.take<float>((size_t)m * m);
   float* H = c.take<float>((size_t)m * m);
@@ -292,8 +292,14 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
                      pt2q_gram_flags_ints(m) * sizeof(int), stream)) != PT2Q_OK)
     return rc;
   if ((rc = pt2q_launch_prepare_hessian(G, m, m, N, percdamp, H, m, damp, st)) != PT2Q_OK) return rc;
-  // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G)
-  if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st)) != PT2Q_OK) return rc;
+  // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G).
+  // Hinv only feeds the error feedback; a single block (per-channel, b >= m) has none, so the
+  // factorisation would be dead work: skip it and report success.
+  if (b < m) {
+    if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st)) != PT2Q_OK) return rc;
+  } else if (hipMemsetAsync(info_dev, 0, sizeof(int), st) != hipSuccess) {
+    return PT2Q_E_HIP;
+  }
   int f = (flags & ~PT2Q_AGA_MASK) | PT2Q_AGA_ACT;
   return run_blocks(W, wdtype, ldw, n, m, b, f, G, m, Hinv, m, max_iter, alpha, mu, T, tdtype,
                     perm, iters_dev, w, st);

@@ -191,7 +191,7 @@ PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count
     if (R.has(s)) {
       int k = l + 16 * s;
       A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
-      A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
+      if (A.Et) A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
     }
 }
 
@@ -322,6 +322,304 @@ __global__ void count_zero_rows_kernel(const float* T, long ldt, int n, int b, i
   if (z) atomicAdd(out, 1);
 }
 
+// ----------------------------------------------------------------- wide blocks (b > 512)
+//
+// Per-channel quantisation (block_size = m, BASELINE config 5) makes a block as wide as the
+// layer (5120 .. 13824 columns): a row no longer fits in registers.  Here ONE LANE OWNS ONE ROW
+// (64 rows per wave) and streams the row's columns from HBM/L2 on every pass, keeping only the
+// 16 residue-class partials of the canonical SUM16 in registers; fold16() applies the same
+// xor-8/4/2/1 butterfly to them, so every value is bit-identical to the 16-lane kernels and to
+// the oracle.  The codes live in the output array T itself between passes.  Each round pass
+// also accumulates the next grid's partials from the codes it just wrote (same values, same
+// order), so an ITF iteration costs one pass over W and T.
+
+PT2Q_DEV float fold16(const float (&p)[16]) {
+  float q[8], r[4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = p[j] + p[j + 8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = q[j] + q[j + 4];
+  float s0 = r[0] + r[2], s1 = r[1] + r[3];
+  return s0 + s1;
+}
+
+struct WideArgs {
+  int mode;          // PT2Q_STAGE_* ; BLOCK = fused init+ITF+AGA+E of the block loop
+  const float* W;    // FM: Wt[col * ldw + i] (feature-major); RM: W[i * ldw + k]
+  long ldw;
+  int n, b;
+  const int* blk;    // FM: b column indices (selection order); RM: unused
+  const float* S1;
+  const float* d;
+  int max_iter;
+  float* alpha;
+  float* mu;
+  void* T;           // FM: int8 Tt[col * ldt + i]; RM: float T[i * ldt + k]
+  long ldt;
+  float* Et;         // FM: b x lde error term, nullable
+  long lde;
+  int* iters;
+  int* counters;     // [0] all-zero init rows, [1] workgroups done
+  int pass;          // STAGE_FULL: 0 = init + count, 1 = finish
+};
+constexpr int MODE_BLOCK = 100;
+
+template <bool FM>
+struct WideRow {
+  const WideArgs& A;
+  int i;
+  bool valid;
+  PT2Q_DEV long col(int k) const { return FM ? (long)A.blk[k] : (long)k; }
+  PT2Q_DEV float w(int k) const {
+    if (!valid) return 0.0f;
+    return FM ? A.W[col(k) * A.ldw + i] : A.W[(long)i * A.ldw + k];
+  }
+  PT2Q_DEV float t(int k) const {
+    if (!valid) return 0.0f;
+    return FM ? (float)((const int8_t*)A.T)[col(k) * A.ldt + i] : ((const float*)A.T)[(long)i * A.ldt + k];
+  }
+  PT2Q_DEV void set_t(int k, float v) const {
+    if (!valid) return;
+    if (FM) ((int8_t*)A.T)[col(k) * A.ldt + i] = (int8_t)v;
+    else ((float*)A.T)[(long)i * A.ldt + k] = v;
+  }
+};
+
+// SUM16 over the row of one lane: f(k) gives the k-th term.
+template <typename F>
+PT2Q_DEV float wide_sum(int b, F&& f) {
+  float p[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) p[j] = 0.0f;
+  int k0 = 0;
+  for (; k0 + 16 <= b; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) p[j] = p[j] + f(k0 + j);
+  }
+  for (int j = 0; k0 + j < b; ++j) p[j] = p[j] + f(k0 + j);
+  return fold16(p);
+}
+
+struct Grid3 {
+  float wt[16], t[16], t2[16];
+  PT2Q_DEV void zero() {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wt[j] = t[j] = t2[j] = 0.0f;
+  }
+  PT2Q_DEV void add(int j, float w, float tv) {
+    wt[j] = wt[j] + w * tv;
+    t[j] = t[j] + tv;
+    t2[j] = t2[j] + tv * tv;
+  }
+};
+
+PT2Q_DEV void grid_from(const Grid3& G, float fb, float wsum, float* a, float* m) {
+  float swt = fold16(G.wt), ts = fold16(G.t), t2 = fold16(G.t2);
+  float den = clampmin(fb * t2 - ts * ts);
+  *a = (fb * swt - ts * wsum) / den;
+  *m = (t2 * wsum - ts * swt) / den;
+}
+
+template <bool FM>
+PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, int b, Grid3& G) {
+  G.zero();
+  int k0 = 0;
+  for (; k0 + 16 <= b; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) G.add(j, R.w(k0 + j), R.t(k0 + j));
+  }
+  for (int j = 0; k0 + j < b; ++j) G.add(j, R.w(k0 + j), R.t(k0 + j));
+}
+
+// flexible_round over the row, writing T; accumulates the next grid's partials. Returns changed.
+template <bool FM>
+PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, int b, float a, float m, Grid3& G) {
+  const float as = clampmin(a);
+  bool changed = false;
+  G.zero();
+  auto one = [&](int k, int j) {
+    float w = R.w(k), old = R.t(k);
+    float z = (w - m) / as;
+    float nt = (z > 0.5f) ? 1.0f : ((z < -0.5f) ? -1.0f : 0.0f);
+    if (nt != old) {
+      changed = true;
+      R.set_t(k, nt);
+    }
+    G.add(j, w, nt);
+  };
+  int k0 = 0;
+  for (; k0 + 16 <= b; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) one(k0 + j, j);
+  }
+  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
+  return changed;
+}
+
+// ternary_init; writes T. Returns whether the row's codes are all zero.
+template <bool FM>
+PT2Q_DEV bool wide_init(const WideRow<FM>& R, int b, float wsum, float* a, float* m) {
+  const float fb = (float)b;
+  const float mu = wsum / fb;
+  float delta = 0.75f * (wide_sum(b, [&](int k) { return fabsf(R.w(k) - mu); }) / fb);
+  float pn[16], pd[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pn[j] = pd[j] = 0.0f;
+  auto one = [&](int k, int j) {
+    float wc = R.w(k) - mu;
+    float t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
+    R.set_t(k, t);
+    pn[j] = pn[j] + t * wc;
+    pd[j] = pd[j] + fabsf(t);
+  };
+  int k0 = 0;
+  for (; k0 + 16 <= b; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) one(k0 + j, j);
+  }
+  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
+  float num = fold16(pn), cnt = fold16(pd);
+  *a = num / clampmin(cnt);
+  *m = mu;
+  return cnt == 0.0f;
+}
+
+template <bool FM>
+PT2Q_DEV int wide_itf(const WideRow<FM>& R, int b, float wsum, int max_iter, float* a, float* m) {
+  Grid3 G;
+  wide_grid_pass(R, b, G);
+  int it = 0;
+  bool any = true;
+  for (; it < max_iter; ++it) {
+    if (!any) break;
+    grid_from(G, (float)b, wsum, a, m);
+    bool ch = wide_round_pass(R, b, *a, *m, G);
+    any = __any(ch);
+  }
+  return it;
+}
+
+template <bool FM>
+PT2Q_DEV void wide_aga(const WideRow<FM>& R, int b, const float* S1, float d, float* a, float* m) {
+  float pv[16], pws[16], pwts[16], pt2s[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pv[j] = pws[j] = pwts[j] = pt2s[j] = 0.0f;
+  auto one = [&](int k, int j) {
+    float t = R.t(k), w = R.w(k), c = S1[k];
+    pv[j] = fmaf(t, c, pv[j]);
+    pws[j] = fmaf(w, c, pws[j]);
+    pwts[j] = fmaf(w * t, c, pwts[j]);
+    pt2s[j] = fmaf(t * t, c, pt2s[j]);
+  };
+  int k0 = 0;
+  for (; k0 + 16 <= b; k0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) one(k0 + j, j);
+  }
+  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
+  float v = fold16(pv), ws1 = fold16(pws), wts1 = fold16(pwts), t2s1 = fold16(pt2s);
+  float v2 = v * v;
+  float den = clampmin(d * t2s1 - v2);
+  *a = (d * wts1 - v * ws1) / den;
+  *m = (t2s1 * ws1 - v * wts1) / den;
+}
+
+// Block-loop mode for rows [row0, row0 + 64): init -> ITF -> AGA -> E.
+template <bool FM>
+PT2Q_DEV void wide_block_rows(const WideArgs& A, int row0, bool skip_itf, bool count_zero) {
+  const int lane = threadIdx.x & 63;
+  WideRow<FM> R{A, row0 + lane, row0 + lane < A.n};
+  const int b = A.b;
+  float wsum = wide_sum(b, [&](int k) { return R.w(k); });
+  float a, m;
+  bool zero = wide_init(R, b, wsum, &a, &m);
+  if (count_zero && R.valid && zero) atomicAdd(&A.counters[0], 1);
+  int it = 0;
+  if (!skip_itf) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
+  if (A.S1) wide_aga(R, b, A.S1, *A.d, &a, &m);
+  if (A.iters && lane == 0 && !skip_itf) atomicMax(A.iters, it);
+  if (!R.valid) return;
+  A.alpha[R.i] = a;
+  A.mu[R.i] = m;
+  if (A.Et)
+    for (int k = 0; k < b; ++k) A.Et[(long)k * A.lde + R.i] = R.w(k) - (a * R.t(k) + m);
+}
+
+// One wave (64 rows) per workgroup: few rows per layer, so spread them over CUs.
+template <bool FM>
+__global__ __launch_bounds__(64) void atq_wide_block_kernel(WideArgs A) {
+  wide_block_rows<FM>(A, blockIdx.x * 64, false, true);
+  // whole-block T_init == 0 repair by the last workgroup (see atq_block_kernel)
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ticket = __hip_atomic_fetch_add(&A.counters[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (ticket == (int)gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  int zero_rows = __hip_atomic_load(&A.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (zero_rows != A.n) return;
+  if (A.iters && threadIdx.x == 0) *A.iters = 0;
+  for (int row0 = 0; row0 < A.n; row0 += 64) wide_block_rows<FM>(A, row0, true, false);
+}
+
+// Per-method stages on row-major W / float T (quantizer.py surface) for b > 512.
+__global__ __launch_bounds__(64) void atq_wide_stage_kernel(WideArgs A) {
+  const int lane = threadIdx.x & 63;
+  WideRow<false> R{A, (int)blockIdx.x * 64 + lane, (int)blockIdx.x * 64 + lane < A.n};
+  const int b = A.b;
+  float wsum = wide_sum(b, [&](int k) { return R.w(k); });
+  float a = R.valid ? A.alpha[R.i] : 0.0f, m = R.valid ? A.mu[R.i] : 0.0f;
+  int it = 0;
+  bool write_am = true;
+  switch (A.mode) {
+    case PT2Q_STAGE_INIT:
+      wide_init(R, b, wsum, &a, &m);
+      break;
+    case PT2Q_STAGE_GRID: {
+      Grid3 G;
+      wide_grid_pass(R, b, G);
+      grid_from(G, (float)b, wsum, &a, &m);
+      break;
+    }
+    case PT2Q_STAGE_ROUND: {
+      Grid3 G;
+      wide_round_pass(R, b, a, m, G);
+      write_am = false;
+      break;
+    }
+    case PT2Q_STAGE_ITF:
+      if (*A.counters != A.n) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
+      break;
+    case PT2Q_STAGE_AGA:
+      wide_aga(R, b, A.S1, *A.d, &a, &m);
+      break;
+    case PT2Q_STAGE_FULL: {
+      bool zero = wide_init(R, b, wsum, &a, &m);
+      if (A.pass == 0) {
+        if (R.valid && zero) atomicAdd(A.counters, 1);
+        return;
+      }
+      if (*A.counters != A.n) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
+      if (A.S1) wide_aga(R, b, A.S1, *A.d, &a, &m);
+      break;
+    }
+  }
+  if (A.iters && lane == 0) atomicMax(A.iters, it);
+  if (R.valid && write_am) {
+    A.alpha[R.i] = a;
+    A.mu[R.i] = m;
+  }
+}
+
 template <typename F>
 int dispatch_ns(int b, F&& f) {
   if (b <= 128) return f(std::integral_constant<int, 8>{});
@@ -338,6 +636,13 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st) {
+  if (b > 512) {
+    WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
+                iters, counters, 0};
+    hipLaunchKernelGGL(atq_wide_block_kernel<true>, dim3(ceil_div(n, 64)), dim3(64), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters};
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
@@ -359,6 +664,7 @@ extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int 
       (!workspace || workspace_bytes < sizeof(int)))
     return PT2Q_E_WORKSPACE;
   int* zero_rows = (int*)workspace;
+  const float* Wp = W;
   int grid = ceil_div(n, ROWS_PER_WG);
   StageArgs A{mode, W, ldw, n, b, alpha, mu, T, ldt, S1, d_dev, max_iter, iters_dev, zero_rows, 0};
   if (iters_dev && (mode == PT2Q_STAGE_ITF || mode == PT2Q_STAGE_FULL))
@@ -368,6 +674,20 @@ extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int 
     hipLaunchKernelGGL(count_zero_rows_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, T, ldt,
                        n, b, zero_rows);
     PT2Q_LAUNCH_CHECK();
+  }
+  if (b > 512) {
+    WideArgs WA{mode, Wp, ldw, n, b, nullptr, S1, d_dev, max_iter, alpha, mu, T,
+                ldt, nullptr, 0, iters_dev, zero_rows, 0};
+    const int wgrid = ceil_div(n, 64);
+    if (mode == PT2Q_STAGE_FULL) {
+      if (hipMemsetAsync(zero_rows, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+      hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64), 0, st, WA);
+      PT2Q_LAUNCH_CHECK();
+      WA.pass = 1;
+    }
+    hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
   }
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;

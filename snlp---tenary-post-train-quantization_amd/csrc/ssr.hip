@@ -279,6 +279,33 @@ __global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, lo
   }
 }
 
+// Wide blocks (b > 512, per-channel): S1[j] = sequential row sum of A[blk_j][blk_l] over l, one
+// thread per j across many workgroups (the same order as aga_s1_kernel), then d in order.
+__global__ __launch_bounds__(256) void s1_rows_kernel(const float* A, long lda, const int* blk,
+                                                      int b, float* S1) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= b) return;
+  const float* row = A + (long)(blk ? blk[j] : j) * lda;
+  float s = 0.0f;
+  int l = 0;
+  for (; l + 8 <= b; l += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = row[blk ? blk[l + u] : l + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = s + v[u];
+  }
+  for (; l < b; ++l) s = s + row[blk ? blk[l] : l];
+  S1[j] = s;
+}
+
+__global__ void s1_total_kernel(const float* S1, int b, float* d) {
+  if (threadIdx.x != 0) return;
+  float dd = 0.0f;
+  for (int j = 0; j < b; ++j) dd = dd + S1[j];
+  *d = dd;
+}
+
 // C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k])   (main.py:201-209)
 __global__ __launch_bounds__(256) void ef_coeff_kernel(const float* Hinv, long ldh,
                                                        const int* blk, const int* rem, int nr,
@@ -342,6 +369,13 @@ int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int*
 
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st) {
+  if (src == 1 && b > 512) {
+    hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, 256)), dim3(256), 0, st, A, lda, blk, b, S1);
+    PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(s1_total_kernel, dim3(1), dim3(64), 0, st, S1, b, d);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   size_t lds = (size_t)b * sizeof(float);
   if (src == 2) lds += 2 * (size_t)b * (b + 1) * sizeof(float);
   else if (b <= 128) lds += (size_t)b * (b + 1) * sizeof(float) + (size_t)b * sizeof(int);

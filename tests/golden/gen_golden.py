@@ -256,10 +256,26 @@ def gen_examples():
          out_err_aga=ox1, T_itf=T1.numpy().astype(np.int8))
 
 
+def gen_wide():
+    print("wide-block fixtures (b > 512: per-channel, BASELINE config 5 shape class)")
+    cases = [
+        ("layer_m_perchannel_640x1024_n2048", 640, 1024, 2048, True, 1024, True),
+        ("layer_m_wide_320x1600_b640_n1024", 320, 1600, 1024, True, 640, True),
+    ]
+    for name, n, m, N, ssr, bs, outl in cases:
+        ws, xs = 1 + n, 2 + m
+        W = synth.weights(ws, n, m)
+        X = synth.activations(xs, N, m, outliers=outl)
+        r = ref_layer_m(W, X, ssr, bs)
+        save(name, variant="M", n=n, m=m, N=N, wseed=ws, xseed=xs, outliers=outl, use_ssr=ssr,
+             block_size=bs, alpha=r["alpha"].numpy(), mu=r["mu"].numpy(),
+             T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
+
+
+GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
+              "trace": gen_trace, "examples": gen_examples, "wide": gen_wide}
+
 if __name__ == "__main__":
-    gen_layers()
-    gen_atq()
-    gen_ssr()
-    gen_hessian()
-    gen_trace()
-    gen_examples()
+    # `python gen_golden.py [group ...]` regenerates only the named groups (default: all)
+    for g in (sys.argv[1:] or list(GENERATORS)):
+        GENERATORS[g]()
