@@ -378,6 +378,217 @@ __global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, in
   }
 }
 
+// ------------------------------------------------------------------ 16-bit Gram, LDS-DMA staged
+//
+// fp16/bf16 X (m % 8 == 0): operand tiles go global -> LDS directly (global_load_lds_dwordx4,
+// no VGPR staging) in their 16-bit form, double-buffered with BK = 64, and are widened to fp32
+// as each lane reads its MFMA operand.  The MFMA row of lane li in sub-tile rm is output row
+// 2*li + rm (a relabeling of the 64 rows a wave owns), so one ds_read_b32 yields both rm (or rn)
+// operands.  LDS image: row k = 256 B = 16 chunks of 8 elements, chunk c stored at c ^ 8*(k&1)
+// so the two k-rows of a k-pair land in different bank halves.  Accumulation is the same f32
+// MFMA k-ascending chain as every other path (bit-identical results).
+constexpr int G16_BK = 64;
+constexpr int G16_ROWB = 256;                 // bytes per k-row (128 elements)
+constexpr int G16_TILEB = G16_BK * G16_ROWB;  // 16 KiB per operand per stage
+#ifndef G16_SB
+#define G16_SB 8
+#endif
+
+template <bool BF16>
+PT2Q_DEV float h2f(uint32_t h) {
+  if constexpr (BF16) {
+    return __uint_as_float(h << 16);
+  } else {
+    _Float16 v;
+    uint16_t u = (uint16_t)h;
+    __builtin_memcpy(&v, &u, 2);
+    return (float)v;
+  }
+}
+
+// Stage one operand tile (k rows [k0, k0+64) x columns [d0, d0+128)) into lds (16 KiB).
+// Each wave issues 4 wave-instructions of 1 KiB; out-of-range chunks read 16 zero bytes.
+PT2Q_DEV void g16_stage(const uint16_t* X, long ld, int d0, int k0, int kend, int M,
+                        uint8_t* lds, const uint16_t* zeros) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave * 4 + j;               // wave-instruction index 0..15
+    const int p = q * 64 + lane;              // LDS chunk index 0..1023
+    const int k = p >> 4, phys = p & 15;
+    const int c = phys ^ ((k & 1) << 3);      // logical chunk held at this position
+    const int gk = k0 + k, gd = d0 + c * 8;
+    const uint16_t* src = (gk < kend && gd < M) ? X + (long)gk * ld + gd : zeros;
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(lds + q * 1024), 16, 0, 0);
+  }
+}
+
+template <bool BF16>
+struct G16Tile {
+  f32x16 acc[2][2];
+  // output coordinates of accumulator element r of sub-tile (rm, rn)
+  PT2Q_DEV static int row(int i0, int rm, int r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, lk = lane >> 5;
+    return i0 + wr * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lk) + rm;
+  }
+  PT2Q_DEV static int col(int j0, int rn) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wc = wave & 1, li = lane & 31;
+    return j0 + wc * 64 + 2 * li + rn;
+  }
+  template <typename F>
+  PT2Q_DEV void for_each(int i0, int j0, F&& f) {
+#pragma unroll
+    for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[rm][rn][r];
+          f(v, row(i0, rm, r), col(j0, rn));
+          acc[rm][rn][r] = v;
+        }
+  }
+
+  // chains over k in [kbeg, kend); As/Bs: 2 stages of 16 KiB each
+  PT2Q_DEV void mma(const GemmDesc& g, int i0, int j0, int kbeg, int kend, uint8_t* As,
+                    uint8_t* Bs, const uint16_t* zeros) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
+    const uint16_t* X = (const uint16_t*)g.A;
+    const bool same = (i0 == j0);  // diagonal tile: one panel serves both operands
+    // byte offsets of this lane's operand pairs within a stage (k-row 2s+lk added per step)
+    const int offA = ((wr * 8 + (li >> 2)) ^ (lk << 3)) * 16 + (li & 3) * 4 + lk * G16_ROWB;
+    const int offB = ((wc * 8 + (li >> 2)) ^ (lk << 3)) * 16 + (li & 3) * 4 + lk * G16_ROWB;
+    const int ntile = (kend - kbeg + G16_BK - 1) / G16_BK;
+    if (ntile <= 0) return;
+    g16_stage(X, g.lda, i0, kbeg, kend, g.M, As, zeros);
+    if (!same) g16_stage(X, g.lda, j0, kbeg, kend, g.M, Bs, zeros);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < ntile; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < ntile) {
+        const int nb = (t + 1) & 1;
+        g16_stage(X, g.lda, i0, kbeg + (t + 1) * G16_BK, kend, g.M, As + nb * G16_TILEB, zeros);
+        if (!same)
+          g16_stage(X, g.lda, j0, kbeg + (t + 1) * G16_BK, kend, g.M, Bs + nb * G16_TILEB, zeros);
+      }
+      const uint8_t* a = As + cur * G16_TILEB + offA;
+      const uint8_t* b = (same ? As : Bs) + cur * G16_TILEB + offB;
+      // operand pairs are read a batch ahead of the MFMAs that consume them
+      constexpr int SB = G16_SB;
+      uint32_t pa[SB], pb[SB];
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        pa[u] = *(const uint32_t*)(a + u * 2 * G16_ROWB);
+        pb[u] = *(const uint32_t*)(b + u * 2 * G16_ROWB);
+      }
+#pragma unroll
+      for (int s0 = 0; s0 < G16_BK / 2; s0 += SB) {
+        uint32_t qa[SB], qb[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          qa[u] = pa[u];
+          qb[u] = pb[u];
+        }
+        if (s0 + SB < G16_BK / 2) {
+#pragma unroll
+          for (int u = 0; u < SB; ++u) {
+            pa[u] = *(const uint32_t*)(a + (s0 + SB + u) * 2 * G16_ROWB);
+            pb[u] = *(const uint32_t*)(b + (s0 + SB + u) * 2 * G16_ROWB);
+          }
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const float a0 = h2f<BF16>(qa[u] & 0xffffu), a1 = h2f<BF16>(qa[u] >> 16);
+          const float b0 = h2f<BF16>(qb[u] & 0xffffu), b1 = h2f<BF16>(qb[u] >> 16);
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+};
+
+// Persistent segmented-K Gram over 16-bit X, same unit scheme as gram_streamk_kernel.
+template <bool BF16>
+__global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, int nseg,
+                                                             int seglen, int* flags, int* timeout,
+                                                             const uint16_t* zeros) {
+  constexpr int BM = 128, BN = 128;
+  // ONE __shared__ object: a second one beside the DMA staging makes hipcc wait vmcnt(0)
+  // before every k-step's first ds_read (cdna_hip_programming.md §5, trap 4a)
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * G16_TILEB + 64];
+  uint8_t* As = smem;
+  uint8_t* Bs = smem + 2 * G16_TILEB;
+  long& s_unit = *(long*)(smem + 4 * G16_TILEB);
+  const int ntile = T * (T + 1) / 2;
+  const long units = (long)ntile * nseg;
+  int* counter = timeout + 1;
+  for (;;) {
+    if (threadIdx.x == 0) s_unit = atomicAdd(counter, 1);
+    __syncthreads();
+    const long u = s_unit;
+    __syncthreads();
+    if (u >= units) break;
+    const int seg = (int)(u / ntile), tl = (int)(u % ntile);
+    int ti, tj;
+    upper_tile(tl, T, ti, tj);
+    const int i0 = ti * BM, j0 = tj * BN;
+    G16Tile<BF16> F;
+    if (seg == 0 && g.mode != GEMM_CHAIN_POS) {
+      F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
+    } else {
+      if (seg > 0 && threadIdx.x == 0) {
+        long spins = 0;
+        while (__hip_atomic_load(&flags[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seg) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1l << 28)) {
+            atomicExch(timeout, 1);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      F.for_each(i0, j0, [&](float& a, int row, int col) {
+        bool in = row < g.M && col < g.N;
+        a = g.C[in ? (long)row * g.ldc + col : 0];
+      });
+      F.for_each(i0, j0, [&](float& a, int row, int col) {
+        if (!(row < g.M && col < g.N)) a = 0.0f;
+      });
+    }
+    const int kbeg = seg * seglen, kend = min(g.K, kbeg + seglen);
+    F.mma(g, i0, j0, kbeg, kend, As, Bs, zeros);
+    const bool last = (seg == nseg - 1);
+    const bool mirror = last && (ti != tj);
+    F.for_each(i0, j0, [&](float& a, int row, int col) {
+      if (row >= g.M || col >= g.N) return;
+      g.C[(long)row * g.ldc + col] = a;
+      if (mirror) g.C[(long)col * g.ldc + row] = a;
+    });
+    if (!last) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[tl], seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, typename TIn>
 bool vec_ok(const GemmDesc& g) {
   const int vw = 16 / (int)sizeof(TIn);
@@ -438,8 +649,18 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   int dev = 0, cus = 256, per_cu = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   auto kern = vec_ok<128, 128, TIn>(g) ? gram_streamk_kernel<TIn, true> : gram_streamk_kernel<TIn, false>;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1)
+  // 16-bit inputs with 16-byte rows: the LDS-DMA kernel (PT2Q_GRAM_DMA=0 disables)
+  static const char* dma_env = std::getenv("PT2Q_GRAM_DMA");
+  const bool dma = sizeof(TIn) == 2 && vec_ok<128, 128, TIn>(g) && !(dma_env && dma_env[0] == '0');
+  void (*kern16)(GemmDesc, int, int, int, int*, int*, const uint16_t*) =
+      std::is_same<TIn, uint16_t>::value ? gram16_streamk_kernel<true> : gram16_streamk_kernel<false>;
+  if (dma) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern16, 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
+             per_cu < 1) {
     per_cu = 1;
+  }
   const int P = cus * per_cu;  // one resident wave of workgroups (correctness does not need it)
   // segment length (>= 2048 rows, multiple of 2*BK): minimise the makespan estimate
   // rounds(units / P) * (seglen + per-unit overhead of ~256 rows: partial reload/store, wait)
@@ -456,9 +677,20 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
       seglen = len;
     }
   }
-  if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2), st) != hipSuccess) return PT2Q_E_HIP;
+  // flags: ntile tile flags, timeout, unit counter, then 16 zero bytes (aligned) for the DMA
+  static const char* seg_env = std::getenv("PT2Q_GRAM_SEGLEN");  // tuning override
+  if (seg_env && std::atoi(seg_env) >= 64) {
+    seglen = std::atoi(seg_env) / (2 * BK) * (2 * BK);
+    nseg = ceil_div(g.K, seglen);
+  }
+  if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2 + 8), st) != hipSuccess) return PT2Q_E_HIP;
   int* timeout = flags + ntile;
-  hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
+  if (dma) {
+    const uint16_t* zeros = (const uint16_t*)(((uintptr_t)(flags + ntile + 2) + 15) & ~(uintptr_t)15);
+    hipLaunchKernelGGL(kern16, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout, zeros);
+  } else {
+    hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
+  }
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
@@ -481,7 +713,7 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
 
 size_t pt2q_gram_flags_ints(int m) {
   long T = ceil_div(m, 128);
-  return (size_t)(T * (T + 1) / 2 + 2);  // tile flags, timeout, unit counter
+  return (size_t)(T * (T + 1) / 2 + 2 + 8);  // tile flags, timeout, unit counter, zero chunk
 }
 
 // Symmetric Gram C = XᵀX (STORE): balanced persistent kernel when it pays (big K, enough
