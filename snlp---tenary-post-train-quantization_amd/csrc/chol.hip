@@ -17,32 +17,48 @@ namespace {
 
 constexpr int NB = 64;
 
-// The same factorisation in ONE wave: lane c keeps column c of the block in registers
-// (col[r] = D[r][c]); each step publishes row k through LDS (one 64-float row, read back as
-// broadcasts).  Entries below the diagonal are scratch, never written back.  Padding
-// (nb < NB) is an identity block, which leaves the real entries untouched.
-__global__ __launch_bounds__(64) void chol_diag_wave_kernel(float* A, long lda, int p0, int nb,
-                                                            int* info) {
-  __shared__ __attribute__((aligned(16))) float row[2][NB];
-  const int c = threadIdx.x;
-  float col[NB];
+// The diagonal-block factorisation with four waves: wave q keeps rows [16q, 16q+16) of every
+// column in registers (lane c = column c, col[s] = D[16q+s][c]).  Step k: the wave owning row
+// k forms U[k][·] from its registers (U[k][k] = sqrt(D[k][k]) via readlane, U[k][c] =
+// D[k][c]/U[k][k]) and publishes it in LDS (entries c <= k as 0); after ONE barrier every wave
+// applies D[r][c] = fmaf(-U[k][r], U[k][c], D[r][c]) to its rows (an fmaf with a zero factor is
+// an exact no-op, so rows <= k and columns <= k are untouched).  The k loop runs over the four
+// row quarters at run time with 16 unrolled steps inside, which keeps the code small (a fully
+// unrolled 64-step body overflowed the instruction cache and spilled).  Entries below the
+// diagonal are scratch, never written back.  Padding (nb < NB) is an identity block.
+__global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int p0, int nb,
+                                                        int* info) {
+  __shared__ __attribute__((aligned(16))) float urow[2][NB];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  float col[16];
 #pragma unroll
-  for (int r = 0; r < NB; ++r)
-    col[r] = (r < nb && c < nb) ? A[(long)(p0 + r) * lda + p0 + c] : ((r == c) ? 1.0f : 0.0f);
+  for (int s = 0; s < 16; ++s) {
+    const int r = 16 * q + s;
+    col[s] = (r < nb && c < nb) ? A[(long)(p0 + r) * lda + p0 + c] : ((r == c) ? 1.0f : 0.0f);
+  }
+  for (int kq = 0; kq < 4; ++kq) {
 #pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[k]), k));
-    if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
-    const float ukk = sqrtf(dkk);
-    col[k] = (c == k) ? ukk : ((c > k) ? col[k] / ukk : col[k]);
-    row[k & 1][c] = col[k];
-    __syncthreads();
+    for (int ks = 0; ks < 16; ++ks) {
+      const int k = 16 * kq + ks;
+      float* ur = urow[ks & 1];
+      if (q == kq) {
+        const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[ks]), k));
+        if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
+        const float ukk = sqrtf(dkk);
+        col[ks] = (c == k) ? ukk : ((c > k) ? col[ks] / ukk : col[ks]);
+        ur[c] = (c > k) ? col[ks] : 0.0f;
+      }
+      __syncthreads();
+      const float ukc = ur[c];
 #pragma unroll
-    for (int r = k + 1; r < NB; ++r) col[r] = fmaf(-row[k & 1][r], col[k], col[r]);
+      for (int s = 0; s < 16; ++s) col[s] = fmaf(-ur[16 * q + s], ukc, col[s]);
+    }
   }
 #pragma unroll
-  for (int r = 0; r < NB; ++r)
-    if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[r];
+  for (int s = 0; s < 16; ++s) {
+    const int r = 16 * q + s;
+    if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[s];
+  }
 }
 
 constexpr int LPR = 4;           // lanes cooperating on one panel column / inverse row
@@ -146,23 +162,80 @@ __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, 
 
 }  // namespace
 
+namespace {
+
+// A second stream per device for the triangular-inverse chain, which runs beside the
+// factorisation (trtri of column block J needs only rows <= J of U).  Captured into a hipGraph
+// the fork/join become graph edges.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+SideStream* side_stream() {
+  static SideStream ss[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  return &x;
+}
+
+int trtri_block(const float* U, float* Ui, long ld, int m, int c0, hipStream_t st) {
+  int nb = (m - c0 < NB) ? m - c0 : NB;
+  hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div((long)(c0 + nb) * LPR, 256)), dim3(256), 0,
+                     st, U, ld, Ui, ld, c0, nb);
+  PT2Q_LAUNCH_CHECK();
+  int rest = m - c0 - nb;
+  if (rest <= 0) return PT2Q_OK;
+  GemmDesc g{};
+  g.M = c0 + nb; g.N = rest; g.K = nb;
+  g.A = Ui + c0; g.lda = ld; g.a_layout = LAY_ROWMAJOR;                    // (k, j) = Ui[k][c0+j]
+  g.B = U + (long)c0 * ld + c0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;  // (j, i) = U[c0+j][c0+nb+i]
+  g.in_dtype = PT2Q_F32;
+  g.C = Ui + c0 + nb; g.ldc = ld;
+  g.mode = GEMM_CHAIN_POS;
+  return pt2q_launch_gemm(g, st);
+}
+
+}  // namespace
+
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
                                  float* U, float* Ui, int* info, hipStream_t st) {
   const long ld = m;  // U and Ui are packed m x m
   if (hipMemsetAsync(info, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
   hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
                      U, ld, m);
   PT2Q_LAUNCH_CHECK();
+  // Uinv = U^-1 by column blocks, right-looking: Ui[k][i] holds the running chain of every
+  // not-yet-final column; after block J is final, one CHAIN GEMM extends the chains of all
+  // later columns by the terms j in J (ascending), so each element keeps its canonical order.
+  // Block J runs on the side stream as soon as the factorisation has finished rows of block J.
+  SideStream* ss = side_stream();
+  hipStream_t tst = ss ? ss->s : st;
   int rc;
   for (int p0 = 0; p0 < m; p0 += NB) {
     int nb = (m - p0 < NB) ? m - p0 : NB;
-    hipLaunchKernelGGL(chol_diag_wave_kernel, dim3(1), dim3(64), 0, st, U, ld, p0, nb, info);
+    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
     PT2Q_LAUNCH_CHECK();
     int rest = m - p0 - nb;
+    if (rest > 0) {
+      hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div((long)rest * LPR, 256)), dim3(256), 0, st,
+                         U, ld, p0, nb, m);
+      PT2Q_LAUNCH_CHECK();
+    }
+    // rows [p0, p0+nb) of U are final: hand block J to the inverse chain
+    if (ss) {
+      if (hipEventRecord(ss->fork, st) != hipSuccess) return PT2Q_E_HIP;
+      if (hipStreamWaitEvent(tst, ss->fork, 0) != hipSuccess) return PT2Q_E_HIP;
+    }
+    if ((rc = trtri_block(U, Ui, ld, m, p0, tst)) != PT2Q_OK) return rc;
     if (rest <= 0) break;
-    hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div((long)rest * LPR, 256)), dim3(256), 0, st, U,
-                       ld, p0, nb, m);
-    PT2Q_LAUNCH_CHECK();
     GemmDesc g{};
     g.M = rest; g.N = rest; g.K = nb;
     g.A = U + (long)p0 * ld + p0 + nb; g.lda = ld; g.a_layout = LAY_KMAJOR;
@@ -172,25 +245,9 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
     if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
   }
-  // Uinv = U^-1 by column blocks, right-looking: Ui[k][i] holds the running chain of every
-  // not-yet-final column; after block J is final, one CHAIN GEMM extends the chains of all
-  // later columns by the terms j in J (ascending), so each element keeps its canonical order.
-  if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
-  for (int c0 = 0; c0 < m; c0 += NB) {
-    int nb = (m - c0 < NB) ? m - c0 : NB;
-    hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div((long)(c0 + nb) * LPR, 256)), dim3(256), 0,
-                       st, U, ld, Ui, ld, c0, nb);
-    PT2Q_LAUNCH_CHECK();
-    int rest = m - c0 - nb;
-    if (rest <= 0) break;
-    GemmDesc g{};
-    g.M = c0 + nb; g.N = rest; g.K = nb;
-    g.A = Ui + c0; g.lda = ld; g.a_layout = LAY_ROWMAJOR;            // (k, j) = Ui[k][c0+j]
-    g.B = U + (long)c0 * ld + c0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;  // (j, i) = U[c0+j][c0+nb+i]
-    g.in_dtype = PT2Q_F32;
-    g.C = Ui + c0 + nb; g.ldc = ld;
-    g.mode = GEMM_CHAIN_POS;
-    if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
+  if (ss) {
+    if (hipEventRecord(ss->join, tst) != hipSuccess) return PT2Q_E_HIP;
+    if (hipStreamWaitEvent(st, ss->join, 0) != hipSuccess) return PT2Q_E_HIP;
   }
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
   GemmDesc g{};
