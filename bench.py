@@ -187,7 +187,7 @@ def main():
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
                        "n": n, "m": m, "tokens": N, "io_dtype": a.io_dtype, "block_size": bs,
                        "parallelism": f"layer-sharded x{world}" + (", rccl gather" if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": "gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)",
+            "roofline": {"bound": "mfma", "kernel": "gram16_streamk_kernel (symmetric Gram XᵀX: LDS-DMA fp16 staging, f32 MFMA 32x32x2)",
                          "achieved": achieved, "peak": MI355X_F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / MI355X_F32_MFMA_PEAK_TFLOPS, "traffic": None,
                          "avg_launch_ms": gram_ms, "flops_per_launch": gram_flops},

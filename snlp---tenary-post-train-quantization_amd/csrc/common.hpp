@@ -54,6 +54,24 @@ PT2Q_DEV float sumn_lane(const float* v, long n, long stride, int t) {
   return p;
 }
 
+// SUMN of v[0..n) (stride) for a whole workgroup: the vector is first staged in LDS with every
+// lane's loads in flight at once (lds >= n floats), then lanes 0..63 reduce it in the canonical
+// order.  The result is returned to every thread.  Call from all threads of the block.
+template <bool FMA_SQ>
+PT2Q_DEV float block_sumn_lds(const float* v, long n, long stride, float* lds, float* out_slot) {
+  for (long i = threadIdx.x; i < n; i += blockDim.x) lds[i] = v[i * stride];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float p = sumn_lane<FMA_SQ>(lds, n, 1, threadIdx.x);
+    p = bfly64(p);
+    if (threadIdx.x == 0) *out_slot = p;
+  }
+  __syncthreads();
+  return *out_slot;
+}
+
+constexpr int SUMN_LDS_MAX = 12288;  // floats staged in LDS by block_sumn_lds users (48 KiB)
+
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 #define PT2Q_LAUNCH_CHECK()                                      \

@@ -43,8 +43,15 @@ __global__ void hess_scale_kernel(const float* G, long ldg, int m, float fn, flo
 // damp = percdamp * (SUMN(diag H) / m); H_ii += damp   (main.py:132-133, gptq.py:97-98)
 __global__ __launch_bounds__(1024) void hess_damp_kernel(float* H, long ldh, int m, float percdamp,
                                                          float* damp_out) {
-  __shared__ float dmp;
-  if (threadIdx.x < 64) {
+  __shared__ float dmp, tot;
+  __shared__ float stage[SUMN_LDS_MAX];
+  if (m <= SUMN_LDS_MAX) {
+    const float p = block_sumn_lds<false>(H, m, ldh + 1, stage, &tot);
+    if (threadIdx.x == 0) {
+      dmp = percdamp * (p / (float)m);
+      if (damp_out) *damp_out = dmp;
+    }
+  } else if (threadIdx.x < 64) {
     float p = sumn_lane<false>(H, m, ldh + 1, threadIdx.x);
     p = bfly64(p);
     if (threadIdx.x == 0) {

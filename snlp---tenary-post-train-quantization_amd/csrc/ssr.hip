@@ -49,8 +49,12 @@ __global__ __launch_bounds__(256) void ssr_wbar_sum_kernel(const float* part, in
 
 // nw = clamp(sqrt(SUMN fma wbar^2)) ; wn = wbar / nw   (in place)
 __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) {
-  __shared__ float nws;
-  if (threadIdx.x < 64) {
+  __shared__ float nws, tot;
+  __shared__ float stage[SUMN_LDS_MAX];
+  if (n <= SUMN_LDS_MAX) {
+    const float p = block_sumn_lds<true>(wn, n, 1, stage, &tot);
+    if (threadIdx.x == 0) nws = clampmin(sqrtf(p));
+  } else if (threadIdx.x < 64) {
     float p = sumn_lane<true>(wn, n, 1, threadIdx.x);
     p = bfly64(p);
     if (threadIdx.x == 0) nws = clampmin(sqrtf(p));
@@ -299,11 +303,52 @@ __global__ __launch_bounds__(256) void s1_rows_kernel(const float* A, long lda, 
   S1[j] = s;
 }
 
-__global__ void s1_total_kernel(const float* S1, int b, float* d) {
+// Blocks up to 512 columns: one workgroup per row j gathers A[blk_j][blk_l] (all loads in
+// flight at once), then one lane sums them in l order (the aga_s1_kernel order).
+__global__ __launch_bounds__(128) void s1_row_wg_kernel(const float* A, long lda, const int* blk,
+                                                        int b, float* S1) {
+  __shared__ float v[512];
+  const int j = blockIdx.x;
+  const float* row = A + (long)(blk ? blk[j] : j) * lda;
+  for (int l = threadIdx.x; l < b; l += 128) v[l] = row[blk ? blk[l] : l];
+  __syncthreads();
   if (threadIdx.x != 0) return;
+  float s = 0.0f;
+  int l = 0;
+  for (; l + 8 <= b; l += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = v[l + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = s + t[u];
+  }
+  for (; l < b; ++l) s = s + v[l];
+  S1[j] = s;
+}
+
+// d = sequential sum of S1 (j ascending); S1 is staged through LDS in chunks so the serial
+// chain never waits on a global load.
+__global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, float* d) {
+  __shared__ float v[4096];
   float dd = 0.0f;
-  for (int j = 0; j < b; ++j) dd = dd + S1[j];
-  *d = dd;
+  for (int j0 = 0; j0 < b; j0 += 4096) {
+    const int len = min(4096, b - j0);
+    __syncthreads();
+    for (int j = threadIdx.x; j < len; j += 256) v[j] = S1[j0 + j];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int j = 0;
+      for (; j + 8 <= len; j += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = v[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dd = dd + t[u];
+      }
+      for (; j < len; ++j) dd = dd + v[j];
+    }
+  }
+  if (threadIdx.x == 0) *d = dd;
 }
 
 // C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k])   (main.py:201-209)
@@ -369,10 +414,13 @@ int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int*
 
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st) {
-  if (src == 1 && b > 512) {
-    hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, 256)), dim3(256), 0, st, A, lda, blk, b, S1);
+  if (src == 1) {
+    if (b > 512)
+      hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, 256)), dim3(256), 0, st, A, lda, blk, b, S1);
+    else
+      hipLaunchKernelGGL(s1_row_wg_kernel, dim3(b), dim3(128), 0, st, A, lda, blk, b, S1);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(s1_total_kernel, dim3(1), dim3(64), 0, st, S1, b, d);
+    hipLaunchKernelGGL(s1_total_kernel, dim3(1), dim3(256), 0, st, S1, b, d);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }

@@ -20,7 +20,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GRAM = "gram_streamk_kernel"
+GRAM = "streamk_kernel"  # gram16_streamk_kernel (fp16/bf16) or gram_streamk_kernel
 CUS, SIMDS, XCDS = 256, 4, 8
 
 
