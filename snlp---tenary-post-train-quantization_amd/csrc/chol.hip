@@ -10,6 +10,8 @@
 // Blocked right-looking with NB = 64 panels; the trailing updates and the triangular products
 // run on the f32-MFMA GEMM (gemm.hip) whose k-ordered chains keep every element bit-identical
 // to the unblocked definition above (oracle/pt2q_oracle.c).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -34,7 +36,9 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int 
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
     const int r = 16 * q + s;
-    col[s] = (r < nb && c < nb) ? A[(long)(p0 + r) * lda + p0 + c] : ((r == c) ? 1.0f : 0.0f);
+    const bool in = r < nb && c < nb;
+    col[s] = A[in ? (long)(p0 + r) * lda + p0 + c : (long)p0 * lda + p0];  // branch-free loads
+    col[s] = in ? col[s] : ((r == c) ? 1.0f : 0.0f);
   }
   for (int kq = 0; kq < 4; ++kq) {
 #pragma unroll
@@ -65,10 +69,21 @@ constexpr int LPR = 4;           // lanes cooperating on one panel column / inve
 constexpr int SEG = NB / LPR;    // entries owned per lane
 
 // Loads the nb x nb diagonal block at (r0, r0) into D (identity padding beyond nb).
+// (256 threads: all 16 loads of a thread are issued before the first LDS store.)
 PT2Q_DEV void load_diag_block(float (*D)[NB + 4], const float* A, long lda, int r0, int nb) {
-  for (int q = threadIdx.x; q < NB * NB; q += blockDim.x) {
-    int r = q / NB, c = q % NB;
-    D[r][c] = (r < nb && c < nb) ? A[(long)(r0 + r) * lda + r0 + c] : ((r == c) ? 1.0f : 0.0f);
+  constexpr int PER = NB * NB / 256;
+  float v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = threadIdx.x + 256 * u, r = q / NB, c = q % NB;
+    const bool in = r < nb && c < nb;
+    v[u] = A[in ? (long)(r0 + r) * lda + r0 + c : (long)r0 * lda + r0];
+    v[u] = in ? v[u] : ((r == c) ? 1.0f : 0.0f);
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    D[q / NB][q % NB] = v[u];
   }
 }
 
@@ -87,7 +102,9 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int
 #pragma unroll
   for (int s = 0; s < SEG; ++s) {
     int k = sub * SEG + s;
-    x[s] = (valid && k < nb) ? A[(long)(p0 + k) * lda + i] : 0.0f;
+    const bool in = valid && k < nb;
+    x[s] = A[in ? (long)(p0 + k) * lda + i : (long)p0 * lda + p0];  // branch-free loads
+    x[s] = in ? x[s] : 0.0f;
   }
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
@@ -126,7 +143,9 @@ __global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long
 #pragma unroll
   for (int s = 0; s < SEG; ++s) {
     int q = sub * SEG + s;
-    acc[s] = (valid && k < c0 && q < nb) ? Ui[(long)k * ldi + c0 + q] : 0.0f;
+    const bool in = valid && k < c0 && q < nb;
+    acc[s] = Ui[in ? (long)k * ldi + c0 + q : 0];  // branch-free loads
+    acc[s] = in ? acc[s] : 0.0f;
   }
   const int jb = (k > c0) ? k - c0 : 0;  // first in-block j (local)
 #pragma unroll
@@ -164,12 +183,13 @@ __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, 
 
 namespace {
 
-// A second stream per device for the triangular-inverse chain, which runs beside the
-// factorisation (trtri of column block J needs only rows <= J of U).  Captured into a hipGraph
-// the fork/join become graph edges.
+// Two extra streams per device: the triangular-inverse chain (trtri of column block J needs
+// only rows <= J of U) and the bulk trailing update of the factorisation (look-ahead: only the
+// next block row is updated on the critical path).  Captured into a hipGraph the fork/join
+// events become graph edges.
 struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t s = nullptr, bulk = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, bulk_done = nullptr;
 };
 
 SideStream* side_stream() {
@@ -178,11 +198,28 @@ SideStream* side_stream() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   SideStream& x = ss[dev];
   if (!x.s) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&x.bulk, hipStreamNonBlocking) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.bulk_done, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
   }
   return &x;
+}
+
+// U[r0.., c0..] (rows x cols) -= U[p0 + k][r0 + i] * U[p0 + k][c0 + j] over the nb rows of
+// block J (chains continue from U, k ascending).
+int trailing_update(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols,
+                    bool upper, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return PT2Q_OK;
+  GemmDesc g{};
+  g.M = rows; g.N = cols; g.K = nb;
+  g.A = U + (long)p0 * ld + r0; g.lda = ld; g.a_layout = LAY_KMAJOR;
+  g.B = U + (long)p0 * ld + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;
+  g.in_dtype = PT2Q_F32;
+  g.C = U + (long)r0 * ld + c0; g.ldc = ld;
+  g.mode = GEMM_CHAIN_NEG; g.upper = upper ? 1 : 0; g.mirror = 0;
+  return pt2q_launch_gemm(g, st);
 }
 
 int trtri_block(const float* U, float* Ui, long ld, int m, int c0, hipStream_t st) {
@@ -217,37 +254,51 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   // later columns by the terms j in J (ascending), so each element keeps its canonical order.
   // Block J runs on the side stream as soon as the factorisation has finished rows of block J.
   SideStream* ss = side_stream();
-  hipStream_t tst = ss ? ss->s : st;
+  hipStream_t tst = ss ? ss->s : st, bst = ss ? ss->bulk : st;
   int rc;
   for (int p0 = 0; p0 < m; p0 += NB) {
-    int nb = (m - p0 < NB) ? m - p0 : NB;
+    const int nb = (m - p0 < NB) ? m - p0 : NB;
     hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
     PT2Q_LAUNCH_CHECK();
-    int rest = m - p0 - nb;
+    const int rest = m - p0 - nb;
     if (rest > 0) {
       hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div((long)rest * LPR, 256)), dim3(256), 0, st,
                          U, ld, p0, nb, m);
       PT2Q_LAUNCH_CHECK();
     }
-    // rows [p0, p0+nb) of U are final: hand block J to the inverse chain
+    // rows [p0, p0+nb) of U are final: hand block J to the inverse and bulk-update streams
     if (ss) {
       if (hipEventRecord(ss->fork, st) != hipSuccess) return PT2Q_E_HIP;
       if (hipStreamWaitEvent(tst, ss->fork, 0) != hipSuccess) return PT2Q_E_HIP;
     }
     if ((rc = trtri_block(U, Ui, ld, m, p0, tst)) != PT2Q_OK) return rc;
     if (rest <= 0) break;
-    GemmDesc g{};
-    g.M = rest; g.N = rest; g.K = nb;
-    g.A = U + (long)p0 * ld + p0 + nb; g.lda = ld; g.a_layout = LAY_KMAJOR;
-    g.B = U + (long)p0 * ld + p0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;
-    g.in_dtype = PT2Q_F32;
-    g.C = U + (long)(p0 + nb) * ld + p0 + nb; g.ldc = ld;
-    g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
-    if ((rc = pt2q_launch_gemm(g, st)) != PT2Q_OK) return rc;
+    // critical path: the next block row only (its rows got block J-1's terms from the bulk
+    // update of J-1, so wait for that first); the rest of the trailing triangle goes to the
+    // bulk stream, after the bulk update of J-1 (same stream) and panel J (fork event).
+    // Look-ahead (next block row on the critical path, the rest on the bulk stream) measured
+    // slower at m = 4096 (the bulk update then competes with the chain for CUs); opt-in only.
+    static const char* la_env = std::getenv("PT2Q_CHOL_LOOKAHEAD");
+    if (!(la_env && la_env[0] == '1')) {  // one trailing update on the critical path
+      if ((rc = trailing_update(U, ld, p0, nb, p0 + nb, rest, p0 + nb, rest, true, st)) != PT2Q_OK)
+        return rc;
+      continue;
+    }
+    const int nb2 = (rest < NB) ? rest : NB;
+    if (ss && p0 > 0 && hipStreamWaitEvent(st, ss->bulk_done, 0) != hipSuccess) return PT2Q_E_HIP;
+    if ((rc = trailing_update(U, ld, p0, nb, p0 + nb, nb2, p0 + nb, rest, false, st)) != PT2Q_OK)
+      return rc;
+    if (ss && hipStreamWaitEvent(bst, ss->fork, 0) != hipSuccess) return PT2Q_E_HIP;
+    if ((rc = trailing_update(U, ld, p0, nb, p0 + nb + nb2, rest - nb2, p0 + nb + nb2, rest - nb2,
+                              true, bst)) != PT2Q_OK)
+      return rc;
+    if (ss && hipEventRecord(ss->bulk_done, bst) != hipSuccess) return PT2Q_E_HIP;
   }
   if (ss) {
     if (hipEventRecord(ss->join, tst) != hipSuccess) return PT2Q_E_HIP;
     if (hipStreamWaitEvent(st, ss->join, 0) != hipSuccess) return PT2Q_E_HIP;
+    if (hipEventRecord(ss->bulk_done, bst) != hipSuccess) return PT2Q_E_HIP;
+    if (hipStreamWaitEvent(st, ss->bulk_done, 0) != hipSuccess) return PT2Q_E_HIP;
   }
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
   GemmDesc g{};
