@@ -145,6 +145,24 @@ int pt2q_unpack_ternary(const uint8_t* packed, int64_t count, int8_t* T, void* s
 int pt2q_fill_synthetic(float* out, int64_t count, uint64_t seed, float scale, int64_t cols,
                         int outlier_every, float scale_outlier, void* stream);
 
+/* ---- Ternary inference (model.py:17-127 TernaryLinear) ----
+ * y[t][i] = Σ_p Wd[i][p] x[t][g[p]] + bias[i], Wd[i][p] = xdtype(alpha[i][p/bs]·c[i][p] + mu[i][p/bs]).
+ * Positions p are the input columns in block order (P = pt2q_ternary_linear_positions(m),
+ * padded to 128).  pt2q_ternary_pack lays out the 2-bit codes (n x P/4 bytes) and the gather
+ * index g (P int32) once per layer from the quantizer's outputs (T int8 n x m in ORIGINAL column
+ * order, perm int64 m): mode 0 = correct reconstruction (gptq.py:201-230), mode 1 = the
+ * reference TernaryLinear.forward exactly as written (its double permutation, model.py:75-95). */
+size_t pt2q_ternary_linear_positions(int m);
+int pt2q_ternary_pack(const int8_t* T, int64_t ldt, int n, int m, const int64_t* perm, int mode,
+                      uint8_t* codes, int* gather, void* stream);
+/* x: tokens x m (fp16 or bf16, leading dim ldx); alpha, mu: n x B fp32; bias: n fp32 or NULL;
+ * y: tokens x n (ydtype = xdtype or PT2Q_F32). */
+size_t pt2q_ternary_linear_workspace_bytes(int tokens, int n, int m);
+int pt2q_ternary_linear(const void* x, int xdtype, int tokens, int64_t ldx, int n, int m,
+                        const uint8_t* codes, const int* gather, const float* alpha,
+                        const float* mu, int B, int bs, const float* bias, void* y, int ydtype,
+                        int64_t ldy, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

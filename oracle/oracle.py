@@ -286,3 +286,40 @@ def quantize_layer_g(W, Hsum, nsamples, block_size=128, use_ssr=True, percdamp=0
     out["T"] = out["T"].astype(np.float32)
     out["spd"] = spd
     return out
+
+
+def ternary_weight(alpha, mu, T, perm, block_size, compat, dtype=np.float16):
+    """The dense weight a TernaryLinear multiplies by, rounded to the layer dtype.
+
+    compat=True: model.py:97-110 (_dequantize: contiguous blocks of T) followed by the column
+    re-index of forward (model.py:88-90), folded into one effective weight:
+    out = x[..., perm] @ W[:, inv_perm]ᵀ  ==  x @ W_eff^T with W_eff[:, j] = W[:, inv_perm[inv_perm[j]]].
+    compat=False: the correct reconstruction gptq.py:201-230 (block k <-> columns perm[k·b:(k+1)·b]).
+    alpha/mu are rounded to `dtype` first (the reference stores them in the layer dtype), then
+    alpha*t + mu is formed in fp32 and rounded to `dtype` (t in {-1,0,1} makes alpha*t exact)."""
+    a = np.asarray(alpha, np.float32).astype(dtype).astype(np.float32)
+    m_ = np.asarray(mu, np.float32).astype(dtype).astype(np.float32)
+    T = np.asarray(T).astype(np.float32)
+    perm = np.asarray(perm, np.int64)
+    n, m = T.shape
+    bs = block_size if block_size < m else m
+    W = np.zeros((n, m), np.float32)
+    for k in range(a.shape[1]):
+        s, e = k * bs, min((k + 1) * bs, m)
+        cols = np.arange(s, e) if compat else perm[s:e]
+        W[:, cols] = (a[:, k:k + 1] * T[:, cols] + m_[:, k:k + 1]).astype(dtype).astype(np.float32)
+    if compat:
+        inv = np.argsort(perm)
+        W = W[:, inv[inv]]
+    return W
+
+
+def ternary_linear(x, alpha, mu, T, perm, bias, block_size, compat, dtype=np.float16):
+    """TernaryLinear.forward (model.py:75-95): fp32 accumulation of the dtype-rounded operands,
+    output rounded to dtype.  Floating-point: compared with a tolerance."""
+    W = ternary_weight(alpha, mu, T, perm, block_size, compat, dtype)
+    xf = np.asarray(x, np.float32).astype(dtype).astype(np.float64)
+    y = xf.reshape(-1, xf.shape[-1]) @ W.astype(np.float64).T
+    if bias is not None:
+        y = y + np.asarray(bias, np.float32).astype(dtype).astype(np.float64)
+    return y.astype(np.float32).astype(dtype).reshape(*np.shape(x)[:-1], W.shape[0])

@@ -5,7 +5,8 @@ Drop-in for the reference's hot-path surface:
     compute_column_similarity_to_mean, select_next_block_ssr                      (reorder.py)
     GPTQ, GPTQQuantizer                                                            (gptq.py)
     PT2LLMQuantizer.quantize_layer                                                 (main.py)
-    pack_ternary, unpack_ternary                                                   (utils.py)
+    pack_ternary, unpack_ternary, save/load_quantized_model                        (utils.py)
+    TernaryLinear, replace_linear_with_ternary                                     (model.py)
 All compute runs in libpt2q.so (HIP, gfx950); importing fails loudly if it is not built.
 """
 from . import _lib
@@ -15,6 +16,8 @@ from .gptq import GPTQ, GPTQQuantizer
 from .pt2llm import PT2LLMQuantizer
 from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_llm_layers,
                           quantize_decoder_layer)
+from .ternary import (TernaryLinear, load_quantized_model, replace_linear_with_ternary,
+                      save_quantized_model)
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
                      gram, hessian_inverse, pack_ternary, prepare_hessian, quantize_blocks,
                      quantize_layer, quantize_shared, unpack_ternary)
@@ -27,4 +30,5 @@ __all__ = [
     "cholesky_inverse", "quantize_blocks", "quantize_layer", "dequantize", "pack_ternary",
     "unpack_ternary", "fill_synthetic", "hessian_inverse", "quantize_shared", "GramAccumulator",
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
+    "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
 ]

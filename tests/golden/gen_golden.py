@@ -272,8 +272,30 @@ def gen_wide():
              T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
 
 
+def gen_ternary():
+    print("TernaryLinear forward fixtures (model.py:17-127, fp16 on CPU, reference semantics)")
+    import model as rmod
+    for name, n, m, N, bs, tokens in (("ternary_linear_384x512", 384, 512, 256, 128, 15),
+                                      ("ternary_linear_200x1000_pc", 200, 1000, 512, 1000, 4)):
+        ws, xs = 11 + n, 12 + m
+        W = synth.weights(ws, n, m)
+        X = synth.activations(xs, N, m)
+        r = ref_layer_m(W, X, True, bs)
+        torch.manual_seed(n)
+        bias = (torch.randn(n) * 0.1).half()
+        lay = rmod.TernaryLinear(m, n, block_size=bs, bias=True, dtype=torch.float16)
+        lay.set_quantized_params(r["alpha"].half(), r["mu"].half(), r["T"], r["perm"], bias)
+        x = (torch.from_numpy(synth.activations(13 + m, tokens, m)) * 0.5).half()
+        with torch.no_grad():
+            out = lay(x)
+        save(name, n=n, m=m, N=N, wseed=ws, xseed=xs, block_size=bs, alpha=r["alpha"].numpy(),
+             mu=r["mu"].numpy(), T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy(),
+             bias=bias.numpy(), x=x.numpy(), out=out.numpy())
+
+
 GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
-              "trace": gen_trace, "examples": gen_examples, "wide": gen_wide}
+              "trace": gen_trace, "examples": gen_examples, "wide": gen_wide,
+              "ternary": gen_ternary}
 
 if __name__ == "__main__":
     # `python gen_golden.py [group ...]` regenerates only the named groups (default: all)

@@ -247,3 +247,15 @@ def test_oracle_thread_count_invariance():
     b = orc.quantize_layer_m(W, X)
     for k in ("alpha", "mu", "T", "perm"):
         np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("name", ["ternary_linear_384x512", "ternary_linear_200x1000_pc"])
+def test_ternary_linear_oracle_vs_reference(name):
+    """oracle.ternary_linear(compat=True) reproduces the reference TernaryLinear.forward
+    (model.py:75-110, fp16, run on CPU by gen_golden.py).  fp16 output: tolerance = 2 ulp of
+    the output magnitude plus accumulation-order noise."""
+    g = load_golden(name)
+    y = orc.ternary_linear(g["x"], g["alpha"], g["mu"], g["T"], g["perm"], g["bias"],
+                           int(g["block_size"]), compat=True)
+    ref = g["out"].astype(np.float32)
+    np.testing.assert_allclose(y.astype(np.float32), ref, rtol=2e-3, atol=2e-3)
