@@ -518,38 +518,72 @@ struct G16Tile {
   }
 };
 
-// Persistent segmented-K Gram over 16-bit X, same unit scheme as gram_streamk_kernel.
+#ifdef PT2Q_GRAM_PROFILE
+// dev-only (tools/gram_probe.hip): summed per-workgroup cycles [reload+wait, mma, total, wgs]
+__device__ unsigned long long g16_prof[4];
+#endif
+
+// Persistent Gram over 16-bit X with a STATIC balanced split ("stream-K"): the upper tiles, in
+// supertile order, laid end to end along K form one line of ntile*Kp rows of work; workgroup w
+// takes the contiguous range [w*L, (w+1)*L), L >= Kp.  A range is [head: end of tile a0]
+// [full tiles] [tail: start of tile a1].  The workgroup does its tail FIRST (chains from zero,
+// partial tile published in C + flag), then its full tiles, then its head, which continues the
+// chains of tile a0 from the partial workgroup w-1 published at its start: the wait is normally
+// already satisfied, every fp32 chain stays k-ascending and unsplit, and each tile is split at
+// most once.  (Replaces a dynamic unit queue whose flag waits cost ~4 % of the kernel.)
+// The only dependency is on workgroup w-1, which the in-order dispatcher starts first.
 template <bool BF16>
-__global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, int nseg,
-                                                             int seglen, int* flags, int* timeout,
+__global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, int Kp, long L,
+                                                             int* flags, int* timeout,
                                                              const uint16_t* zeros) {
   constexpr int BM = 128, BN = 128;
   // ONE __shared__ object: a second one beside the DMA staging makes hipcc wait vmcnt(0)
   // before every k-step's first ds_read (cdna_hip_programming.md §5, trap 4a)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * G16_TILEB + 64];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * G16_TILEB];
   uint8_t* As = smem;
   uint8_t* Bs = smem + 2 * G16_TILEB;
-  long& s_unit = *(long*)(smem + 4 * G16_TILEB);
   const int ntile = T * (T + 1) / 2;
-  const long units = (long)ntile * nseg;
-  int* counter = timeout + 1;
-  for (;;) {
-    if (threadIdx.x == 0) s_unit = atomicAdd(counter, 1);
-    __syncthreads();
-    const long u = s_unit;
-    __syncthreads();
-    if (u >= units) break;
-    const int seg = (int)(u / ntile), tl = (int)(u % ntile);
+  const long W = (long)ntile * Kp;
+  // no XCD remap here: w-1 must have a lower dispatch index than w (in-order dispatch) so that
+  // the one dependency can never wait on a workgroup that has not been started
+  const int w = blockIdx.x;
+  const long s = (long)w * L, e = min(s + L, W);
+  if (s >= e) return;
+  const int a0 = (int)(s / Kp), k0 = (int)(s % Kp);
+  const int a1 = (int)((e - 1) / Kp), k1 = (int)(e - (long)a1 * Kp);
+#ifdef PT2Q_GRAM_PROFILE
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+  unsigned long long t_wait = 0, t_mma = 0;
+#endif
+  const bool head = k0 > 0;                          // tile a0 rows [k0, ...) after w-1's part
+  const bool tail = k1 < Kp && !(head && a1 == a0);  // tile a1 rows [0, k1), continued by w+1
+  const int f0 = head ? a0 + 1 : a0, f1 = tail ? a1 - 1 : a1;  // full tiles [f0, f1]
+  const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
+  const int npieces = (tail ? 1 : 0) + nfull + (head ? 1 : 0);
+  // one loop body (a lambda called three times was inlined three times: 1 wave/SIMD)
+  for (int q = 0; q < npieces; ++q) {
+    int a, kb, ke;
+    bool from_partial = false;
+    if (tail && q == 0) {
+      a = a1; kb = 0; ke = k1;
+    } else if (head && q == npieces - 1) {
+      a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
+    } else {
+      a = f0 + q - (tail ? 1 : 0); kb = 0; ke = Kp;
+    }
     int ti, tj;
-    upper_tile(tl, T, ti, tj);
+    upper_tile(a, T, ti, tj);
     const int i0 = ti * BM, j0 = tj * BN;
     G16Tile<BF16> F;
-    if (seg == 0 && g.mode != GEMM_CHAIN_POS) {
-      F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
+#ifdef PT2Q_GRAM_PROFILE
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (!from_partial && g.mode != GEMM_CHAIN_POS) {
+      F.for_each(i0, j0, [&](float& v, int, int) { v = 0.0f; });
     } else {
-      if (seg > 0 && threadIdx.x == 0) {
+      if (from_partial && threadIdx.x == 0) {
         long spins = 0;
-        while (__hip_atomic_load(&flags[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seg) {
+        while (__hip_atomic_load(&flags[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 1) {
           __builtin_amdgcn_s_sleep(2);
           if (++spins > (1l << 28)) {
             atomicExch(timeout, 1);
@@ -560,33 +594,48 @@ __global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
-      F.for_each(i0, j0, [&](float& a, int row, int col) {
+      F.for_each(i0, j0, [&](float& v, int row, int col) {
         bool in = row < g.M && col < g.N;
-        a = g.C[in ? (long)row * g.ldc + col : 0];
+        v = g.C[in ? (long)row * g.ldc + col : 0];
       });
-      F.for_each(i0, j0, [&](float& a, int row, int col) {
-        if (!(row < g.M && col < g.N)) a = 0.0f;
+      F.for_each(i0, j0, [&](float& v, int row, int col) {
+        if (!(row < g.M && col < g.N)) v = 0.0f;
       });
     }
-    const int kbeg = seg * seglen, kend = min(g.K, kbeg + seglen);
-    F.mma(g, i0, j0, kbeg, kend, As, Bs, zeros);
-    const bool last = (seg == nseg - 1);
-    const bool mirror = last && (ti != tj);
-    F.for_each(i0, j0, [&](float& a, int row, int col) {
+#ifdef PT2Q_GRAM_PROFILE
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
+    F.mma(g, i0, j0, kb, min(ke, g.K), As, Bs, zeros);
+#ifdef PT2Q_GRAM_PROFILE
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    t_wait += t1 - t0;
+    t_mma += t2 - t1;
+#endif
+    const bool final = (ke >= Kp);
+    const bool mirror = final && (ti != tj);
+    F.for_each(i0, j0, [&](float& v, int row, int col) {
       if (row >= g.M || col >= g.N) return;
-      g.C[(long)row * g.ldc + col] = a;
-      if (mirror) g.C[(long)col * g.ldc + row] = a;
+      g.C[(long)row * g.ldc + col] = v;
+      if (mirror) g.C[(long)col * g.ldc + row] = v;
     });
-    if (!last) {
+    if (!final) {  // publish the partial for workgroup w+1
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&flags[tl], seg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&flags[a], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
+#ifdef PT2Q_GRAM_PROFILE
+  if (threadIdx.x == 0) {
+    atomicAdd(&g16_prof[0], t_wait);
+    atomicAdd(&g16_prof[1], t_mma);
+    atomicAdd(&g16_prof[2], __builtin_amdgcn_s_memtime() - t_start);
+    atomicAdd(&g16_prof[3], 1ull);
+  }
+#endif
 }
 
 template <int BM, int BN, typename TIn>
@@ -652,7 +701,7 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   // 16-bit inputs with 16-byte rows: the LDS-DMA kernel (PT2Q_GRAM_DMA=0 disables)
   static const char* dma_env = std::getenv("PT2Q_GRAM_DMA");
   const bool dma = sizeof(TIn) == 2 && vec_ok<128, 128, TIn>(g) && !(dma_env && dma_env[0] == '0');
-  void (*kern16)(GemmDesc, int, int, int, int*, int*, const uint16_t*) =
+  void (*kern16)(GemmDesc, int, int, long, int*, int*, const uint16_t*) =
       std::is_same<TIn, uint16_t>::value ? gram16_streamk_kernel<true> : gram16_streamk_kernel<false>;
   if (dma) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern16, 256, 0) != hipSuccess || per_cu < 1)
@@ -687,7 +736,13 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   int* timeout = flags + ntile;
   if (dma) {
     const uint16_t* zeros = (const uint16_t*)(((uintptr_t)(flags + ntile + 2) + 15) & ~(uintptr_t)15);
-    hipLaunchKernelGGL(kern16, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout, zeros);
+    // static split: P16 workgroups, each L >= Kp rows of the tile-major work line
+    const int Kp = ceil_div(g.K, G16_BK) * G16_BK;
+    const int P16 = P < ntile ? P : ntile;
+    const long Wt = (long)ntile * Kp;
+    const long L = ((Wt + P16 - 1) / P16 + G16_BK - 1) / G16_BK * G16_BK;
+    hipLaunchKernelGGL(kern16, dim3((unsigned)ceil_div(Wt, L)), dim3(256), 0, st, g, T, Kp, L, flags,
+                       timeout, zeros);
   } else {
     hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
   }
