@@ -66,24 +66,40 @@ __global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int 
 }
 
 constexpr int LPR = 4;           // lanes cooperating on one panel column / inverse row
+
+// Broadcast lane `owner` of each aligned group of 4 lanes (one DPP quad_perm move instead of a
+// ds_bpermute round trip through LDS).  owner is a compile-time constant after unrolling.
+template <int O>
+PT2Q_DEV float quad_bcast_c(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), O * 0x55, 0xF, 0xF, false));
+}
+PT2Q_DEV float quad_bcast(float v, int owner) {
+  return owner == 0 ? quad_bcast_c<0>(v)
+                    : owner == 1 ? quad_bcast_c<1>(v) : owner == 2 ? quad_bcast_c<2>(v) : quad_bcast_c<3>(v);
+}
 constexpr int SEG = NB / LPR;    // entries owned per lane
 
-// Loads the nb x nb diagonal block at (r0, r0) into D (identity padding beyond nb).
-// (256 threads: all 16 loads of a thread are issued before the first LDS store.)
-PT2Q_DEV void load_diag_block(float (*D)[NB + 4], const float* A, long lda, int r0, int nb) {
+// Loads the nb x nb diagonal block at (r0, r0) as its STRICT upper part Dus (zero on and below
+// the diagonal) plus the diagonal dg (identity padding beyond nb: dg = 1, Dus = 0).  With the
+// zeros in place the step loops below need no masks or branches: an fmaf with a zero factor is
+// an exact no-op on every nonzero chain (only the sign of an exact zero can differ, which the
+// contract treats as equal).  256 threads: all 16 loads of a thread are in flight together.
+PT2Q_DEV void load_diag_block(float (*Dus)[NB + 4], float* dg, const float* A, long lda, int r0,
+                              int nb) {
   constexpr int PER = NB * NB / 256;
   float v[PER];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int q = threadIdx.x + 256 * u, r = q / NB, c = q % NB;
-    const bool in = r < nb && c < nb;
+    const bool in = r < nb && c < nb && r <= c;
     v[u] = A[in ? (long)(r0 + r) * lda + r0 + c : (long)r0 * lda + r0];
     v[u] = in ? v[u] : ((r == c) ? 1.0f : 0.0f);
   }
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
-    const int q = threadIdx.x + 256 * u;
-    D[q / NB][q % NB] = v[u];
+    const int q = threadIdx.x + 256 * u, r = q / NB, c = q % NB;
+    Dus[r][c] = (c > r) ? v[u] : 0.0f;
+    if (r == c) dg[r] = v[u];
   }
 }
 
@@ -92,11 +108,12 @@ PT2Q_DEV void load_diag_block(float (*D)[NB + 4], const float* A, long lda, int 
 // lanes share a column (16 rows each); the lane owning row k divides and broadcasts x_k.
 __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int p0, int nb,
                                                          int m) {
-  __shared__ __attribute__((aligned(16))) float D[NB][NB + 4];
-  load_diag_block(D, A, lda, p0, nb);
+  __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
+  __shared__ float dg[NB];
+  load_diag_block(Dus, dg, A, lda, p0, nb);
   __syncthreads();
   const int i = p0 + nb + (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
-  const int sub = threadIdx.x & (LPR - 1), base = threadIdx.x & 63 & ~(LPR - 1);
+  const int sub = threadIdx.x & (LPR - 1);
   const bool valid = i < m;
   float x[SEG];
 #pragma unroll
@@ -108,18 +125,12 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int
   }
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
-    if (k < nb) {
-      const int owner = k / SEG, ks = k % SEG;
-      const float mine = x[ks] / D[k][k];
-      const float xk = __shfl(mine, base | owner);
-      if (sub == owner) x[ks] = xk;
+    const int owner = k / SEG, ks = k % SEG;
+    const float xk = quad_bcast(x[ks] / dg[k], owner);
+    x[ks] = (sub == owner) ? xk : x[ks];
+    const float* row = &Dus[k][sub * SEG];
 #pragma unroll
-      for (int s = 0; s < SEG; ++s) {
-        const int r = sub * SEG + s;
-        const float nv = fmaf(-D[k][r], xk, x[s]);
-        x[s] = (r > k) ? nv : x[s];
-      }
-    }
+    for (int s = 0; s < SEG; ++s) x[s] = fmaf(-row[s], xk, x[s]);
   }
   if (!valid) return;
 #pragma unroll
@@ -131,13 +142,16 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int
 
 // In-block part of the triangular inverse for column block [c0, c0+nb): rows k < c0+nb.
 // Ui[k][c0..] holds the running chains for k < c0 (zero otherwise).  Four lanes share a row.
+// For rows inside the block, columns left of the diagonal start at zero and only ever receive
+// zero terms, so they need no mask until the final store.
 __global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long ldu, float* Ui,
                                                             long ldi, int c0, int nb) {
-  __shared__ __attribute__((aligned(16))) float D[NB][NB + 4];
-  load_diag_block(D, U, ldu, c0, nb);
+  __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
+  __shared__ float dg[NB];
+  load_diag_block(Dus, dg, U, ldu, c0, nb);
   __syncthreads();
   const int k = (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
-  const int sub = threadIdx.x & (LPR - 1), base = threadIdx.x & 63 & ~(LPR - 1);
+  const int sub = threadIdx.x & (LPR - 1);
   const bool valid = k < c0 + nb;
   float acc[SEG];
 #pragma unroll
@@ -150,19 +164,13 @@ __global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long
   const int jb = (k > c0) ? k - c0 : 0;  // first in-block j (local)
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    if (j < nb) {
-      const int owner = j / SEG, js = j % SEG;
-      const bool active = j >= jb;
-      const float mine = (c0 + j == k) ? 1.0f / D[j][j] : -acc[js] / D[j][j];
-      const float xj = __shfl(mine, base | owner);
-      if (sub == owner && active) acc[js] = xj;
+    const int owner = j / SEG, js = j % SEG;
+    const float mine = (c0 + j == k) ? 1.0f / dg[j] : -acc[js] / dg[j];
+    const float xj = quad_bcast(mine, owner);
+    acc[js] = (sub == owner) ? xj : acc[js];
+    const float* row = &Dus[j][sub * SEG];
 #pragma unroll
-      for (int s = 0; s < SEG; ++s) {
-        const int q = sub * SEG + s;
-        const float nv = fmaf(xj, D[j][q], acc[s]);
-        acc[s] = (active && q > j) ? nv : acc[s];
-      }
-    }
+    for (int s = 0; s < SEG; ++s) acc[s] = fmaf(xj, row[s], acc[s]);
   }
   if (!valid) return;
 #pragma unroll

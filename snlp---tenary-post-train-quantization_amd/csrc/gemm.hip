@@ -262,7 +262,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
   int ti, tj;
-  if (g.upper) {
+  if (g.upper && g.kstart_diag == 2) {
+    // K starts at the tile's column (lauum): work falls with tj, so dispatch tiles column by
+    // column (tj ascending = longest first) for a greedy longest-processing-time balance
+    const int L = blockIdx.x;
+    tj = (int)((sqrtf(8.0f * (float)L + 1.0f) - 1.0f) * 0.5f);
+    while ((tj + 1) * (tj + 2) / 2 <= L) ++tj;
+    while (tj * (tj + 1) / 2 > L) --tj;
+    ti = L - tj * (tj + 1) / 2;
+  } else if (g.upper) {
     upper_tile(xcd_remap(blockIdx.x, gridDim.x), tiles_n, ti, tj);
   } else {
     ti = blockIdx.x / tiles_n;
