@@ -167,32 +167,44 @@ PT2Q_DEV int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-template <int BM, int BN>
+// Accumulator tile.  SW = false: MFMA rows are C rows (lane <-> C column).  SW = true: the
+// MFMA computes the transposed tile (operands swapped; fmaf(a,b,c) == fmaf(b,a,c), so the chains
+// are unchanged), so lane <-> C row and each group of 4 registers <-> 4 consecutive C columns,
+// which lets the epilogue move C with 16-byte accesses.
+template <int BM, int BN, bool SW = false>
 struct Frag {
   static constexpr int RM = BM / 64, RN = BN / 64;
   f32x16 acc[RM][RN];
+  PT2Q_DEV static int row_of(int i0, int rm, int r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, li = lane & 31, lk = lane >> 5;
+    return SW ? i0 + wr * (BM / 2) + rm * 32 + li
+              : i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+  }
+  PT2Q_DEV static int col_of(int j0, int rn, int r) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wc = wave & 1, li = lane & 31, lk = lane >> 5;
+    return SW ? j0 + wc * (BN / 2) + rn * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk
+              : j0 + wc * (BN / 2) + rn * 32 + li;
+  }
   template <typename F>
   PT2Q_DEV void for_each(int i0, int j0, F&& f) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm)
 #pragma unroll
       for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          int row = i0 + wr * (BM / 2) + rm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
-          int col = j0 + wc * (BN / 2) + rn * 32 + li;
           float v = acc[rm][rn][r];
-          f(v, row, col);
+          f(v, row_of(i0, rm, r), col_of(j0, rn, r));
           acc[rm][rn][r] = v;
         }
   }
 };
 
 // Extend the chains of one output tile over K-range [kbeg, kend) (k ascending).
-template <int BM, int BN, typename TIn, bool VEC>
-PT2Q_DEV void tile_mma(Frag<BM, BN>& F, const GemmDesc& g, int i0, int j0, int kbeg, int kend,
+template <int BM, int BN, typename TIn, bool VEC, bool SW = false>
+PT2Q_DEV void tile_mma(Frag<BM, BN, SW>& F, const GemmDesc& g, int i0, int j0, int kbeg, int kend,
                        float (*As)[BK][BM + PAD], float (*Bs)[BK][BN + PAD]) {
   constexpr int RM = BM / 64, RN = BN / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -220,7 +232,8 @@ PT2Q_DEV void tile_mma(Frag<BM, BN>& F, const GemmDesc& g, int i0, int j0, int k
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn)
           F.acc[rm][rn] =
-              __builtin_amdgcn_mfma_f32_32x32x2f32(sgn * a[s][rm], b[s][rn], F.acc[rm][rn], 0, 0, 0);
+              SW ? __builtin_amdgcn_mfma_f32_32x32x2f32(b[s][rn], sgn * a[s][rm], F.acc[rm][rn], 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_32x32x2f32(sgn * a[s][rm], b[s][rn], F.acc[rm][rn], 0, 0, 0);
   };
   // elements with k >= kend are zero-filled: an exact no-op for the chains
   if (kbeg < kend) {
@@ -277,33 +290,78 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
     tj = blockIdx.x % tiles_n;
   }
   const int i0 = ti * BM, j0 = tj * BN;
-  Frag<BM, BN> F;
+  Frag<BM, BN, true> F;
+  // C moves in 16-byte groups of 4 consecutive columns when rows are 16-byte aligned
+  const bool cvec = (g.ldc % 4 == 0) && ((uintptr_t)g.C % 16 == 0);
+  constexpr int RM = BM / 64, RN = BN / 64;
   F.for_each(i0, j0, [&](float& a, int, int) { a = 0.0f; });
   if (g.mode == GEMM_CHAIN_NEG || g.mode == GEMM_CHAIN_POS) {
     // chains continue from C (no output-row gather in this mode); all loads issued before use
-    F.for_each(i0, j0, [&](float& a, int row, int col) {
-      bool in = row < g.M && col < g.N;
-      a = g.C[in ? (long)row * g.ldc + col : 0];
-    });
-    F.for_each(i0, j0, [&](float& a, int row, int col) {
-      if (!(row < g.M && col < g.N)) a = 0.0f;
-    });
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = F.row_of(i0, rm, 4 * q), col = F.col_of(j0, rn, 4 * q);
+          const bool rin = row < g.M;
+          const float* p = g.C + (rin ? (long)row * g.ldc : 0);
+          if (cvec && rin && col + 3 < g.N) {
+            const f32x4 v = *(const f32x4*)(p + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) F.acc[rm][rn][4 * q + e] = v[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool in = rin && col + e < g.N;
+              const float v = p[in ? col + e : 0];
+              F.acc[rm][rn][4 * q + e] = in ? v : 0.0f;
+            }
+          }
+        }
   }
   int kbeg = 0;
   if (g.kstart_diag == 1) kbeg = i0 - (i0 % BK);
   if (g.kstart_diag == 2) kbeg = j0 - (j0 % BK);
-  tile_mma<BM, BN, TIn, VEC>(F, g, i0, j0, kbeg, g.K, As, Bs);
+  tile_mma<BM, BN, TIn, VEC, true>(F, g, i0, j0, kbeg, g.K, As, Bs);
   const bool mirror = g.upper && g.mirror && (ti != tj);
-  F.for_each(i0, j0, [&](float& a, int row, int col) {
-    if (row >= g.M || col >= g.N) return;
-    long crow = g.crow ? g.crow[row] : row;
-    float* p = g.C + crow * g.ldc + col;
-    float v = a;
-    if (g.mode == GEMM_ADD) v = *p + v;
-    else if (g.mode == GEMM_SUB) v = *p - v;
-    *p = v;
-    if (mirror) g.C[(long)col * g.ldc + row] = v;
-  });
+#pragma unroll
+  for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+    for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = F.row_of(i0, rm, 4 * q), col = F.col_of(j0, rn, 4 * q);
+        if (row >= g.M) continue;
+        const long crow = g.crow ? g.crow[row] : row;
+        float* p = g.C + crow * g.ldc + col;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = F.acc[rm][rn][4 * q + e];
+        if (cvec && col + 3 < g.N) {
+          if (g.mode == GEMM_ADD || g.mode == GEMM_SUB) {
+            const f32x4 c = *(const f32x4*)p;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (g.mode == GEMM_ADD) ? c[e] + v[e] : c[e] - v[e];
+          }
+          *(f32x4*)p = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (col + e >= g.N) continue;
+            float x = v[e];
+            if (g.mode == GEMM_ADD) x = p[e] + x;
+            else if (g.mode == GEMM_SUB) x = p[e] - x;
+            p[e] = x;
+            v[e] = x;
+          }
+        }
+        if (mirror) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < g.N) g.C[(long)(col + e) * g.ldc + row] = v[e];
+        }
+      }
 }
 
 // Persistent, balanced ("stream-K with exact chain continuation") symmetric Gram, STORE mode:
