@@ -129,11 +129,14 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     const int nr = r - bs;
     int* rem = w.rem[cur];
     int* nrem = w.rem[cur ^ 1];
+    // variant M with blocks <= 128: the top-k workgroup also forms S1/d (no separate launch)
+    const bool s1_in_topk = ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
     if (ssr) {
       if (r > b) {
         if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st)) != PT2Q_OK)
           return rc;
-        if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
+        if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st,
+                                       s1_in_topk ? A : nullptr, lda, w.S1, w.d)) != PT2Q_OK)
           return rc;
       } else {
         if ((rc = pt2q_launch_select_seq(1, 0, bs, m, rem, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
@@ -145,18 +148,17 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     }
     const float* S1 = nullptr;
     if (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_HESS) {
-      if ((rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK)
+      if (!s1_in_topk &&
+          (rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK)
         return rc;
       S1 = w.S1;
     }
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
                                     w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
                                     nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
-                                    st)) != PT2Q_OK)
-      return rc;
+                                    st, Hinv, ldhi, nrem, nr, w.Ck, m)) != PT2Q_OK)
+      return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
     if (nr > 0) {
-      if ((rc = pt2q_launch_ef_coeffs(Hinv, ldhi, w.blk, bs, nrem, nr, w.Ck, m, st)) != PT2Q_OK)
-        return rc;
       GemmDesc g{};
       g.M = nr; g.N = n; g.K = bs;
       g.A = w.Ck; g.lda = m; g.a_layout = LAY_KMAJOR;     // (e, k) = C[k][e]

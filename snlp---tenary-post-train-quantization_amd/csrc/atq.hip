@@ -22,6 +22,20 @@ constexpr int ROWS_PER_WAVE = 4;
 constexpr int WAVES = 4;
 constexpr int ROWS_PER_WG = ROWS_PER_WAVE * WAVES;
 
+// flexible_round's code of RN((w - mu) / as) at the ±0.5 thresholds (quantizer.py:127-131),
+// without a division in the common case: qa = d * rcp(as) is within 2^-21 (relative) of the
+// exact quotient, so whenever qa is farther than 2^-20 from a threshold the exact quotient, and
+// its correctly rounded value (rounding is monotonic), lie on the same side.  Near a threshold,
+// or if the reciprocal is unreliable, the correctly rounded division decides, exactly as before.
+PT2Q_DEV float round_code(float d, float as, float ras, bool ras_ok) {
+  float q = d * ras;
+  const float aq = fabsf(q);
+  if (!ras_ok || !(fabsf(aq - 0.5f) > aq * 0x1p-20f)) q = d / as;
+  return (q > 0.5f) ? 1.0f : ((q < -0.5f) ? -1.0f : 0.0f);
+}
+PT2Q_DEV float rcp_approx(float as) { return __builtin_amdgcn_rcpf(as); }
+PT2Q_DEV bool rcp_ok(float as) { return as < 1e30f; }  // as >= 1e-8 by the clamp
+
 template <int NS>
 struct Row {
   float w[NS];
@@ -90,12 +104,13 @@ PT2Q_DEV void row_grid(const Row<NS>& R, float wsum, float* a, float* m) {
 template <int NS>
 PT2Q_DEV bool row_round(Row<NS>& R, float a, float m) {
   float as = clampmin(a);
+  const float ras = rcp_approx(as);
+  const bool rok = rcp_ok(as);
   bool changed = false;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (R.has(s)) {
-      float z = (R.w[s] - m) / as;
-      float nt = (z > 0.5f) ? 1.0f : ((z < -0.5f) ? -1.0f : 0.0f);
+      float nt = round_code(R.w[s] - m, as, ras, rok);
       changed |= (nt != R.t[s]);
       R.t[s] = nt;
     }
@@ -200,28 +215,45 @@ __global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
   const int wave = threadIdx.x >> 6;
   const int row0 = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE;
   block_rows<NS>(A, row0, false, true);
-  // Last-arriving workgroup repairs the whole-block T_init == 0 case (quantizer.py:164 breaks
-  // at iteration 0 and returns the init grid).  Release/acquire per cdna_hip_programming §6 G16.
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int ticket = __hip_atomic_fetch_add(&A.counters[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (ticket == (int)gridDim.x - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+}
+
+// The whole-block T_init == 0 case (quantizer.py:164 breaks at iteration 0 and returns the init
+// grid): a second launch reads the zero-row count after the kernel boundary and, only then,
+// redoes every row without ITF.  (A last-arriving-workgroup repair inside atq_block_kernel cost
+// an agent-scope release fence - an L2 write-back - per workgroup.)
+template <int NS>
+__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A) {
+  if (A.counters[0] != A.n) return;
+  const int wave = threadIdx.x >> 6;
+  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
+}
+
+// After the block's ATQ: the zero-block repair (rare) and the error-feedback coefficients
+// C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k]) (main.py:201-209) in ONE launch; the
+// two parts are independent.
+struct CoeffArgs {
+  const float* Hinv;
+  long ldh;
+  const int* rem;
+  int nr, bs;
+  float* C;
+  long ldc;
+};
+
+template <int NS>
+__global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A, CoeffArgs K, int fix_wgs) {
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (q < (long)K.nr * K.bs) {
+    const int k = (int)(q / K.nr), e = (int)(q % K.nr);
+    const long rowb = (long)A.blk[k] * K.ldh;
+    const float dg = clampmin(K.Hinv[rowb + A.blk[k]]);
+    K.C[(long)k * K.ldc + e] = K.Hinv[rowb + K.rem[e]] / dg;
   }
-  __syncthreads();
-  if (!last) return;
-  int zero_rows = __hip_atomic_load(&A.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (zero_rows != A.n) return;
-  if (A.iters && threadIdx.x == 0) *A.iters = 0;
-  for (int row0b = wave * ROWS_PER_WAVE; row0b < A.n; row0b += ROWS_PER_WG)
-    block_rows<NS>(A, row0b, true, false);
+  if ((int)blockIdx.x >= fix_wgs || A.counters[0] != A.n) return;
+  const int wave = threadIdx.x >> 6;
+  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
 }
 
 // ----------------------------------------------------------------- per-stage kernel (row-major)
@@ -435,12 +467,13 @@ PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, int b, Grid3& G) {
 template <bool FM>
 PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, int b, float a, float m, Grid3& G) {
   const float as = clampmin(a);
+  const float ras = rcp_approx(as);
+  const bool rok = rcp_ok(as);
   bool changed = false;
   G.zero();
   auto one = [&](int k, int j) {
     float w = R.w(k), old = R.t(k);
-    float z = (w - m) / as;
-    float nt = (z > 0.5f) ? 1.0f : ((z < -0.5f) ? -1.0f : 0.0f);
+    float nt = round_code(w - m, as, ras, rok);
     if (nt != old) {
       changed = true;
       R.set_t(k, nt);
@@ -549,26 +582,14 @@ PT2Q_DEV void wide_block_rows(const WideArgs& A, int row0, bool skip_itf, bool c
 template <bool FM>
 __global__ __launch_bounds__(64) void atq_wide_block_kernel(WideArgs A) {
   wide_block_rows<FM>(A, blockIdx.x * 64, false, true);
-  // whole-block T_init == 0 repair by the last workgroup (see atq_block_kernel)
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int ticket = __hip_atomic_fetch_add(&A.counters[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (ticket == (int)gridDim.x - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  int zero_rows = __hip_atomic_load(&A.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (zero_rows != A.n) return;
-  if (A.iters && threadIdx.x == 0) *A.iters = 0;
-  for (int row0 = 0; row0 < A.n; row0 += 64) wide_block_rows<FM>(A, row0, true, false);
+}
+
+// whole-block T_init == 0 repair after the kernel boundary (see atq_zero_fixup_kernel)
+template <bool FM>
+__global__ __launch_bounds__(64) void atq_wide_zero_fixup_kernel(WideArgs A) {
+  if (A.counters[0] != A.n) return;
+  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  wide_block_rows<FM>(A, blockIdx.x * 64, true, false);
 }
 
 // Per-method stages on row-major W / float T (quantizer.py surface) for b > 512.
@@ -635,12 +656,16 @@ int dispatch_ns(int b, F&& f) {
 int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
-                          hipStream_t st) {
+                          hipStream_t st, const float* Hinv, long ldh, const int* rem, int nr,
+                          float* C, long ldc) {
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
     hipLaunchKernelGGL(atq_wide_block_kernel<true>, dim3(ceil_div(n, 64)), dim3(64), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<true>, dim3(ceil_div(n, 64)), dim3(64), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    if (Hinv && nr > 0) return pt2q_launch_ef_coeffs(Hinv, ldh, blk, b, rem, nr, C, ldc, st);
     return PT2Q_OK;
   }
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters};
@@ -648,6 +673,15 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
     hipLaunchKernelGGL(atq_block_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+    PT2Q_LAUNCH_CHECK();
+    if (Hinv && nr > 0) {  // zero-block repair + EF coefficients in one launch
+      CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc};
+      const int cgrid = ceil_div((long)nr * b, 256);
+      hipLaunchKernelGGL(atq_post_kernel<NS>, dim3(cgrid > grid ? cgrid : grid), dim3(256), 0, st, A,
+                         K, grid);
+    } else {
+      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+    }
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   });

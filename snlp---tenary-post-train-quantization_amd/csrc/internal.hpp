@@ -7,13 +7,15 @@
 int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
-                          hipStream_t st);
+                          hipStream_t st, const float* Hinv = nullptr, long ldh = 0,
+                          const int* rem = nullptr, int nr = 0, float* C = nullptr, long ldc = 0);
 
 // ---- SSR / selection (ssr.hip)
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
                                float* part, float* wn, float* sim, hipStream_t st);
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
-                         int64_t* perm_out, hipStream_t st);
+                         int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
+                         float* S1 = nullptr, float* d = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
                            int* newrem, int64_t* perm_out, hipStream_t st);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,

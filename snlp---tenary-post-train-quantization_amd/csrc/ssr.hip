@@ -113,14 +113,67 @@ PT2Q_DEV uint32_t orderable(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// S1[j] = l-ascending sum of A[blk_j][blk_l], d = j-ascending sum of S1 (aga_s1 order) for
+// b <= 128, by one workgroup: every gather load of a thread is in flight before the first LDS
+// store; gb >= b*(b+1) floats of LDS, s1 >= b floats of LDS, bl = the b indices in LDS.
+PT2Q_DEV void s1_block(const float* A, long lda, const int* bl, int b, float* gb, float* s1,
+                       float* S1, float* d) {
+  const int tid = threadIdx.x, nt = blockDim.x, ld = b + 1, tot = b * b;
+  for (int q0 = 0; q0 < tot; q0 += 16 * nt) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = q0 + u * nt + tid, qq = q < tot ? q : 0;
+      v[u] = A[(long)bl[qq / b] * lda + bl[qq % b]];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = q0 + u * nt + tid;
+      if (q < tot) gb[(q / b) * ld + (q % b)] = v[u];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < b; j += nt) {
+    float sj = 0.0f;
+    for (int l = 0; l < b; ++l) sj = sj + gb[j * ld + l];
+    s1[j] = sj;
+    S1[j] = sj;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float dd = 0.0f;
+    for (int j = 0; j < b; ++j) dd = dd + s1[j];
+    *d = dd;
+  }
+}
+
+// Single-kernel S1 for the sequential / take-the-rest selections (b <= 128, raw Gram).
+__global__ __launch_bounds__(1024) void s1_fused_kernel(const float* A, long lda, const int* blk,
+                                                        int b, float* S1, float* d) {
+  __shared__ float gb[128 * 129];
+  __shared__ float s1[128];
+  __shared__ int bl[128];
+  for (int j = threadIdx.x; j < b; j += blockDim.x) bl[j] = blk ? blk[j] : j;
+  __syncthreads();
+  s1_block(A, lda, bl, b, gb, s1, S1, d);
+}
+
 // Ordered top-b of r similarities: keys (value desc, position asc), bitonic sort in LDS.
 // Writes blk (selection order), newrem (ascending), perm_out (int64, nullable).
+// With G != nullptr (variant M, b <= 128) the same workgroup then forms S1/d for AGA from the
+// raw Gram over the block it just selected (one launch instead of three).
 __global__ __launch_bounds__(1024) void ssr_topk_kernel(const float* sim, const int* rem, int r,
                                                         int b, int P, int* blk, int* newrem,
-                                                        int64_t* perm_out) {
-  extern __shared__ unsigned long long keys[];  // P keys, then r flag bytes, then scan ints
-  unsigned char* sel = (unsigned char*)(keys + P);
+                                                        int64_t* perm_out, const float* G,
+                                                        long ldg, float* S1, float* d,
+                                                        int keys_floats) {
+  // LDS: keys region (P keys; reused for the S1 gather), r flag bytes, scan ints, b indices,
+  // b partial sums
+  extern __shared__ unsigned long long keys[];
+  unsigned char* sel = (unsigned char*)((float*)keys + keys_floats);
   int* scan = (int*)(sel + ((r + 15) & ~15));
+  int* bl = scan + 1024;
+  float* s1 = (float*)(bl + 128);
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int e = tid; e < P; e += nt)
     keys[e] = (e < r) ? (((unsigned long long)orderable(sim[e]) << 32) |
@@ -148,10 +201,12 @@ __global__ __launch_bounds__(1024) void ssr_topk_kernel(const float* sim, const 
     int e = (int)(0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFull));
     int j = rem[e];
     blk[t] = j;
+    if (G) bl[t] = j;
     if (perm_out) perm_out[t] = j;
     sel[e] = 1;
   }
   __syncthreads();
+  if (G) s1_block(G, ldg, bl, b, (float*)keys, s1, S1, d);  // keys are dead after the pick
   // stable compaction of the unselected positions (ascending)
   const int per = (r + nt - 1) / nt;
   const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
@@ -390,13 +445,19 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
 }
 
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
-                         int64_t* perm_out, hipStream_t st) {
+                         int64_t* perm_out, hipStream_t st, const float* G, long ldg, float* S1,
+                         float* d) {
   int P = 1;
   while (P < r) P <<= 1;
-  size_t lds = (size_t)P * 8 + (size_t)((r + 15) & ~15) + 1024 * sizeof(int);
+  if (G && b > 128) return PT2Q_E_ARG;
+  int keys_floats = 2 * P;
+  if (G && keys_floats < b * (b + 1)) keys_floats = b * (b + 1);
+  keys_floats = (keys_floats + 3) & ~3;
+  size_t lds = (size_t)keys_floats * 4 + (size_t)((r + 15) & ~15) + 1024 * sizeof(int) +
+               128 * sizeof(int) + 128 * sizeof(float);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   hipLaunchKernelGGL(ssr_topk_kernel, dim3(1), dim3(1024), lds, st, sim, rem, r, b, P, blk,
-                     newrem, perm_out);
+                     newrem, perm_out, G, ldg, S1, d, keys_floats);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
@@ -414,6 +475,11 @@ int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int*
 
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st) {
+  if (src == 1 && b <= 128) {
+    hipLaunchKernelGGL(s1_fused_kernel, dim3(1), dim3(1024), 0, st, A, lda, blk, b, S1, d);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   if (src == 1) {
     if (b > 512)
       hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, 256)), dim3(256), 0, st, A, lda, blk, b, S1);
