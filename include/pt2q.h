@@ -65,11 +65,15 @@ size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags);
 size_t pt2q_cholesky_workspace_bytes(int m);
 
 /* G = XᵀX (accumulate=0), G = G + XᵀX (accumulate=1), or continue (accumulate=2): every
- * entry's k-ascending chain resumes from G, so Grams streamed batch by batch are bit-identical
- * to one Gram of the concatenated rows.  X: N x m of type xdtype.
+ * entry's chain resumes from G, so Grams streamed batch by batch are bit-identical to one Gram
+ * of the concatenated rows.  X: N x m of type xdtype (X may be NULL when N = 0).
+ * Arithmetic: f32 X -> k-ascending fmaf chains (f32 MFMA); fp16 / bf16 X -> the 16-bit MFMA
+ * chain (v_mfma_f32_32x32x16_*: rows in groups of 8, one rounding per group; restated by
+ * oracle orc_gram16), for which the continue guarantee needs every batch but the last to have
+ * a multiple of 8 rows.
  * Replaces main.py:128 (H = X.T @ X over the captured activations, main.py:293),
- * gptq.py:59-76 (GPTQ.add_batch, accumulate=1). Writes the full symmetric matrix.  workspace (nullable, pt2q_gram_workspace_bytes(m)) enables the balanced
- * persistent kernel for long K. */
+ * gptq.py:59-76 (GPTQ.add_batch, accumulate=1). Writes the full symmetric matrix.
+ * workspace (nullable, pt2q_gram_workspace_bytes(m)) enables the balanced split over all CUs. */
 size_t pt2q_gram_workspace_bytes(int m);
 int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G, int64_t ldg,
               int accumulate, void* workspace, size_t workspace_bytes, void* stream);

@@ -20,6 +20,7 @@ f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
 i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
 i8p = np.ctypeslib.ndpointer(dtype=np.int8, flags="C_CONTIGUOUS")
 i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(dtype=np.uint16, flags="C_CONTIGUOUS")
 L = ctypes.c_long
 I = ctypes.c_int
 F = ctypes.c_float
@@ -47,6 +48,8 @@ def lib():
             "orc_ssr_select": (I, [f32p, L, I, i64p, I, I, i64p, i64p, f32p]),
             "orc_gram": (None, [f32p, L, L, I, f32p, L]),
             "orc_gram_accumulate": (None, [f32p, L, L, I, f32p, L]),
+            "orc_gram16": (None, [u16p, L, L, I, f32p, L, I, I]),
+            "orc_mfma16_tiles": (None, [I, u16p, u16p, f32p, f32p, I]),
             "orc_prepare_hessian": (F, [f32p, L, I, L, F, f32p, L]),
             "orc_cholesky_upper": (I, [f32p, L, I, f32p, L]),
             "orc_trtri_upper": (None, [f32p, L, I, f32p, L]),
@@ -194,6 +197,42 @@ def gram(X):
     return G
 
 
+def _bits16(X):
+    """(uint16 bits, is_bf16) of an fp16 array, or of bf16 data given as a torch tensor or as
+    uint16 bits tagged by the caller."""
+    if hasattr(X, "dtype") and str(X.dtype) == "torch.bfloat16":
+        import torch
+        return np.ascontiguousarray(X.contiguous().view(torch.int16).numpy().view(np.uint16)), True
+    return np.ascontiguousarray(np.asarray(X, dtype=np.float16)).view(np.uint16), False
+
+
+def gram16(X, G=None, bf16_bits=False):
+    """XᵀX of 16-bit X (numpy fp16, torch bf16, or raw bf16 bits with bf16_bits=True) under the
+    gfx950 16-bit MFMA arithmetic (pt2q_oracle.c orc_gram16); with G given, continues G's chains
+    by this batch (pt2q_gram accumulate=2).  main.py:128."""
+    if bf16_bits:
+        Xb, bf = np.ascontiguousarray(X, np.uint16), True
+    else:
+        Xb, bf = _bits16(X)
+    if Xb.ndim == 3:
+        Xb = Xb.reshape(-1, Xb.shape[-1])
+    N, m = Xb.shape
+    cont = G is not None
+    G = np.zeros((m, m), np.float32) if G is None else np.ascontiguousarray(G, np.float32).copy()
+    lib().orc_gram16(np.ascontiguousarray(Xb), m, N, m, G, m, int(cont), int(bf))
+    return G
+
+
+def mfma16_tiles(A, B, C, bf16=False):
+    """The oracle's model of one v_mfma_f32_32x32x16_{f16,bf16} per tile: A (t,32,16) and
+    B (t,16,32) as uint16 bits, C (t,32,32) f32."""
+    A = np.ascontiguousarray(A).view(np.uint16); B = np.ascontiguousarray(B).view(np.uint16)
+    C = _f32(C)
+    D = np.empty_like(C)
+    lib().orc_mfma16_tiles(A.shape[0], A, B, C, D, int(bf16))
+    return D
+
+
 def gram_accumulate(H, X):
     """GPTQ.add_batch gptq.py:59-76: H += XᵀX (in place)."""
     X = _f32(X)
@@ -265,12 +304,25 @@ def quantize_blocks(W, A, Hinv, block_size=128, use_ssr=True, aga_src=1, max_ite
             "iters": iters, "W_final": Wt.T.copy()}
 
 
+def is16(X):
+    """fp16 numpy data or a torch bf16 tensor: the 16-bit Gram arithmetic applies."""
+    return (isinstance(X, np.ndarray) and X.dtype == np.float16) or str(getattr(X, "dtype", "")) == "torch.bfloat16"
+
+
+def gram_any(X):
+    """The Gram the engine computes for activations of X's dtype: the 16-bit MFMA model for
+    fp16 / bf16 (gram16), the f32 fmaf chain otherwise (gram)."""
+    return gram16(X) if is16(X) else gram(X)
+
+
 def quantize_layer_m(W, X, block_size=128, use_ssr=True, percdamp=0.01, max_iter=100):
-    """PT2LLMQuantizer.quantize_layer main.py:102-230 (variant M)."""
-    X = _f32(X)
+    """PT2LLMQuantizer.quantize_layer main.py:102-230 (variant M).  X may be fp16 (numpy) or
+    bf16 (torch): its Gram then follows the 16-bit MFMA arithmetic, as on the device."""
+    if not is16(X):
+        X = _f32(X)
     if X.ndim == 3:
         X = X.reshape(-1, X.shape[-1])
-    G = gram(X)
+    G = gram_any(X)
     H, _ = prepare_hessian(G, X.shape[0], percdamp)
     Hinv, spd = cholesky_inverse(H)
     out = quantize_blocks(W, G, Hinv, block_size, use_ssr, 1, max_iter)

@@ -219,7 +219,8 @@ extern "C" size_t pt2q_gram_workspace_bytes(int m) {
 extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G,
                          int64_t ldg, int accumulate, void* workspace, size_t workspace_bytes,
                          void* stream) {
-  if (!X || !G || N < 0 || m <= 0 || !dtype_ok(xdtype) || ldx < m || ldg < m) return PT2Q_E_ARG;
+  if ((!X && N > 0) || !G || N < 0 || m <= 0 || !dtype_ok(xdtype) || ldx < m || ldg < m)
+    return PT2Q_E_ARG;
   GemmDesc g{};
   g.M = m; g.N = m; g.K = (int)N;
   g.A = X; g.lda = ldx; g.a_layout = LAY_KMAJOR;

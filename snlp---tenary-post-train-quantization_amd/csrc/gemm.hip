@@ -840,6 +840,7 @@ size_t pt2q_gram_flags_ints(int m) {
 // Symmetric Gram C = XᵀX (STORE): balanced persistent kernel when it pays (big K, enough
 // tiles), else the one-tile-per-workgroup GEMM.  flags: pt2q_gram_flags_ints(m) ints or NULL.
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st) {
+  if (g.in_dtype == PT2Q_F16 || g.in_dtype == PT2Q_BF16) return pt2q_launch_gram16(g, flags, st);
   const int T = ceil_div(g.M, 128);
   const long ntile = (long)T * (T + 1) / 2;
   static const char* mode = std::getenv("PT2Q_GRAM_STREAMK");

@@ -48,6 +48,9 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st);
 size_t pt2q_gram_flags_ints(int m);
+// 16-bit-input Gram on the 16-bit MFMA (gram16.hip): every shape, STORE / ADD / CHAIN_POS
+int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st);
+size_t pt2q_gram16_flags_ints(int m);
 
 // ---- misc (misc.hip)
 int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,

@@ -42,7 +42,9 @@ def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate=False,
 
     accumulate=False: G = XᵀX.  True: G = G + XᵀX (gptq.py:75 add_batch).  "continue": every
     entry's fp32 chain resumes from G, so a Gram streamed batch by batch is bit-identical to one
-    Gram of the concatenated rows (the captured-and-concatenated X of main.py:293)."""
+    Gram of the concatenated rows (the captured-and-concatenated X of main.py:293) — for fp16 /
+    bf16 activations, whose 16-bit MFMA chain advances in groups of 8 rows, when every batch
+    but the last has a multiple of 8 rows."""
     X = _float_input(X.reshape(-1, X.shape[-1]))
     N, m = X.shape
     if G is None:

@@ -9,14 +9,15 @@ import pytest
 import torch
 
 import synth
-from test_gpu_parity import bits_equal, cuda, host
+from test_gpu_parity import bits_equal, cuda, host, oracle_gram
 from oracle import oracle as orc
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("splits,m,dt", [((100, 37, 200), 96, torch.float32),
-                                         ((1000, 3000, 16384), 2048, torch.float16)])
+                                         ((1000, 3000, 16384), 2048, torch.float16),
+                                         ((64, 192, 2048), 256, torch.bfloat16)])
 def test_gram_continue_equals_concatenated(pt2q, splits, m, dt):
     X = synth.activations(21 + m, sum(splits), m)
     Xd = cuda(X).to(dt)
@@ -26,7 +27,7 @@ def test_gram_continue_equals_concatenated(pt2q, splits, m, dt):
         acc.add(Xd[s:s + k])
         s += k
     assert acc.nsamples == X.shape[0]
-    assert bits_equal(host(acc.G), orc.gram(host(Xd.float())))
+    assert bits_equal(host(acc.G), oracle_gram(Xd))
 
 
 def test_quantize_shared_equals_per_linear(pt2q):

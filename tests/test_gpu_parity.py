@@ -32,31 +32,49 @@ def bits_equal(a, b):
 
 # ------------------------------------------------------------------ building blocks
 
+def oracle_gram(Xd):
+    """The oracle Gram for device activations Xd: the 16-bit MFMA arithmetic for fp16/bf16
+    (orc.gram16), the f32 fmaf chain for f32."""
+    if Xd.dtype == torch.float16:
+        return orc.gram16(host(Xd))
+    if Xd.dtype == torch.bfloat16:
+        return orc.gram16(Xd.cpu())
+    return orc.gram(host(Xd))
+
+
+def oracle_x(Xd):
+    """Device activations as the oracle takes them (fp16 numpy / bf16 torch / f32 numpy)."""
+    return Xd.cpu() if Xd.dtype == torch.bfloat16 else host(Xd)
+
+
 @pytest.mark.parametrize("N,m,dt", [(300, 200, torch.float32), (1024, 384, torch.float32),
-                                    (2048, 256, torch.float16), (512, 130, torch.bfloat16)])
+                                    (2048, 256, torch.float16), (512, 130, torch.bfloat16),
+                                    (77, 40, torch.float16), (0, 64, torch.float16),
+                                    (1000, 520, torch.bfloat16)])
 def test_gram_bitexact(pt2q, N, m, dt):
+    """Small / ragged shapes (m % 8 != 0 takes the register-staged 16-bit path; N = 0)."""
     X = synth.activations(7 + m, N, m)
     Xd = cuda(X).to(dt)
     G = pt2q.gram(Xd)
-    ref = orc.gram(host(Xd.float()))
+    ref = oracle_gram(Xd)
     assert bits_equal(host(G), ref)
-    # accumulate (gptq.py add_batch): H = H + XᵀX
+    # accumulate (gptq.py add_batch): H = H + XᵀX (product rounded, then one add)
     G2 = pt2q.gram(Xd[: N // 2], G.clone(), accumulate=True)
-    ref2 = ref.copy()
-    orc.gram_accumulate(ref2, host(Xd[: N // 2].float()))
+    ref2 = ref + oracle_gram(Xd[: N // 2])
     assert bits_equal(host(G2), ref2)
 
 
-@pytest.mark.parametrize("N,m,dt", [(16384, 2048, torch.float16), (20000, 2100, torch.float16),
-                                     (17000, 2048, torch.float32), (16448, 2176, torch.bfloat16)])
+@pytest.mark.parametrize("N,m,dt", [(2048, 4096, torch.float16), (1000, 4104, torch.bfloat16),
+                                     (777, 4100, torch.float16), (17000, 2048, torch.float32)])
 def test_gram_streamk_bitexact(pt2q, N, m, dt):
-    """The balanced persistent Gram (segmented K, chains continued through fp32 partials) is
-    taken for K >= 16384 and >= 128 tiles of 128x128; it must equal the oracle bit-for-bit,
-    including ragged m / N (scalar-load path for m % 8 != 0)."""
+    """The balanced persistent Gram (static split of the tile line over one workgroup per CU,
+    chains continued through fp32 partials: 16-bit X splits from m >= 4096) must equal the
+    oracle bit-for-bit, including ragged m / N (m % 8 != 0: register-staged operands)."""
+    orc.set_threads(16)
     X = synth.activations(13 + m, N, m)
     Xd = cuda(X).to(dt)
     G = pt2q.gram(Xd)
-    assert bits_equal(host(G), orc.gram(host(Xd.float())))
+    assert bits_equal(host(G), oracle_gram(Xd))
 
 
 @pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500)])
@@ -187,9 +205,10 @@ def test_per_channel_config5_shape(pt2q):
     N = 4096
     W = synth.weights(5120, n, m)
     X = synth.activations(5121, N, m)
-    out = pt2q.quantize_layer(cuda(W), cuda(X).to(torch.bfloat16), block_size=m, use_ssr=True)
-    Xb = host(cuda(X).to(torch.bfloat16).float())
-    ref = _oracle_m(W, Xb, m, True)
+    orc.set_threads(16)
+    Xd = cuda(X).to(torch.bfloat16)
+    out = pt2q.quantize_layer(cuda(W), Xd, block_size=m, use_ssr=True)
+    ref = _oracle_m(W, oracle_x(Xd), m, True)
     _assert_layer_bitexact(out, ref)
     np.testing.assert_array_equal(host(out.perm), np.arange(m))
 
@@ -354,13 +373,14 @@ def test_layer_m_bitexact_larger(pt2q, n, m, N, ssr, bs):
     _assert_layer_bitexact(out, _oracle_m(W, X, bs, ssr))
 
 
-def test_layer_m_fp16_inputs_equal_upcast(pt2q):
-    """fp16 layer + activations (configs C3/C4): the engine computes on the exact fp32 upcast."""
+def test_layer_m_fp16_inputs(pt2q):
+    """fp16 layer + activations (configs C3/C4): W is used as its exact fp32 upcast, the Gram of
+    the fp16 activations follows the 16-bit MFMA arithmetic (orc.gram16)."""
     W = synth.weights(31, 512, 640)
     X = synth.activations(32, 1024, 640)
     Wh, Xh = cuda(W).half(), cuda(X).half()
     out = pt2q.quantize_layer(Wh, Xh)
-    ref = _oracle_m(host(Wh.float()), host(Xh.float()), 128, True)
+    ref = _oracle_m(host(Wh.float()), host(Xh), 128, True)
     _assert_layer_bitexact(out, ref)
 
 

@@ -259,3 +259,34 @@ def test_ternary_linear_oracle_vs_reference(name):
                            int(g["block_size"]), compat=True)
     ref = g["out"].astype(np.float32)
     np.testing.assert_allclose(y.astype(np.float32), ref, rtol=2e-3, atol=2e-3)
+
+
+# ------------------------------------------------------------------ 16-bit MFMA arithmetic
+@pytest.mark.parametrize("name,bf16", [("f16_mixed", 0), ("f16_extremes", 0), ("f16_targeted", 0),
+                                       ("bf16_mixed", 1)])
+def test_mfma16_model_matches_hardware(name, bf16):
+    """The oracle's model of v_mfma_f32_32x32x16_{f16,bf16} (orc_mfma16_tiles) reproduces
+    outputs recorded on an MI355X (tests/golden/mfma16_probe.npz, made by
+    tools/mfma_f16_probe.{hip,py}): exponent extremes, fp16 subnormals, f32-subnormal
+    accumulators, cancellation, Gram-like chains."""
+    g = load_golden("mfma16_probe")
+    D = orc.mfma16_tiles(g[name + "_A"], g[name + "_B"], g[name + "_C"], bf16=bf16)
+    ref = g[name + "_D"]
+    same = (D.view(np.uint32) == ref.view(np.uint32)) | ((D == 0) & (ref == 0))
+    assert same.all(), int((~same).sum())
+
+
+def test_gram16_chain_properties():
+    """orc_gram16: symmetric; continuing a chain batch by batch (batches of multiples of 8 rows)
+    equals one call; close to the f64 Gram; zero rows are no-ops."""
+    rng = np.random.default_rng(5)
+    X = (rng.standard_normal((200, 48)) * np.where(rng.random(48) < 0.1, 30, 1)).astype(np.float16)
+    G = orc.gram16(X)
+    assert np.array_equal(G, G.T)
+    G2 = orc.gram16(X[96:], orc.gram16(X[:96]))
+    assert np.array_equal(G, G2)
+    Xz = np.concatenate([X, np.zeros((8, 48), np.float16)])
+    assert np.array_equal(orc.gram16(Xz), G)
+    ref = X.astype(np.float64).T @ X.astype(np.float64)
+    scale = np.sqrt(np.outer(np.diag(ref), np.diag(ref)))
+    assert np.max(np.abs(G - ref) / scale) < 1e-6
