@@ -5,7 +5,9 @@ Llama-2-7B q_proj-shaped linear (4096 x 4096, fp16 weights) per GPU per step, ca
 N = 262144 activation rows (the reference CLI default 128 samples x 2048 tokens, fp16,
 synthetic with 1 % x20 outlier channels), variant M (main.py:102-230): Gram -> damping ->
 Cholesky inverse -> 32 blocks of [SSR select -> ATQ init/ITF/AGA -> error feedback].
-Arithmetic is fp32 throughout (dtype "f32"); inputs are resident in HBM before timing.
+Arithmetic: the Gram of the fp16 activations runs on the fp16 MFMA (f32 accumulate; the oracle
+restates its rounding); everything after it is fp32.  Inputs are resident in HBM
+before timing.
 
 N>1 (torchrun, one rank per GPU): every rank quantises its own layer (weak scaling) and the
 results (2-bit packed codes, scales, permutation) are gathered to rank 0 over RCCL inside the
@@ -27,7 +29,8 @@ import pt2q_loader  # noqa: E402
 pt2q = pt2q_loader.load()
 from pt2q import sharding  # noqa: E402
 
-MI355X_F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (dense f32 MFMA)
+MI355X_F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md:42 (dense f32 MFMA)
+MI355X_F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md:43 (dense fp16/bf16 MFMA, no sparsity)
 MI355X_HBM_PEAK_GBS = 8000.0
 
 
@@ -140,8 +143,8 @@ def main():
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / max(a.steps, 1)
 
-    # dominant kernel: the symmetric f32-MFMA Gram XᵀX, timed alone with HIP events on the
-    # stream it is launched on (torch's current stream)
+    # dominant kernel: the symmetric Gram XᵀX (16-bit MFMA for fp16/bf16 X, f32 MFMA for f32 X),
+    # timed alone with HIP events on the stream it is launched on (torch's current stream)
     G = torch.empty((m, m), dtype=torch.float32, device=dev)
     reps = 3
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -168,6 +171,13 @@ def main():
     torch.cuda.synchronize()
     s_layer_2048 = (time.perf_counter() - t2) / 5
 
+    if a.io_dtype == "fp32":
+        kname = "gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)"
+        peak = MI355X_F32_MFMA_PEAK_TFLOPS
+    else:
+        kname = ("gram16x_kernel (symmetric Gram XᵀX: LDS-DMA staging, ds_read_b64_tr_b16, "
+                 "16-bit MFMA 32x32x16, f32 accumulate)")
+        peak = MI355X_F16_MFMA_PEAK_TFLOPS
     if rank == 0:
         res = {
             "metric": "weight-columns quantized/sec (d=4096 linear, 262144 calibration rows)",
@@ -181,15 +191,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "fp16->f32" if a.io_dtype != "fp32" else "f32",
             "data": "synthetic (counter-hash weights std 0.02; unit-variance activations, 1% x20 outlier channels)",
             "config": {"workload": f"llama2-7b q_proj {n}x{m}, N={N} (CLI 128x2048), variant M, "
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
                        "n": n, "m": m, "tokens": N, "io_dtype": a.io_dtype, "block_size": bs,
                        "parallelism": f"layer-sharded x{world}" + (", rccl gather" if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": "gram16_streamk_kernel (symmetric Gram XᵀX: LDS-DMA fp16 staging, f32 MFMA 32x32x2)",
-                         "achieved": achieved, "peak": MI355X_F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / MI355X_F32_MFMA_PEAK_TFLOPS, "traffic": None,
+            "roofline": {"bound": "mfma", "kernel": kname,
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": None,
                          "avg_launch_ms": gram_ms, "flops_per_launch": gram_flops},
             "extra": {"s_per_layer_n2048": s_layer_2048,
                       "cols_per_s_n2048": m / s_layer_2048,
