@@ -38,19 +38,38 @@ constexpr int GX_DMA_PER_STAGE = 12;        // LDS-DMA wave-instructions per wav
 
 __device__ uint4 gx_zero16;  // the source of out-of-range chunks (zero-initialised)
 
-// Upper tiles of the 128 x 256 grid, column-block major: block tj holds ti = 0 .. 2tj+1.
-PT2Q_DEV void gx_tile(int a, int TI, int& ti, int& tj) {
-  int t = 0;
-  for (;;) {
-    const int c = min(2 * t + 2, TI);
-    if (a < c) {
-      ti = a;
-      tj = t;
-      return;
+// Upper tiles of the 128 x 256 grid (tile (ti, tj) exists iff ti <= 2tj + 1), ordered by
+// super-blocks of (2SJ) x SJ tiles (column-block major over super-blocks, column major inside
+// one), so that a contiguous run of the order -- one XCD's share -- covers a compact square of
+// G and its workgroups read few distinct panels of X through their common L2.
+PT2Q_DEV int gx_col_count(int tj, int lo, int hi) {  // tiles ti in [lo, hi) of column tj
+  return max(0, min(hi, 2 * tj + 2) - lo);
+}
+
+PT2Q_DEV void gx_tile(int a, int TI, int TJ, int SJ, int& ti, int& tj) {
+  const int SI = 2 * SJ;
+  for (int J = 0; J * SJ < TJ; ++J) {
+    const int tj1 = min(TJ, (J + 1) * SJ);
+    for (int I = 0; I * SI < TI; ++I) {
+      const int lo = I * SI, hi = min(TI, lo + SI);
+      int c = 0;
+      for (int t = J * SJ; t < tj1; ++t) c += gx_col_count(t, lo, hi);
+      if (a >= c) {
+        a -= c;
+        continue;
+      }
+      for (int t = J * SJ; t < tj1; ++t) {
+        const int ct = gx_col_count(t, lo, hi);
+        if (a < ct) {
+          ti = lo + a;
+          tj = t;
+          return;
+        }
+        a -= ct;
+      }
     }
-    a -= c;
-    ++t;
   }
+  ti = tj = 0;  // unreachable for a < gx_ntile
 }
 
 long gx_ntile(int m) {
@@ -96,11 +115,77 @@ PT2Q_DEV void gx_stage(const uint16_t* X, long ld, int i0, int j0, int k0, int k
   }
 }
 
-// The MFMA operand of this lane: 8 k-consecutive elements (rows 8h .. 8h+7 of the k16 step)
-// of one column, as two transposed 4-row reads.
-PT2Q_DEV s16x8 gx_frag(const uint8_t* p, int rowb) {
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 4 * rowb));
+// Fast staging (DMA path, whole stage in range): this lane's 12 chunk sources as byte offsets
+// from the stage's first k-row (fixed for a piece), so each DMA is one global_load_lds with a
+// scalar base and a 32-bit vector offset, and the LDS destination is wave-uniform (M0).
+PT2Q_DEV void gx_voff(long ld, int i0, int j0, uint32_t (&vo)[12]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (wave * 4 + j) * 4 + (lane >> 4), c = (lane & 15) ^ ((row & 3) << 2);
+    vo[j] = (uint32_t)(((long)row * ld + i0 + 8 * c) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = (wave * 8 + j) * 2 + (lane >> 5), c = (lane & 31) ^ ((row & 3) << 2);
+    vo[4 + j] = (uint32_t)(((long)row * ld + j0 + 8 * c) * 2);
+  }
+}
+
+// Quarter qq of a fast stage: A chunk j = qq, B chunks j = 2qq, 2qq + 1.
+PT2Q_DEV void gx_stage_q(const uint16_t* Xk0, const uint32_t (&vo)[12], uint8_t* stg, int qq) {
+#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
+  return;
+#endif
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* sb = (const char*)Xk0;
+  typedef __attribute__((address_space(3))) void* lptr;
+  __builtin_amdgcn_global_load_lds((const void*)(sb + vo[qq]), (lptr)(stg + (wave * 4 + qq) * 1024), 16, 0, 0);
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vo[4 + 2 * qq + e]),
+                                     (lptr)(stg + GX_ASTG + (wave * 8 + 2 * qq + e) * 1024), 16, 0, 0);
+}
+
+// LDS reads are inline asm: hipcc cannot tell them apart from the LDS-DMA writes still in
+// flight and would wait vmcnt(0) before the first read of every stage (cdna_hip_programming.md
+// §5 trap 4a).  Ordering is by hand: counted vmcnt + raw barrier for the DMA, lgkmcnt(0) tied
+// to the fragment registers before the MFMAs that use them.
+template <int OFF>
+PT2Q_DEV s16x4 gx_tr(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// The 12 transposed reads of one k16 step (rows 16S .. 16S+15 of the stage): per fragment 8
+// k-consecutive elements of one column = two 4-row reads.
+struct GxFrags {
+  s16x4 lo[6], hi[6];  // 0, 1: A tiles mt; 2..5: B tiles nt
+};
+
+template <int S>
+PT2Q_DEV void gx_read(GxFrags& f, const uint32_t (&addr)[6]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    f.lo[q] = gx_tr<S * 16 * GX_AROW>(addr[q]);
+    f.hi[q] = gx_tr<S * 16 * GX_AROW + 4 * GX_AROW>(addr[q]);
+  }
+#pragma unroll
+  for (int q = 2; q < 6; ++q) {
+    f.lo[q] = gx_tr<S * 16 * GX_BROW>(addr[q]);
+    f.hi[q] = gx_tr<S * 16 * GX_BROW + 4 * GX_BROW>(addr[q]);
+  }
+}
+
+PT2Q_DEV void gx_wait(GxFrags& f) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]),
+                 "+v"(f.lo[5]), "+v"(f.hi[0]), "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3]),
+                 "+v"(f.hi[4]), "+v"(f.hi[5]));
+}
+
+PT2Q_DEV s16x8 gx_cat(s16x4 lo, s16x4 hi) {
   return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -126,6 +211,21 @@ struct GxTile {
     return j0 + wc * 128 + nt * 32 + (lane & 31);
   }
 
+  template <bool BF16>
+  PT2Q_DEV void mma(const GxFrags& f) {
+#ifdef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
+    return;
+#endif
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = gx_mfma<BF16>(gx_cat(f.lo[mt], f.hi[mt]), gx_cat(f.lo[2 + nt], f.hi[2 + nt]),
+                                    acc[mt][nt]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+
   // continue the chains over X rows [kbeg, kend) (kbeg a multiple of 64)
   template <bool BF16, bool DMA>
   PT2Q_DEV void chain(const uint16_t* X, long ld, int M, int i0, int j0, int kbeg, int kend,
@@ -147,33 +247,54 @@ struct GxTile {
       const int cf = wc * 16 + nt * 4 + 2 * gh + (p >> 1);
       offB[nt] = GX_ASTG + (8 * h + q) * GX_BROW + ((cf ^ (q << 2)) << 4) + 8 * (p & 1);
     }
+    const bool fastcols = DMA && i0 + GX_BM <= M && j0 + GX_BN <= M;
+    uint32_t vo[12];
+    if (fastcols) gx_voff(ld, i0, j0, vo);
     gx_stage<DMA>(X, ld, i0, j0, kbeg, kend, M, smem);
     if (nk > 1) gx_stage<DMA>(X, ld, i0, j0, kbeg + GX_BK, kend, M, smem + GX_STG);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
     for (int t = 0; t < nk; ++t) {
+      // stage t landed (this wave's DMAs; stage t+1 may stay in flight), then a raw barrier:
+      // __syncthreads()'s fence would wait vmcnt(0) and drain the prefetch every step.  The
+      // barrier also retires every wave's reads of stage t-1, whose slot stage t+2 reuses.
       if (t + 1 < nk)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GX_DMA_PER_STAGE) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + 2 < nk)
-        gx_stage<DMA>(X, ld, i0, j0, kbeg + (t + 2) * GX_BK, kend, M, smem + ((t + 2) % GX_NS) * GX_STG);
-      const uint8_t* S = smem + (t % GX_NS) * GX_STG;
+      asm volatile("s_barrier" ::: "memory");
+      // stage t+2 goes into the slot stage t-1 used, issued in quarters between the k16 steps
+      const bool pre = t + 2 < nk;
+      const int kn = kbeg + (t + 2) * GX_BK;
+      uint8_t* stn = smem + ((t + 2) % GX_NS) * GX_STG;
+      const bool fast = pre && fastcols && kn + GX_BK <= kend;
+      const uint16_t* Xn = X + (long)kn * ld;
+      if (pre && !fast) gx_stage<DMA>(X, ld, i0, j0, kn, kend, M, stn);
+      const uint32_t base = lds0 + (uint32_t)((t % GX_NS) * GX_STG);
+      uint32_t addr[6];
 #pragma unroll
-      for (int s = 0; s < GX_BK / 16; ++s) {
-        s16x8 a[2], b[4];
+      for (int q = 0; q < 2; ++q) addr[q] = base + offA[q];
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) a[mt] = gx_frag(S + s * 16 * GX_AROW + offA[mt], GX_AROW);
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) b[nt] = gx_frag(S + s * 16 * GX_BROW + offB[nt], GX_BROW);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = gx_mfma<BF16>(a[mt], b[nt], acc[mt][nt]);
-        __builtin_amdgcn_s_setprio(0);
-      }
+      for (int q = 0; q < 4; ++q) addr[2 + q] = base + offB[q];
+      GxFrags f0, f1;
+      gx_read<0>(f0, addr);
+      gx_wait(f0);
+      gx_read<1>(f1, addr);
+      if (fast) gx_stage_q(Xn, vo, stn, 0);
+      mma<BF16>(f0);
+      gx_wait(f1);
+      gx_read<2>(f0, addr);
+      if (fast) gx_stage_q(Xn, vo, stn, 1);
+      mma<BF16>(f1);
+      gx_wait(f0);
+      gx_read<3>(f1, addr);
+      if (fast) gx_stage_q(Xn, vo, stn, 2);
+      mma<BF16>(f0);
+      gx_wait(f1);
+      if (fast) gx_stage_q(Xn, vo, stn, 3);
+      mma<BF16>(f1);
     }
-    __syncthreads();  // the ring is reused by the next piece
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // the ring is reused by the next piece
   }
 };
 
@@ -185,7 +306,7 @@ struct GxTile {
 // full tiles, then the head piece of its first tile, continuing the partial that workgroup
 // r-1 (= w - NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
 template <bool BF16, bool DMA>
-__global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int Kp, long ntile, int NG,
+__global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ, int SJ, int Kp, long ntile, int NG,
                                                       int R, int* flags, int* timeout) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[GX_LDS];
   const uint16_t* X = (const uint16_t*)g.A;
@@ -216,7 +337,7 @@ __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int Kp
     }
     a += (int)t0;  // global tile index (flags are per tile)
     int ti, tj;
-    gx_tile(a, TI, ti, tj);
+    gx_tile(a, TI, TJ, SJ, ti, tj);
     const int i0 = ti * GX_BM, j0 = tj * GX_BN;
     GxTile F;
     if (from_partial && threadIdx.x == 0) {
@@ -298,7 +419,10 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
   if (g.in_dtype != PT2Q_F16 && g.in_dtype != PT2Q_BF16) return PT2Q_E_ARG;
   if (g.M != g.N || g.A != g.B || g.lda != g.ldb) return PT2Q_E_ARG;
   const int m = g.M;
-  const int TI = ceil_div(m, GX_BM);
+  const int TI = ceil_div(m, GX_BM), TJ = ceil_div(m, GX_BN);
+  static const char* sj_env = std::getenv("PT2Q_GRAM_SUPER");  // tuning override
+  // super-block side ~ the square one XCD's share of the triangle covers
+  const int SJ = sj_env ? std::max(1, std::atoi(sj_env)) : (m <= 6144 ? 4 : 8);
   const long ntile = gx_ntile(m);
   const int Kp = std::max(1, ceil_div(g.K, GX_BK)) * GX_BK;  // K = 0: one all-zero stage
   const long W = ntile * Kp;
@@ -322,12 +446,13 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
   }
   (void)W;
   int* timeout = split ? flags + ntile : nullptr;
-  const bool dma = ((uintptr_t)g.A % 16 == 0) && (g.lda % 8 == 0) && (m % 8 == 0);
+  // (fast staging keeps a stage's byte offsets in 32 bits: 64 rows * lda * 2 < 2^32)
+  const bool dma = ((uintptr_t)g.A % 16 == 0) && (g.lda % 8 == 0) && (m % 8 == 0) && g.lda < (1l << 25);
   const bool bf = g.in_dtype == PT2Q_BF16;
-  void (*k)(GemmDesc, int, int, long, int, int, int*, int*) =
+  void (*k)(GemmDesc, int, int, int, int, long, int, int, int*, int*) =
       bf ? (dma ? gram16x_kernel<true, true> : gram16x_kernel<true, false>)
          : (dma ? gram16x_kernel<false, true> : gram16x_kernel<false, false>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, Kp, ntile, NG, R, flags, timeout);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, TJ, SJ, Kp, ntile, NG, R, flags, timeout);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

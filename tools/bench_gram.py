@@ -23,6 +23,7 @@ for _ in range(reps):
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / reps
+peak, pname = (157.3, "f32") if dt == torch.float32 else (2500.0, "16-bit")
 fl = float(N) * m * (m + 1)
 print(f"gram N={N} m={m} {dt} tile={os.environ.get('PT2Q_GEMM_TILE', 'auto')}: {ms:.2f} ms  "
-      f"{fl / ms / 1e9:.1f} TFLOP/s ({fl / ms / 1e9 / 157.3 * 100:.1f}% of f32 MFMA peak)")
+      f"{fl / ms / 1e9:.1f} TFLOP/s ({fl / ms / 1e9 / peak * 100:.1f}% of {pname} MFMA peak)")

@@ -20,7 +20,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GRAM = "streamk_kernel"  # gram16_streamk_kernel (fp16/bf16) or gram_streamk_kernel
+GRAM = "gram16x_kernel"  # the 16-bit Gram (fp16/bf16 X); gram_streamk_kernel for f32 X
 CUS, SIMDS, XCDS = 256, 4, 8
 
 
@@ -35,6 +35,17 @@ def pmc(src, counter):
     if not vals:
         raise SystemExit(f"no {GRAM} dispatch in {path}")
     return sum(vals.values()) / len(vals), len(vals)
+
+
+def extra_counters(src):
+    """Optional passes: L2 hit/miss and LDS bank conflicts of the Gram (per launch)."""
+    out = {}
+    for c in ("TCC_HIT_sum", "TCC_MISS_sum", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS"):
+        if os.path.exists(os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")):
+            out[c] = pmc(src, c)[0]
+    if "TCC_HIT_sum" in out and "TCC_MISS_sum" in out:
+        out["l2_hit_frac"] = out["TCC_HIT_sum"] / max(1.0, out["TCC_HIT_sum"] + out["TCC_MISS_sum"])
+    return out
 
 
 def gram_duration_ns(src, counter):
@@ -77,6 +88,7 @@ def main():
         "l2_fabric_GBps": traffic / dur_ns,
         "clock_GHz": cycles / dur_ns,
         "mfma_busy_frac": mfma_util,
+        **extra_counters(src),
         "source": f"profiles/{tag}_summary.md: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
                   "SQ_VALU_MFMA_BUSY_CYCLES | GRBM_GUI_ACTIVE, separate passes; "
                   "FETCH_SIZE x2 (gfx950), KB x1024; includes Infinity-Cache hits",
@@ -99,7 +111,10 @@ def main():
                      f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.1f} |")
     lines += ["", "## Gram PMC (separate passes, `tools/bench_gram.py 262144 4096 fp16`)", ""]
     for k in ("fetch_size_kb", "write_size_kb", "hbm_bytes_per_launch", "algorithmic_bytes_per_launch",
-              "avg_duration_ms_pmc_run", "l2_fabric_GBps", "clock_GHz", "mfma_busy_frac"):
+              "avg_duration_ms_pmc_run", "l2_fabric_GBps", "clock_GHz", "mfma_busy_frac",
+              "l2_hit_frac", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_LDS"):
+        if k not in rec:
+            continue
         v = rec[k]
         lines.append(f"- {k}: {v:.4g}" if isinstance(v, float) else f"- {k}: {v}")
     if len(sys.argv) > 2:
