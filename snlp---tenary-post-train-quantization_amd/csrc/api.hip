@@ -63,7 +63,7 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
   w.rem[0] = c.take<int>((size_t)m);
   w.rem[1] = c.take<int>((size_t)m);
   w.blk = c.take<int>((size_t)bb);
-  w.counters = c.take<int>((size_t)2 * B);
+  w.counters = c.take<int>((size_t)4 * B);  // [2k, 2k+1] ATQ; [2B+2k, 2B+2k+1] top-k/S1 sync
   w.iters = c.take<int>((size_t)B);
   return c.ok;
 }
@@ -88,7 +88,7 @@ size_t blocks_bytes(int n, int m, int b) {
   add((size_t)m * 4);
   add((size_t)m * 4);
   add((size_t)bb * 4);
-  add((size_t)2 * B * 4);
+  add((size_t)4 * B * 4);
   add((size_t)B * 4);
   (void)c;
   return total;
@@ -115,7 +115,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   // W (n x m) -> Wt (m x ldw, fp32)
   if ((rc = pt2q_launch_transpose_to_f32(W, wdtype, ldw_in, n, m, w.Wt, w.ldw, st)) != PT2Q_OK)
     return rc;
-  if (hipMemsetAsync(w.counters, 0, sizeof(int) * 2 * B, st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(w.counters, 0, sizeof(int) * 4 * B, st) != hipSuccess) return PT2Q_E_HIP;
   if (hipMemsetAsync(iters, 0, sizeof(int) * B, st) != hipSuccess) return PT2Q_E_HIP;
   // rem0 = [0, m)
   if ((rc = pt2q_launch_select_seq(0, 0, 0, m, nullptr, w.blk, w.rem[0], nullptr, st)) != PT2Q_OK)
@@ -136,7 +136,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
         if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st)) != PT2Q_OK)
           return rc;
         if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st,
-                                       s1_in_topk ? A : nullptr, lda, w.S1, w.d)) != PT2Q_OK)
+                                       s1_in_topk ? A : nullptr, lda, w.S1, w.d,
+                                       w.counters + 2 * B + 2 * k)) != PT2Q_OK)
           return rc;
       } else {
         if ((rc = pt2q_launch_select_seq(1, 0, bs, m, rem, w.blk, nrem, perm + processed, st)) != PT2Q_OK)

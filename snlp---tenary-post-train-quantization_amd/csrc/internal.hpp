@@ -15,7 +15,7 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
                                float* part, float* wn, float* sim, hipStream_t st);
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
-                         float* S1 = nullptr, float* d = nullptr);
+                         float* S1 = nullptr, float* d = nullptr, int* sync = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
                            int* newrem, int64_t* perm_out, hipStream_t st);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,

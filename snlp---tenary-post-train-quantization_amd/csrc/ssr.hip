@@ -158,81 +158,217 @@ __global__ __launch_bounds__(1024) void s1_fused_kernel(const float* A, long lda
   s1_block(A, lda, bl, b, gb, s1, S1, d);
 }
 
-// Ordered top-b of r similarities: keys (value desc, position asc), bitonic sort in LDS.
-// Writes blk (selection order), newrem (ascending), perm_out (int64, nullable).
-// With G != nullptr (variant M, b <= 128) the same workgroup then forms S1/d for AGA from the
-// raw Gram over the block it just selected (one launch instead of three).
-__global__ __launch_bounds__(1024) void ssr_topk_kernel(const float* sim, const int* rem, int r,
-                                                        int b, int P, int* blk, int* newrem,
-                                                        int64_t* perm_out, const float* G,
-                                                        long ldg, float* S1, float* d,
-                                                        int keys_floats) {
-  // LDS: keys region (P keys; reused for the S1 gather), r flag bytes, scan ints, b indices,
-  // b partial sums
-  extern __shared__ unsigned long long keys[];
-  unsigned char* sel = (unsigned char*)((float*)keys + keys_floats);
-  int* scan = (int*)(sel + ((r + 15) & ~15));
-  int* bl = scan + 1024;
-  float* s1 = (float*)(bl + 128);
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int e = tid; e < P; e += nt)
-    keys[e] = (e < r) ? (((unsigned long long)orderable(sim[e]) << 32) |
-                         (unsigned long long)(0xFFFFFFFFu - (uint32_t)e))
-                      : 0ull;
-  for (int e = tid; e < r; e += nt) sel[e] = 0;
-  __syncthreads();
-  // bitonic sort, descending
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int idx = tid; idx < P / 2; idx += nt) {
-        int lo = 2 * idx - (idx & (stride - 1));
-        int hi = lo + stride;
-        bool desc = ((lo & size) == 0);
-        unsigned long long a = keys[lo], c = keys[hi];
-        if ((a < c) == desc) {
-          keys[lo] = c;
-          keys[hi] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int t = tid; t < b; t += nt) {
-    int e = (int)(0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFull));
-    int j = rem[e];
-    blk[t] = j;
-    if (G) bl[t] = j;
-    if (perm_out) perm_out[t] = j;
-    sel[e] = 1;
-  }
-  __syncthreads();
-  if (G) s1_block(G, ldg, bl, b, (float*)keys, s1, S1, d);  // keys are dead after the pick
-  // stable compaction of the unselected positions (ascending)
-  const int per = (r + nt - 1) / nt;
-  const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
-  int cnt = 0;
-  for (int e = e0; e < e1; ++e) cnt += !sel[e];
-  // block exclusive scan of cnt: wave-inclusive scan by shuffles, then wave totals
-  const int lane = tid & 63, wv = tid >> 6;
-  int incl = cnt;
+PT2Q_DEV int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(incl, off);
-    if (lane >= off) incl += y;
+    const int y = __shfl_up(v, off);
+    if (lane >= off) v += y;
   }
-  if (lane == 63) scan[wv] = incl;
+  return v;
+}
+
+// Exclusive workgroup scan of v (blockDim.x <= 4096); sc >= 65 ints of LDS.  *total = sum.
+PT2Q_DEV int block_excl_scan(int v, int* sc, int* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+  const int incl = wave_incl_scan(v);
+  if (lane == 63) sc[wv] = incl;
+  __syncthreads();
+  if (wv == 0) {
+    const int x = lane < nw ? sc[lane] : 0;
+    const int xi = wave_incl_scan(x);
+    if (lane < nw) sc[lane] = xi - x;
+    if (lane == 63) sc[64] = xi;
+  }
+  __syncthreads();
+  const int r = sc[wv] + incl - v;
+  *total = sc[64];
+  __syncthreads();  // sc may be reused at once
+  return r;
+}
+
+constexpr int TOPK_THREADS = 1024;
+constexpr int TOPK_HPAD = 257;  // per-wave histogram stride (bank-spread)
+
+// Ordered top-b of r similarities under the total order (value desc, position asc) -- the order
+// torch.topk(sorted=True) gives here (reorder.py:133), keys being unique -- by radix selection:
+// four 8-bit histogram passes over the orderable value bits find the b-th largest value v*;
+// every value > v* is taken, plus the first (by position) b - #(> v*) values equal to v*; the
+// b picks are then ranked among themselves.  Writes blk (selection order), newrem (ascending,
+// reorder.py:139-141), perm_out (int64, nullable).  With G != nullptr (variant M, b <= 128)
+// the same workgroup then forms S1/d for AGA from the raw Gram over the block it just selected.
+// LDS: region0 (max(r + 16*257, b*(b+1)) words: values + wave histograms, later the S1 gather),
+// r flag bytes, scan ints, b picks / their values / block indices / partial sums.
+constexpr int S1_ROWS = TOPK_THREADS / 128;  // S1 rows per helper workgroup
+
+// Helper workgroups 1.. of the top-k launch (variant M): wait for workgroup 0's pick, gather
+// rows of G[blk][blk] in parallel and sum each in l order; the last one to finish forms d in j
+// order (the s1_block order).  Workgroup 0 is dispatched first and waits on nobody, so the
+// spin cannot deadlock.  sync[0]: pick published; sync[1]: helpers done.
+PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* S1, float* d,
+                        int* sync, float* gb) {
+  const int tid = threadIdx.x, nh = gridDim.x - 1;
+  if (tid == 0) {
+    long spins = 0;
+    while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+           ++spins < (1l << 26))
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  const int jj = tid >> 7, l = tid & 127;
+  const int j = (blockIdx.x - 1) * S1_ROWS + jj;
+  if (j < b && l < b) gb[jj * 129 + l] = G[(long)blk[j] * ldg + blk[l]];
+  __syncthreads();
+  if (l == 0 && j < b) {
+    const float* row = gb + jj * 129;
+    float s = 0.0f;
+    int q = 0;
+    for (; q + 8 <= b; q += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = row[q + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = s + t[u];
+    }
+    for (; q < b; ++q) s = s + row[q];
+    S1[j] = s;
+  }
+  __shared__ int last;
   __syncthreads();
   if (tid == 0) {
-    int acc = 0;
-    for (int q = 0; q < (nt >> 6); ++q) {
-      int v = scan[q];
-      scan[q] = acc;
-      acc += v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = atomicAdd(&sync[1], 1) == nh - 1;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid < b) gb[tid] = S1[tid];
+  __syncthreads();
+  if (tid == 0) {
+    float dd = 0.0f;
+    for (int q = 0; q < b; ++q) dd = dd + gb[q];
+    *d = dd;
+  }
+}
+
+__global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim, const int* rem, int r,
+                                                                int b, int* blk, int* newrem,
+                                                                int64_t* perm_out, const float* G,
+                                                                long ldg, float* S1, float* d,
+                                                                int region0, int* sync) {
+  extern __shared__ uint32_t vals[];
+  if (blockIdx.x > 0) {
+    s1_helper(G, ldg, blk, b, S1, d, sync, (float*)vals);
+    return;
+  }
+  int* hist = (int*)(vals + r);
+  unsigned char* sel = (unsigned char*)(vals + region0);
+  int* sc = (int*)(sel + ((r + 15) & ~15));
+  int* pick = sc + 80;                  // b positions, ascending
+  uint32_t* pv = (uint32_t*)(pick + b); // their values
+  int* bl = (int*)(pv + b);             // b block indices (selection order)
+  float* s1 = (float*)(bl + b);
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6;
+  for (int e = tid; e < r; e += nt) vals[e] = orderable(sim[e]);
+  uint32_t prefix = 0, pmask = 0;
+  int kk = b;  // rank (1-based) of v* among the values matching prefix
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 16 * TOPK_HPAD; i += nt) hist[i] = 0;
+    __syncthreads();
+    int* hw = hist + wv * TOPK_HPAD;
+    for (int e = tid; e < r; e += nt) {
+      const uint32_t u = vals[e];
+      if ((u & pmask) == prefix) atomicAdd(&hw[(u >> shift) & 255], 1);
+    }
+    __syncthreads();
+    int* hm = hist + 16 * TOPK_HPAD;  // merged histogram
+    if (tid < 256) {
+      int t = 0;
+#pragma unroll
+      for (int w = 0; w < TOPK_THREADS / 64; ++w) t += hist[w * TOPK_HPAD + tid];
+      hm[tid] = t;
+    }
+    __syncthreads();
+    if (wv == 0) {  // lane l owns bins 255-4l .. 252-4l (descending)
+      int c[4], s = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        c[q] = hm[255 - 4 * lane - q];
+        s += c[q];
+      }
+      const int incl = wave_incl_scan(s);
+      int run = incl - s;
+      if (run < kk && kk <= incl) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (run < kk && kk <= run + c[q]) {
+            sc[70] = 255 - 4 * lane - q;
+            sc[71] = kk - run;
+          }
+          run += c[q];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= (uint32_t)sc[70] << shift;
+    pmask |= 255u << shift;
+    kk = sc[71];
+    __syncthreads();
+  }
+  // prefix = v*; the first kk positions holding v* are picked, with every value above it
+  const int per = (r + nt - 1) / nt;
+  const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
+  int ceq = 0, tot;
+  for (int e = e0; e < e1; ++e) ceq += vals[e] == prefix;
+  int eq = block_excl_scan(ceq, sc, &tot);
+  int cs = 0, cu = 0;
+  for (int e = e0; e < e1; ++e) {
+    const uint32_t u = vals[e];
+    const bool s = u > prefix || (u == prefix && eq++ < kk);
+    sel[e] = s;
+    cs += s;
+    cu += !s;
+  }
+  // one scan for both compactions (r < 2^16): picks and the unselected remainder, ascending
+  const int both = block_excl_scan((cs << 16) | cu, sc, &tot);
+  int os = both >> 16, ou = both & 0xFFFF;
+  for (int e = e0; e < e1; ++e) {
+    if (sel[e]) {
+      pick[os] = e;
+      pv[os++] = vals[e];
+    } else {
+      newrem[ou++] = rem[e];
     }
   }
   __syncthreads();
-  int o = scan[wv] + incl - cnt;
-  for (int e = e0; e < e1; ++e)
-    if (!sel[e]) newrem[o++] = rem[e];
+  // rank of pick t: picks above it in (value desc, position asc); picks are position-ascending
+  for (int t = tid; t < b; t += nt) {
+    const uint32_t ut = pv[t];
+    int rank = 0, s = 0;
+    for (; s + 8 <= b; s += 8) {
+      uint32_t us[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) us[u] = pv[s + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rank += (us[u] > ut) | ((us[u] == ut) & (s + u < t));
+    }
+    for (; s < b; ++s) rank += (pv[s] > ut) | ((pv[s] == ut) & (s < t));
+    const int j = rem[pick[t]];
+    blk[rank] = j;
+    if (perm_out) perm_out[rank] = j;
+  }
+  (void)lane;
+  (void)bl;
+  (void)s1;
+  if (G) {  // publish the pick to the S1 helpers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Sequential block (use_ssr=False: main.py:167-169, gptq.py:135-137) or "take the rest"
@@ -446,18 +582,17 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
 
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G, long ldg, float* S1,
-                         float* d) {
-  int P = 1;
-  while (P < r) P <<= 1;
+                         float* d, int* sync) {
   if (G && b > 128) return PT2Q_E_ARG;
-  int keys_floats = 2 * P;
-  if (G && keys_floats < b * (b + 1)) keys_floats = b * (b + 1);
-  keys_floats = (keys_floats + 3) & ~3;
-  size_t lds = (size_t)keys_floats * 4 + (size_t)((r + 15) & ~15) + 1024 * sizeof(int) +
-               128 * sizeof(int) + 128 * sizeof(float);
+  if (b <= 0 || b > r || r >= 65536) return PT2Q_E_UNSUPPORTED;
+  if (G && !sync) return PT2Q_E_ARG;  // sync: 2 ints the caller zeroed before this launch
+  const int region0 = (r + 17 * TOPK_HPAD + 3) & ~3;  // >= S1_ROWS * 129 for the helpers
+  const size_t lds = (size_t)region0 * 4 + (size_t)((r + 15) & ~15) + 80 * sizeof(int) +
+                     (size_t)b * 4 * sizeof(int);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
-  hipLaunchKernelGGL(ssr_topk_kernel, dim3(1), dim3(1024), lds, st, sim, rem, r, b, P, blk,
-                     newrem, perm_out, G, ldg, S1, d, keys_floats);
+  const int grid = G ? 1 + ceil_div(b, S1_ROWS) : 1;
+  hipLaunchKernelGGL(ssr_topk_kernel, dim3(grid), dim3(TOPK_THREADS), lds, st, sim, rem, r, b, blk,
+                     newrem, perm_out, G, ldg, S1, d, region0, sync);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

@@ -237,6 +237,21 @@ def test_ssr_vs_oracle_and_reference(pt2q, name):
     np.testing.assert_array_equal(host(newrem), g["newrem"])
 
 
+@pytest.mark.parametrize("n,m,b,dup", [(256, 700, 128, 7), (512, 4096, 128, 3),
+                                       (64, 300, 256, 2), (128, 11008, 128, 5)])
+def test_ssr_topk_ties_vs_oracle(pt2q, n, m, b, dup):
+    """Exact similarity ties: repeated columns and all-zero columns tie bitwise, so the pick
+    and its order rest on the position tie-break (value desc, position asc)."""
+    W = synth.weights(40 + m, n, m)
+    W[:, 1::dup] = W[:, :1]  # every dup-th column equals column 0
+    W[:, 5::11] = 0.0
+    rem = np.arange(m, dtype=np.int64)[(np.arange(m) % 13) != 4]
+    blk, newrem = pt2q.select_next_block_ssr(cuda(W), cuda(rem), b)
+    rblk, rnew = orc.select_next_block_ssr(W, rem, b)
+    np.testing.assert_array_equal(host(blk), rblk)
+    np.testing.assert_array_equal(host(newrem), rnew)
+
+
 def test_fill_synthetic_matches_numpy(pt2q):
     a = pt2q.fill_synthetic((300, 257), 1234, std=0.02)
     np.testing.assert_array_equal(host(a), synth.weights(1234, 300, 257))
