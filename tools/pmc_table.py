@@ -6,21 +6,21 @@ vals = defaultdict(dict)
 dur = {}
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        if "gram16x" not in r["Kernel_Name"]:
+        if "gram16" not in r["Kernel_Name"]:
             continue
         k = int(r["Dispatch_Id"])
         vals[k][r["Counter_Name"]] = vals[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_kernel_trace.csv"))):
     for r in csv.DictReader(open(f)):
-        if "gram16x" in r["Kernel_Name"]:
+        if "gram16" in r["Kernel_Name"]:
             dur.setdefault(os.path.dirname(f), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 # dispatches are numbered per pass; group by order within the pass
 bypass = defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
-    ids = sorted({int(r["Dispatch_Id"]) for r in csv.DictReader(open(f)) if "gram16x" in r["Kernel_Name"]})
+    ids = sorted({int(r["Dispatch_Id"]) for r in csv.DictReader(open(f)) if "gram16" in r["Kernel_Name"]})
     rows = defaultdict(dict)
     for r in csv.DictReader(open(f)):
-        if "gram16x" in r["Kernel_Name"]:
+        if "gram16" in r["Kernel_Name"]:
             k = int(r["Dispatch_Id"])
             rows[k][r["Counter_Name"]] = rows[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     for pos, k in enumerate(ids):
