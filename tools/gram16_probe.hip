@@ -46,25 +46,6 @@ int main(int argc, char** argv) {
   g.lda = 0; g.ldb = 0;
   ms = time_launch(g, (int*)F, reps);
   printf("resident X N=%ld m=%d: %.3f ms  %.1f TFLOP/s\n", N, m, ms, fl / ms / 1e9);
-#ifdef GX_PROBE_STAMPS
-  {
-    g.lda = m; g.ldb = m;
-    pt2q_launch_gram16(g, (int*)F, 0);
-    (void)hipDeviceSynchronize();
-    std::vector<unsigned long> st(4096);
-    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(gx_stamps), sizeof(unsigned long) * 4096);
-    unsigned long t0 = ~0ul;
-    for (int w = 0; w < 256; ++w) t0 = std::min(t0, st[w * 4]);
-    double mx[3] = {0, 0, 0}, mn[3] = {1e30, 1e30, 1e30}, av[3] = {0, 0, 0};
-    for (int w = 0; w < 256; ++w)
-      for (int k = 0; k < 3; ++k) {
-        double v = (st[w * 4 + k] - t0) / 100.0;  // us
-        mx[k] = std::max(mx[k], v); mn[k] = std::min(mn[k], v); av[k] += v / 256;
-      }
-    const char* nm[3] = {"start", "phase1 end", "end"};
-    for (int k = 0; k < 3; ++k) printf("%-11s us: min %.1f avg %.1f max %.1f\n", nm[k], mn[k], av[k], mx[k]);
-  }
-#endif
   int info = 0;
   (void)hipMemcpy(&info, (int*)F + gx_ntile(m), 4, hipMemcpyDeviceToHost);
   printf("timeout flag %d\n", info);
