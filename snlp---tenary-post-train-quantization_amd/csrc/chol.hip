@@ -106,13 +106,9 @@ PT2Q_DEV void load_diag_block(float (*Dus)[NB + 4], float* dg, const float* A, l
 // Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution against the factored
 // diagonal block, continuing each element's chain from the already-updated A value.  Four
 // lanes share a column (16 rows each); the lane owning row k divides and broadcasts x_k.
-__global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int p0, int nb,
-                                                         int m) {
-  __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
-  __shared__ float dg[NB];
-  load_diag_block(Dus, dg, A, lda, p0, nb);
-  __syncthreads();
-  const int i = p0 + nb + (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
+                         float (*Dus)[NB + 4], float* dg) {
+  const int i = p0 + nb + (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
   const int sub = threadIdx.x & (LPR - 1);
   const bool valid = i < m;
   float x[SEG];
@@ -144,13 +140,9 @@ __global__ __launch_bounds__(256) void chol_panel_kernel(float* A, long lda, int
 // Ui[k][c0..] holds the running chains for k < c0 (zero otherwise).  Four lanes share a row.
 // For rows inside the block, columns left of the diagonal start at zero and only ever receive
 // zero terms, so they need no mask until the final store.
-__global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long ldu, float* Ui,
-                                                            long ldi, int c0, int nb) {
-  __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
-  __shared__ float dg[NB];
-  load_diag_block(Dus, dg, U, ldu, c0, nb);
-  __syncthreads();
-  const int k = (blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float (*Dus)[NB + 4],
+                            float* dg) {
+  const int k = (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
   const int sub = threadIdx.x & (LPR - 1);
   const bool valid = k < c0 + nb;
   float acc[SEG];
@@ -180,6 +172,21 @@ __global__ __launch_bounds__(256) void trtri_inblock_kernel(const float* U, long
   }
 }
 
+// Block J after its diagonal factor: workgroups [0, npanel) solve the panel (rows of block J
+// right of it), the rest run the in-block triangular inverse of block J (which needs only the
+// factored diagonal block and the inverse chains of earlier blocks) -- one launch.
+__global__ __launch_bounds__(256) void chol_panel_trtri_kernel(float* U, long ld, int p0, int nb,
+                                                               int m, float* Ui, int npanel) {
+  __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
+  __shared__ float dg[NB];
+  load_diag_block(Dus, dg, U, ld, p0, nb);
+  __syncthreads();
+  if ((int)blockIdx.x < npanel)
+    chol_panel(U, ld, p0, nb, m, blockIdx.x, Dus, dg);
+  else
+    trtri_inblock(Ui, ld, p0, nb, blockIdx.x - npanel, Dus, dg);
+}
+
 __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m) {
   long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (long)m * m) return;
@@ -191,52 +198,21 @@ __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, 
 
 namespace {
 
-// Two extra streams per device: the triangular-inverse chain (trtri of column block J needs
-// only rows <= J of U) and the bulk trailing update of the factorisation (look-ahead: only the
-// next block row is updated on the critical path).  Captured into a hipGraph the fork/join
-// events become graph edges.
-struct SideStream {
-  hipStream_t s = nullptr, bulk = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, bulk_done = nullptr;
-};
-
-SideStream* side_stream() {
-  static SideStream ss[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& x = ss[dev];
-  if (!x.s) {
-    if (hipStreamCreateWithFlags(&x.bulk, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.bulk_done, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  }
-  return &x;
-}
-
 // U[r0.., c0..] (rows x cols) -= U[p0 + k][r0 + i] * U[p0 + k][c0 + j] over the nb rows of
 // block J (chains continue from U, k ascending).
-int trailing_update(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols,
-                    bool upper, hipStream_t st) {
-  if (rows <= 0 || cols <= 0) return PT2Q_OK;
+GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols) {
   GemmDesc g{};
   g.M = rows; g.N = cols; g.K = nb;
   g.A = U + (long)p0 * ld + r0; g.lda = ld; g.a_layout = LAY_KMAJOR;
   g.B = U + (long)p0 * ld + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;
   g.in_dtype = PT2Q_F32;
   g.C = U + (long)r0 * ld + c0; g.ldc = ld;
-  g.mode = GEMM_CHAIN_NEG; g.upper = upper ? 1 : 0; g.mirror = 0;
-  return pt2q_launch_gemm(g, st);
+  g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
+  return g;
 }
 
-int trtri_block(const float* U, float* Ui, long ld, int m, int c0, hipStream_t st) {
-  int nb = (m - c0 < NB) ? m - c0 : NB;
-  hipLaunchKernelGGL(trtri_inblock_kernel, dim3(ceil_div((long)(c0 + nb) * LPR, 256)), dim3(256), 0,
-                     st, U, ld, Ui, ld, c0, nb);
-  PT2Q_LAUNCH_CHECK();
-  int rest = m - c0 - nb;
-  if (rest <= 0) return PT2Q_OK;
+// Ui[0 .. c0+nb, c0+nb ..] chains += Ui[:, block J] · U[block J, c0+nb ..] (terms j in J).
+GemmDesc trtri_desc(const float* U, float* Ui, long ld, int c0, int nb, int rest) {
   GemmDesc g{};
   g.M = c0 + nb; g.N = rest; g.K = nb;
   g.A = Ui + c0; g.lda = ld; g.a_layout = LAY_ROWMAJOR;                    // (k, j) = Ui[k][c0+j]
@@ -244,11 +220,15 @@ int trtri_block(const float* U, float* Ui, long ld, int m, int c0, hipStream_t s
   g.in_dtype = PT2Q_F32;
   g.C = Ui + c0 + nb; g.ldc = ld;
   g.mode = GEMM_CHAIN_POS;
-  return pt2q_launch_gemm(g, st);
+  return g;
 }
 
 }  // namespace
 
+// One stream, three launches per 64-wide block J: diagonal factor; panel solve + in-block
+// triangular inverse; trailing update + triangular-inverse update (grouped GEMM).  The inverse
+// Uinv = U^-1 is built right-looking by column blocks as soon as rows of block J are final, so
+// no second stream (and no cross-queue dependency in a captured graph) is needed.
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
                                  float* U, float* Ui, int* info, hipStream_t st) {
   const long ld = m;  // U and Ui are packed m x m
@@ -257,56 +237,21 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
                      U, ld, m);
   PT2Q_LAUNCH_CHECK();
-  // Uinv = U^-1 by column blocks, right-looking: Ui[k][i] holds the running chain of every
-  // not-yet-final column; after block J is final, one CHAIN GEMM extends the chains of all
-  // later columns by the terms j in J (ascending), so each element keeps its canonical order.
-  // Block J runs on the side stream as soon as the factorisation has finished rows of block J.
-  SideStream* ss = side_stream();
-  hipStream_t tst = ss ? ss->s : st, bst = ss ? ss->bulk : st;
   int rc;
   for (int p0 = 0; p0 < m; p0 += NB) {
     const int nb = (m - p0 < NB) ? m - p0 : NB;
     hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
     PT2Q_LAUNCH_CHECK();
     const int rest = m - p0 - nb;
-    if (rest > 0) {
-      hipLaunchKernelGGL(chol_panel_kernel, dim3(ceil_div((long)rest * LPR, 256)), dim3(256), 0, st,
-                         U, ld, p0, nb, m);
-      PT2Q_LAUNCH_CHECK();
-    }
-    // rows [p0, p0+nb) of U are final: hand block J to the inverse and bulk-update streams
-    if (ss) {
-      if (hipEventRecord(ss->fork, st) != hipSuccess) return PT2Q_E_HIP;
-      if (hipStreamWaitEvent(tst, ss->fork, 0) != hipSuccess) return PT2Q_E_HIP;
-    }
-    if ((rc = trtri_block(U, Ui, ld, m, p0, tst)) != PT2Q_OK) return rc;
+    const int npanel = rest > 0 ? (int)ceil_div((long)rest * LPR, 256) : 0;
+    const int ninv = (int)ceil_div((long)(p0 + nb) * LPR, 256);
+    hipLaunchKernelGGL(chol_panel_trtri_kernel, dim3(npanel + ninv), dim3(256), 0, st, U, ld, p0, nb,
+                       m, Ui, npanel);
+    PT2Q_LAUNCH_CHECK();
     if (rest <= 0) break;
-    // critical path: the next block row only (its rows got block J-1's terms from the bulk
-    // update of J-1, so wait for that first); the rest of the trailing triangle goes to the
-    // bulk stream, after the bulk update of J-1 (same stream) and panel J (fork event).
-    // Look-ahead (next block row on the critical path, the rest on the bulk stream) measured
-    // slower at m = 4096 (the bulk update then competes with the chain for CUs); opt-in only.
-    static const char* la_env = std::getenv("PT2Q_CHOL_LOOKAHEAD");
-    if (!(la_env && la_env[0] == '1')) {  // one trailing update on the critical path
-      if ((rc = trailing_update(U, ld, p0, nb, p0 + nb, rest, p0 + nb, rest, true, st)) != PT2Q_OK)
-        return rc;
-      continue;
-    }
-    const int nb2 = (rest < NB) ? rest : NB;
-    if (ss && p0 > 0 && hipStreamWaitEvent(st, ss->bulk_done, 0) != hipSuccess) return PT2Q_E_HIP;
-    if ((rc = trailing_update(U, ld, p0, nb, p0 + nb, nb2, p0 + nb, rest, false, st)) != PT2Q_OK)
+    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p0 + nb, rest, p0 + nb, rest),
+                                trtri_desc(U, Ui, ld, p0, nb, rest), st)) != PT2Q_OK)
       return rc;
-    if (ss && hipStreamWaitEvent(bst, ss->fork, 0) != hipSuccess) return PT2Q_E_HIP;
-    if ((rc = trailing_update(U, ld, p0, nb, p0 + nb + nb2, rest - nb2, p0 + nb + nb2, rest - nb2,
-                              true, bst)) != PT2Q_OK)
-      return rc;
-    if (ss && hipEventRecord(ss->bulk_done, bst) != hipSuccess) return PT2Q_E_HIP;
-  }
-  if (ss) {
-    if (hipEventRecord(ss->join, tst) != hipSuccess) return PT2Q_E_HIP;
-    if (hipStreamWaitEvent(st, ss->join, 0) != hipSuccess) return PT2Q_E_HIP;
-    if (hipEventRecord(ss->bulk_done, bst) != hipSuccess) return PT2Q_E_HIP;
-    if (hipStreamWaitEvent(st, ss->bulk_done, 0) != hipSuccess) return PT2Q_E_HIP;
   }
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
   GemmDesc g{};

@@ -270,24 +270,26 @@ PT2Q_DEV void tile_mma(Frag<BM, BN, SW>& F, const GemmDesc& g, int i0, int j0, i
   __syncthreads();  // LDS is reused by the next tile / epilogue
 }
 
+// One output tile of g: bid-th of nblocks workgroups of this GEMM (grouped launches pass
+// their own offsets).
 template <int BM, int BN, typename TIn, bool VEC>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+PT2Q_DEV void gemm_tile(const GemmDesc& g, int tiles_m, int tiles_n, int bid, int nblocks,
+                        float (*As)[BK][BM + PAD], float (*Bs)[BK][BN + PAD]) {
   int ti, tj;
+  (void)tiles_m;
   if (g.upper && g.kstart_diag == 2) {
     // K starts at the tile's column (lauum): work falls with tj, so dispatch tiles column by
     // column (tj ascending = longest first) for a greedy longest-processing-time balance
-    const int L = blockIdx.x;
+    const int L = bid;
     tj = (int)((sqrtf(8.0f * (float)L + 1.0f) - 1.0f) * 0.5f);
     while ((tj + 1) * (tj + 2) / 2 <= L) ++tj;
     while (tj * (tj + 1) / 2 > L) --tj;
     ti = L - tj * (tj + 1) / 2;
   } else if (g.upper) {
-    upper_tile(xcd_remap(blockIdx.x, gridDim.x), tiles_n, ti, tj);
+    upper_tile(xcd_remap(bid, nblocks), tiles_n, ti, tj);
   } else {
-    ti = blockIdx.x / tiles_n;
-    tj = blockIdx.x % tiles_n;
+    ti = bid / tiles_n;
+    tj = bid % tiles_n;
   }
   const int i0 = ti * BM, j0 = tj * BN;
   Frag<BM, BN, true> F;
@@ -362,6 +364,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
             if (col + e < g.N) g.C[(long)(col + e) * g.ldc + row] = v[e];
         }
       }
+}
+
+template <int BM, int BN, typename TIn, bool VEC>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  gemm_tile<BM, BN, TIn, VEC>(g, tiles_m, tiles_n, blockIdx.x, gridDim.x, As, Bs);
+}
+
+// Two independent GEMMs in one launch (workgroups [0, n0) -> g0, the rest -> g1): saves a
+// kernel boundary on a serial chain (Cholesky trailing update + triangular-inverse update).
+template <int BM, int BN, typename TIn, bool VEC>
+__global__ __launch_bounds__(256) void gemm2_kernel(GemmDesc g0, int tm0, int tn0, int n0, GemmDesc g1,
+                                                    int tm1, int tn1) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  const int b = blockIdx.x;
+  if (b < n0)
+    gemm_tile<BM, BN, TIn, VEC>(g0, tm0, tn0, b, n0, As, Bs);
+  else
+    gemm_tile<BM, BN, TIn, VEC>(g1, tm1, tn1, b - n0, (int)gridDim.x - n0, As, Bs);
 }
 
 // Persistent, balanced ("stream-K with exact chain continuation") symmetric Gram, STORE mode:
@@ -816,7 +839,40 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   return PT2Q_OK;
 }
 
+template <int BM, int BN>
+long tiles_of(const GemmDesc& g, int& tm, int& tn) {
+  tm = ceil_div(g.M, BM);
+  tn = ceil_div(g.N, BN);
+  if (g.M <= 0 || g.N <= 0) return 0;
+  return g.upper ? (long)tm * (tm + 1) / 2 : (long)tm * tn;
+}
+
+template <int BM, int BN>
+int launch2_t(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
+  int tm0, tn0, tm1, tn1;
+  const long n0 = tiles_of<BM, BN>(g0, tm0, tn0), n1 = tiles_of<BM, BN>(g1, tm1, tn1);
+  if ((g0.upper && tm0 != tn0) || (g1.upper && tm1 != tn1)) return PT2Q_E_ARG;
+  if (n0 + n1 <= 0) return PT2Q_OK;
+  const bool vec = (n0 == 0 || vec_ok<BM, BN, float>(g0)) && (n1 == 0 || vec_ok<BM, BN, float>(g1));
+  void (*k)(GemmDesc, int, int, int, GemmDesc, int, int) =
+      vec ? gemm2_kernel<BM, BN, float, true> : gemm2_kernel<BM, BN, float, false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)(n0 + n1)), dim3(256), 0, st, g0, tm0, tn0, (int)n0, g1, tm1, tn1);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
 }  // namespace
+
+int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
+  if (g0.in_dtype != PT2Q_F32 || g1.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
+  int a, b;
+  const long c128 = tiles_of<128, 128>(g0, a, b) + tiles_of<128, 128>(g1, a, b);
+  const long c64 = tiles_of<64, 64>(g0, a, b) + tiles_of<64, 64>(g1, a, b);
+  // the launch_dt balance rule on the combined grid
+  const double t128 = std::ceil(c128 / 256.0) * 4.0, t64 = std::ceil(c64 / 256.0) * 1.15;
+  if (c128 >= 64 && t128 <= t64) return launch2_t<128, 128>(g0, g1, st);
+  return launch2_t<64, 64>(g0, g1, st);
+}
 
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PT2Q_OK;

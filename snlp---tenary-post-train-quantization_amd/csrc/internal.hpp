@@ -45,6 +45,8 @@ struct GemmDesc {
   int kstart_diag;  // skip K below min(tile row start): exact for triangular operands (zeros)
 };
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
+// two independent f32 GEMMs in one launch (either may be empty)
+int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st);
 size_t pt2q_gram_flags_ints(int m);
