@@ -326,6 +326,23 @@ PT2Q_DEV void gemm_tile(const GemmDesc& g, int tiles_m, int tiles_n, int bid, in
   if (g.kstart_diag == 1) kbeg = i0 - (i0 % BK);
   if (g.kstart_diag == 2) kbeg = j0 - (j0 % BK);
   tile_mma<BM, BN, TIn, VEC, true>(F, g, i0, j0, kbeg, g.K, As, Bs);
+  // ADD / SUB read the old C: all of its loads are issued together before the first store,
+  // instead of one dependent load per 16-byte group between stores that may alias them
+  const bool pre_c = cvec && (g.mode == GEMM_ADD || g.mode == GEMM_SUB);
+  f32x4 cold[RM][RN][4];
+  if (pre_c) {
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = F.row_of(i0, rm, 4 * q), col = F.col_of(j0, rn, 4 * q);
+          const bool in = row < g.M && col + 3 < g.N;
+          const long crow = in ? (g.crow ? g.crow[row] : row) : 0;
+          cold[rm][rn][q] = *(const f32x4*)(g.C + crow * g.ldc + (in ? col : 0));
+        }
+  }
   const bool mirror = g.upper && g.mirror && (ti != tj);
 #pragma unroll
   for (int rm = 0; rm < RM; ++rm)
@@ -341,8 +358,8 @@ PT2Q_DEV void gemm_tile(const GemmDesc& g, int tiles_m, int tiles_n, int bid, in
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = F.acc[rm][rn][4 * q + e];
         if (cvec && col + 3 < g.N) {
-          if (g.mode == GEMM_ADD || g.mode == GEMM_SUB) {
-            const f32x4 c = *(const f32x4*)p;
+          if (pre_c) {
+            const f32x4 c = cold[rm][rn][q];
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = (g.mode == GEMM_ADD) ? c[e] + v[e] : c[e] - v[e];
           }
@@ -839,6 +856,121 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   return PT2Q_OK;
 }
 
+// ---------------------------------------------------------------- rank-<=64 chain updates
+// C[i][j] = chain continued over k < K <= 64 of sgn * A(i,k) * B(k,j), k ascending (the
+// Cholesky trailing update, GEMM_CHAIN_NEG, and the triangular-inverse update, GEMM_CHAIN_POS).
+// Such a GEMM is a pass over C: one 64 x 64 tile per workgroup with every load in flight at once
+// -- both K x 64 operand panels straight into LDS and the C tile into registers -- then K/2
+// f32 MFMAs per wave and one store.  Bit-identical to the generic kernel (same chain order).
+constexpr int RU_T = 64, RU_K = 64;
+
+// Operand panel (64 columns d, K rows k) into lds[k][d] (zero outside the matrix / past K).
+PT2Q_DEV void ru_panel(const float* base, long ld, int layout, int d0, int DMAX, int K,
+                       float (*lds)[RU_T + 4]) {
+  const int tid = threadIdx.x;
+  float4 v[4];
+  bool ok[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int q = tid + 256 * e;  // 1024 float4 = 64 x 64
+    int d, k;
+    if (layout == LAY_KMAJOR) {
+      k = q >> 4;
+      d = (q & 15) * 4;
+    } else {
+      d = q >> 4;
+      k = (q & 15) * 4;
+    }
+    const long off = layout == LAY_KMAJOR ? (long)k * ld + d0 + d : (long)(d0 + d) * ld + k;
+    // vectors are whole inside or outside (checked at launch: DMAX % 4 == 0 / K % 4 == 0)
+    ok[e] = layout == LAY_KMAJOR ? (k < K && d0 + d < DMAX) : (d0 + d < DMAX && k < K);
+    v[e] = *(const float4*)(base + (ok[e] ? off : 0));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int q = tid + 256 * e;
+    const float4 x = ok[e] ? v[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (layout == LAY_KMAJOR) {
+      *(float4*)&lds[q >> 4][(q & 15) * 4] = x;
+    } else {
+      const int d = q >> 4, k = (q & 15) * 4;
+      lds[k][d] = x.x;
+      lds[k + 1][d] = x.y;
+      lds[k + 2][d] = x.z;
+      lds[k + 3][d] = x.w;
+    }
+  }
+}
+
+PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4], float (*Bs)[RU_T + 4]) {
+  int ti, tj;
+  if (g.upper) {
+    upper_tile(bid, tn, ti, tj);
+  } else {
+    ti = bid / tn;
+    tj = bid % tn;
+  }
+  const int i0 = ti * RU_T, j0 = tj * RU_T;
+  Frag<RU_T, RU_T, true> F;
+  // C tile (16-byte groups of 4 columns: launch checks ldc % 4 == 0, N % 4 == 0, alignment)
+  const float* Cr = g.C;
+  {
+    const int row = F.row_of(i0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = F.col_of(j0, 0, 4 * q);
+      const bool in = row < g.M && col < g.N;
+      const f32x4 v = *(const f32x4*)(Cr + (in ? (long)row * g.ldc + col : 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) F.acc[0][0][4 * q + e] = in ? v[e] : 0.0f;
+    }
+  }
+  ru_panel((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As);
+  ru_panel((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
+  const float sgn = (g.mode == GEMM_CHAIN_NEG) ? -1.0f : 1.0f;
+  // all 32 k-pairs: the panels are zero past K, and a zero term is an exact no-op on a chain
+#pragma unroll
+  for (int s = 0; s < RU_K / 2; ++s) {
+    const float a = As[2 * s + lk][wr * 32 + li], b = Bs[2 * s + lk][wc * 32 + li];
+    F.acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b, sgn * a, F.acc[0][0], 0, 0, 0);
+  }
+  const int row = F.row_of(i0, 0, 0);
+  if (row < g.M) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = F.col_of(j0, 0, 4 * q);
+      if (col >= g.N) continue;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = F.acc[0][0][4 * q + e];
+      *(f32x4*)(g.C + (long)row * g.ldc + col) = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void rank_update2_kernel(GemmDesc g0, int tn0, int n0, GemmDesc g1, int tn1) {
+  __shared__ __attribute__((aligned(16))) float As[RU_K][RU_T + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[RU_K][RU_T + 4];
+  const int b = blockIdx.x;
+  if (b < n0)
+    ru_tile(g0, tn0, b, As, Bs);
+  else
+    ru_tile(g1, tn1, b - n0, As, Bs);
+}
+
+bool ru_ok(const GemmDesc& g) {
+  if (g.M <= 0 || g.N <= 0) return true;
+  auto al = [](const void* p) { return (uintptr_t)p % 16 == 0; };
+  auto vdim = [&](int layout, int dim) { return layout == LAY_KMAJOR ? dim : g.K; };
+  return g.in_dtype == PT2Q_F32 && g.K <= RU_K && !g.crow && !g.mirror &&
+         (g.mode == GEMM_CHAIN_NEG || g.mode == GEMM_CHAIN_POS) && al(g.A) && al(g.B) && al(g.C) &&
+         g.lda % 4 == 0 && g.ldb % 4 == 0 && g.ldc % 4 == 0 && g.N % 4 == 0 &&
+         vdim(g.a_layout, g.M) % 4 == 0 && vdim(g.b_layout, g.N) % 4 == 0;
+}
+
 template <int BM, int BN>
 long tiles_of(const GemmDesc& g, int& tm, int& tn) {
   tm = ceil_div(g.M, BM);
@@ -865,6 +997,16 @@ int launch2_t(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
 
 int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
   if (g0.in_dtype != PT2Q_F32 || g1.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
+  static const char* ru_env = std::getenv("PT2Q_RANK_UPDATE");  // 0: generic grouped GEMM
+  if (ru_ok(g0) && ru_ok(g1) && !(ru_env && ru_env[0] == '0')) {
+    int tm0, tn0, tm1, tn1;
+    const long n0 = tiles_of<RU_T, RU_T>(g0, tm0, tn0), n1 = tiles_of<RU_T, RU_T>(g1, tm1, tn1);
+    if (n0 + n1 <= 0) return PT2Q_OK;
+    hipLaunchKernelGGL(rank_update2_kernel, dim3((unsigned)(n0 + n1)), dim3(256), 0, st, g0, tn0,
+                       (int)n0, g1, tn1);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   int a, b;
   const long c128 = tiles_of<128, 128>(g0, a, b) + tiles_of<128, 128>(g1, a, b);
   const long c64 = tiles_of<64, 64>(g0, a, b) + tiles_of<64, 64>(g1, a, b);

@@ -47,6 +47,37 @@ __global__ __launch_bounds__(256) void ssr_wbar_sum_kernel(const float* part, in
   wbar[i] = t / (float)r;
 }
 
+// wbar[i] = (chunk partials summed in chunk order) / r, then nw = clamp(sqrt(SUMN fma wbar^2))
+// and wn = wbar / nw -- one workgroup, n <= SUMN_LDS_MAX (ssr_wbar_sum + ssr_wbar_final fused)
+__global__ __launch_bounds__(1024) void ssr_wbar_sumfinal_kernel(const float* part, int nchunks,
+                                                                 int n, int r, float* wn) {
+  __shared__ float nws, tot;
+  __shared__ float stage[SUMN_LDS_MAX];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    float t = 0.0f;
+    int c = 0;
+    for (; c + 8 <= nchunks; c += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(c + u) * n + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t = t + v[u];
+    }
+    for (; c < nchunks; ++c) t = t + part[(long)c * n + i];
+    stage[i] = t / (float)r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float p = sumn_lane<true>(stage, n, 1, threadIdx.x);
+    p = bfly64(p);
+    if (threadIdx.x == 0) nws = clampmin(sqrtf(p));
+  }
+  __syncthreads();
+  const float nw = nws;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = stage[i] / nw;
+  (void)tot;
+}
+
 // nw = clamp(sqrt(SUMN fma wbar^2)) ; wn = wbar / nw   (in place)
 __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) {
   __shared__ float nws, tot;
@@ -73,9 +104,39 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
   if (e >= r) return;
   const float* x = Wt + (long)rem[e] * ldw;
   float p = 0.0f;
-  if ((n & 3) == 0 && (ldw & 3) == 0) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  if ((n & 3) == 0 && (ldw & 3) == 0 && n <= 4096) {
+    // one pass over the column: its 16 float4 per lane stay in registers for both chains
+    f4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long base = 4 * t + 256 * u;
+      if (base < n) v[u] = *(const f4*)(x + base);
+    }
+    float ss = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (4 * t + 256 * u < n) {
+        ss = fmaf(v[u][0], v[u][0], ss);
+        ss = fmaf(v[u][1], v[u][1], ss);
+        ss = fmaf(v[u][2], v[u][2], ss);
+        ss = fmaf(v[u][3], v[u][3], ss);
+      }
+    }
+    const float nj = clampmin(sqrtf(bfly64(ss)));
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long base = 4 * t + 256 * u;
+      if (base < n) {
+        const f4 w = *(const f4*)(wn + base);
+        p = fmaf(v[u][0] / nj, w[0], p);
+        p = fmaf(v[u][1] / nj, w[1], p);
+        p = fmaf(v[u][2] / nj, w[2], p);
+        p = fmaf(v[u][3] / nj, w[3], p);
+      }
+    }
+  } else if ((n & 3) == 0 && (ldw & 3) == 0) {
     // float4 path (same per-lane element order {256u + 4t + q})
-    typedef float f4 __attribute__((ext_vector_type(4)));
     float ss = 0.0f;
     for (long base = 4 * t; base < n; base += 256) {
       f4 v = *(const f4*)(x + base);
@@ -569,11 +630,16 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
                      Wt, ldw, n, rem, r, part);
   PT2Q_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ssr_wbar_sum_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, nchunks,
-                     n, r, wn);
-  PT2Q_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), 0, st, wn, n);
-  PT2Q_LAUNCH_CHECK();
+  if (n <= SUMN_LDS_MAX) {
+    hipLaunchKernelGGL(ssr_wbar_sumfinal_kernel, dim3(1), dim3(1024), 0, st, part, nchunks, n, r, wn);
+    PT2Q_LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(ssr_wbar_sum_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, nchunks,
+                       n, r, wn);
+    PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), 0, st, wn, n);
+    PT2Q_LAUNCH_CHECK();
+  }
   hipLaunchKernelGGL(ssr_sim_kernel, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r,
                      wn, sim);
   PT2Q_LAUNCH_CHECK();
