@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="launch eagerly instead of hipGraph replay")
     p.add_argument("--cpu-sample-rows", type=int, default=4096)
+    p.add_argument("--no-n2048", action="store_true",
+                   help="skip the secondary N=2048 timing (profiling: keeps only headline launches)")
     return p.parse_args()
 
 
@@ -159,17 +161,19 @@ def main():
     achieved = gram_flops / (gram_ms * 1e-3) / 1e12
 
     # secondary: s/layer at N=2048 (the survey's other d=4096 CPU reference point)
-    X2 = X[:2048].contiguous()
-    g2 = pt2q.LayerGraph(W, X2, bs, use_ssr) if not a.eager else None
-    run2 = g2.replay if g2 is not None else (
-        lambda: pt2q.quantize_layer(W, X2, bs, use_ssr, workspace=ws, check_spd=False, outputs=outs))
-    run2()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    for _ in range(5):
+    s_layer_2048 = float("nan")
+    X2 = X[:2048].contiguous() if not a.no_n2048 else None
+    if X2 is not None:
+        g2 = pt2q.LayerGraph(W, X2, bs, use_ssr) if not a.eager else None
+        run2 = g2.replay if g2 is not None else (
+            lambda: pt2q.quantize_layer(W, X2, bs, use_ssr, workspace=ws, check_spd=False, outputs=outs))
         run2()
-    torch.cuda.synchronize()
-    s_layer_2048 = (time.perf_counter() - t2) / 5
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for _ in range(5):
+            run2()
+        torch.cuda.synchronize()
+        s_layer_2048 = (time.perf_counter() - t2) / 5
 
     if a.io_dtype == "fp32":
         kname = "gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)"
@@ -201,8 +205,8 @@ def main():
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": None,
                          "avg_launch_ms": gram_ms, "flops_per_launch": gram_flops},
-            "extra": {"s_per_layer_n2048": s_layer_2048,
-                      "cols_per_s_n2048": m / s_layer_2048,
+            "extra": {"s_per_layer_n2048": None if a.no_n2048 else s_layer_2048,
+                      "cols_per_s_n2048": None if a.no_n2048 else m / s_layer_2048,
                       "gram_share_of_step": gram_ms / ms_per_step},
         }
         tr = load_traffic()

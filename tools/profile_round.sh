@@ -13,7 +13,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_under_trace.json 2> $OUT/trace.err || exit 1
+  python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-n2048 > $OUT/bench_under_trace.json 2> $OUT/trace.err || exit 1
 for ctr in FETCH_SIZE WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS; do
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/pmc_$ctr -o run --output-format csv -- \
     python3 $R/tools/bench_gram.py 262144 4096 fp16 > $OUT/pmc_$ctr.log 2>&1 || exit 1

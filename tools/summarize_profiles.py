@@ -103,7 +103,7 @@ def main():
     rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
     lines = [f"# Profile {tag}", "",
              "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 3 --warmup 1 "
-             "--no-cpu-baseline` (tools/profile_round.sh); full table in "
+             "--no-cpu-baseline --no-n2048` (tools/profile_round.sh); full table in "
              f"`{tag}_kernel_stats.csv`.", "",
              "| kernel | calls | avg µs | total ms | % |", "|---|---|---|---|---|"]
     for r in rows[:15]:
