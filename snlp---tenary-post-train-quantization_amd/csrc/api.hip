@@ -159,7 +159,12 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
                                     nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
                                     st, Hinv, ldhi, nrem, nr, w.Ck, m)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
-    if (nr > 0) {
+    static const char* ef_env = std::getenv("PT2Q_EF_GEMM");  // 0: the generic GEMM
+    rc = (nr > 0 && !(ef_env && ef_env[0] == '0'))
+             ? pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st)
+             : PT2Q_E_UNSUPPORTED;
+    if (rc != PT2Q_OK && rc != PT2Q_E_UNSUPPORTED) return rc;
+    if (nr > 0 && rc == PT2Q_E_UNSUPPORTED) {
       GemmDesc g{};
       g.M = nr; g.N = n; g.K = bs;
       g.A = w.Ck; g.lda = m; g.a_layout = LAY_KMAJOR;     // (e, k) = C[k][e]

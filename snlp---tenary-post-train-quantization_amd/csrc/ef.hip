@@ -1,0 +1,266 @@
+// GPTQ error feedback of one block (main.py:214, gptq.py:181-186):
+//   W[:, rem] -= E · C,   E = W_b − (α T + μ) (n × bs),  C = Hinv[blk][:, rem] / diag (bs × nr)
+// in the feature-major layout: Wt[rem_e][i] -= Σ_k C[k][e] · E[k][i], the product a k-ascending
+// f32 chain (v_mfma_f32_32x32x2_f32 issues k in ascending pairs: D = fma(a1,b1, fma(a0,b0, C)),
+// the oracle's order), rounded once, then one subtraction -- the contract of DESIGN.md §3.
+//
+// A K <= 128 GEMM is too short for the generic tile loop (load, sync, compute, reload C): here a
+// persistent workgroup walks 128 × 128 output tiles and keeps the operand stream running across
+// them.  The two 64-deep K halves of a tile live in two LDS stages (A: C[k][e0..], B: E[k][i0..],
+// 64 KiB per stage) filled by LDS-DMA; while one half is multiplied the other half of the next
+// tile is fetched, and the old Wt rows of a tile are loaded into registers while its MFMAs run.
+// Every wave issues the same number of memory instructions per tile (out-of-range rows and
+// columns go through buffer ops with offsets past the end, which the hardware drops), so the
+// hand-counted s_waitcnt vmcnt values below are exact.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int EF_T = 128;                    // output tile (e and i)
+constexpr int EF_KH = 64;                    // k rows per LDS stage
+constexpr int EF_ROWB = EF_T * 4;            // 512 B per k row of a panel
+constexpr int EF_PANEL = EF_KH * EF_ROWB;    // 32 KiB
+constexpr int EF_STAGE = 2 * EF_PANEL;       // A + B
+constexpr int EF_DMA = 16;                   // DMA instructions per wave per stage
+constexpr int EF_CV = 16;                    // C float4 loads (= stores) per lane per tile
+constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropped access)
+
+struct EfArgs {
+  const float* Ck;  // C[k][e], ld m
+  long ldk;
+  const float* Et;  // E[k][i], ld ldw
+  float* Wt;        // Wt[j][i], ld ldw
+  long ldw;
+  const int* crow;  // rem (nr entries)
+  int nr, bs, te, ti, ntile, nh;
+};
+
+// One stage (K half h) of tile (e0, i0) into LDS: 8 DMA of A (2 k-rows of 512 B each), 8 of B.
+// Rows past the data are fetched from row 0 (garbage, zeroed at the MFMA operand or dropped
+// at the store), so every wave issues exactly EF_DMA instructions.
+PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  typedef __attribute__((address_space(3))) void* lptr;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int kr = (wave * 8 + q) * 2 + (lane >> 5);  // k row inside the stage
+    const int k = h * EF_KH + kr;
+    const int d = 4 * (lane & 31);
+    const bool kin = k < a.bs;
+    const int e = e0 + d, i = i0 + d;
+    const float* sa = a.Ck + (kin && e < a.nr ? (long)k * a.ldk + e : 0);
+    const float* sb = a.Et + (kin && i < a.ldw ? (long)k * a.ldw + i : 0);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    __builtin_amdgcn_global_load_lds((const void*)sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
+  }
+}
+
+template <int OFF>
+PT2Q_DEV float ef_ld(uint32_t addr) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+PT2Q_DEV void ef_wait(float (&a)[2], float (&b)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+}
+
+// k-pair S of a stage: lane reads A rows e (2 MFMA row blocks) and B columns i (2 blocks).
+template <int S>
+PT2Q_DEV void ef_read(uint32_t baseA, uint32_t baseB, float (&a)[2], float (&b)[2]) {
+  a[0] = ef_ld<S * 2 * EF_ROWB>(baseA);
+  a[1] = ef_ld<S * 2 * EF_ROWB + 128>(baseA);
+  b[0] = ef_ld<S * 2 * EF_ROWB>(baseB);
+  b[1] = ef_ld<S * 2 * EF_ROWB + 128>(baseB);
+}
+
+struct EfAcc {
+  f32x16 acc[2][2];  // [rm][rn], transposed MFMA: lane <-> e row, registers <-> i columns
+
+  template <int S>
+  PT2Q_DEV void step(uint32_t bA, uint32_t bB, float (&a)[2], float (&b)[2], float (&na)[2],
+                     float (&nb)[2], int kleft) {
+    // k rows past bs are garbage in LDS: zero operands make those steps exact no-ops
+    const bool kin = 2 * S + ((threadIdx.x & 63) >> 5) < kleft;
+    float x[2], y[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      x[u] = kin ? a[u] : 0.0f;
+      y[u] = kin ? b[u] : 0.0f;
+    }
+    // the next pair's reads go out before this pair's MFMAs (pinned: the scheduler would
+    // otherwise sink them below the MFMAs and expose the LDS latency every step)
+    if constexpr (S + 1 < EF_KH / 2) ef_read<S + 1>(bA, bB, na, nb);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn)
+        acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(y[rn], x[rm], acc[rm][rn], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (S + 1 < EF_KH / 2) ef_wait(na, nb);
+  }
+
+  template <int S>
+  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[2], float (&b)[2], float (&na)[2],
+                    float (&nb)[2], int kleft) {
+    if constexpr (S < EF_KH / 2) {
+      step<S>(bA, bB, a, b, na, nb, kleft);
+      run<S + 1>(bA, bB, na, nb, a, b, kleft);
+    }
+  }
+
+  // the 32 k-pairs of one stage
+  PT2Q_DEV void half(uint32_t stg, int kleft) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
+    const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
+    const uint32_t bB = stg + EF_PANEL + lk * EF_ROWB + (wc * 64 + li) * 4;
+    float a[2], b[2], na[2], nb[2];
+    ef_read<0>(bA, bB, a, b);
+    ef_wait(a, b);
+    run<0>(bA, bB, a, b, na, nb, kleft);
+  }
+};
+
+PT2Q_DEV int ef_row(int e0, int rm) {
+  const int lane = threadIdx.x & 63, wr = (threadIdx.x >> 6) >> 1;
+  return e0 + wr * 64 + rm * 32 + (lane & 31);
+}
+PT2Q_DEV int ef_col(int i0, int rn, int q) {
+  const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
+  return i0 + wc * 64 + rn * 32 + 8 * q + 4 * (lane >> 5);
+}
+
+// byte offset of the old/new Wt values of group (rm, rn, q), or EF_DROP; wrow[rm] = the Wt row
+// of this lane's output row in row block rm (-1 past nr)
+PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm, int rn, int q) {
+  const int i = ef_col(i0, rn, q);
+  if (wrow[rm] < 0 || i >= a.ldw) return EF_DROP;
+  return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
+}
+
+PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm) {
+    const int e = ef_row(e0, rm);
+    wrow[rm] = e < a.nr ? a.crow[e] : -1;
+  }
+}
+
+PT2Q_DEV void ef_cload(const EfArgs& a, __amdgpu_buffer_rsrc_t rc, const int (&wrow)[2], int i0,
+                       u32x4 (&c)[EF_CV]) {
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        c[(rm * 2 + rn) * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+}
+
+// s_waitcnt vmcnt(N) for the small set of counts the schedule needs (immediate operand)
+PT2Q_DEV void ef_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+  }
+}
+
+__global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  int t = blockIdx.x;
+  if (t >= a.ntile) return;
+  auto corner = [&](int t, int& e0, int& i0) {
+    e0 = (t / a.ti) * EF_T;
+    i0 = (t % a.ti) * EF_T;
+  };
+  int e0, i0, wrow[2];
+  corner(t, e0, i0);
+  ef_rows(a, e0, wrow);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // prologue: this tile's stages, then its old C
+  ef_stage(a, e0, i0, 0, smem);
+  if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
+  u32x4 c[EF_CV];
+  ef_cload(a, rc, wrow, i0, c);
+  const int S1 = a.nh == 2 ? EF_DMA : 0;
+  // issue order per tile: [stage0] [stage1] [stores of the previous tile] [old C] ...
+  for (bool first = true;; first = false) {
+    const int tn = t + (int)gridDim.x;
+    const bool more = tn < a.ntile;
+    int en = 0, in = 0, nrow[2] = {-1, -1};
+    if (more) corner(tn, en, in);
+    EfAcc F;
+#pragma unroll
+    for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
+    ef_vmcnt(S1 + (first ? 0 : EF_CV) + EF_CV);  // stage 0 landed
+    asm volatile("s_barrier" ::: "memory");
+    if (more) ef_rows(a, en, nrow);  // the next tile's Wt rows (2 loads, long before their use)
+    F.half(lds0, a.bs);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
+    if (more) ef_stage(a, en, in, 0, smem);
+    if (a.nh == 2) {
+      ef_vmcnt((first ? 0 : EF_CV) + EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
+      asm volatile("s_barrier" ::: "memory");
+      F.half(lds0 + EF_STAGE, a.bs - EF_KH);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (more) ef_stage(a, en, in, 1, smem + EF_STAGE);
+    }
+    ef_vmcnt(more ? EF_DMA + S1 : 0);  // the old C landed (younger: the next tile's stages)
+#pragma unroll
+    for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4 o = c[(rm * 2 + rn) * 4 + q];
+          u32x4 w;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            w[u] = __float_as_uint(__uint_as_float(o[u]) - F.acc[rm][rn][4 * q + u]);
+          __builtin_amdgcn_raw_buffer_store_b128(w, rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+        }
+    if (!more) break;
+    t = tn;
+    e0 = en;
+    i0 = in;
+    wrow[0] = nrow[0];
+    wrow[1] = nrow[1];
+    ef_cload(a, rc, wrow, i0, c);
+  }
+}
+
+}  // namespace
+
+// Wt[crow[e]][i] -= sum_k Ck[k][e] * Et[k][i] for e < nr, i < ldw (the padding columns of Wt
+// beyond n are scratch), k < bs <= 128.  Wt has wt_rows rows of ldw floats.
+int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
+                   const int* crow, int nr, int bs, hipStream_t st) {
+  if (nr <= 0) return PT2Q_OK;
+  const long wt_bytes = wt_rows * ldw * 4;
+  if (bs <= 0 || bs > 2 * EF_KH || ldw % 4 || ldk % 4 || (uintptr_t)Ck % 16 || (uintptr_t)Et % 16 ||
+      (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP)
+    return PT2Q_E_UNSUPPORTED;
+  EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1};
+  a.ntile = a.te * a.ti;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = std::min(a.ntile, cus);
+  hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}

@@ -45,6 +45,9 @@ struct GemmDesc {
   int kstart_diag;  // skip K below min(tile row start): exact for triangular operands (zeros)
 };
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
+// block error feedback Wt[crow[e]][i] -= sum_k Ck[k][e] Et[k][i] (ef.hip); E_UNSUPPORTED if bs > 128
+int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
+                   const int* crow, int nr, int bs, hipStream_t st);
 // two independent f32 GEMMs in one launch (either may be empty)
 int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
