@@ -30,6 +30,8 @@ constexpr int EF_DMA = 16;                   // DMA instructions per wave per st
 constexpr int EF_CV = 16;                    // C float4 loads (= stores) per lane per tile
 constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropped access)
 
+__device__ uint4 ef_zero16;  // DMA source of the k rows past bs (zero-initialised)
+
 struct EfArgs {
   const float* Ck;  // C[k][e], ld m
   long ldk;
@@ -41,8 +43,9 @@ struct EfArgs {
 };
 
 // One stage (K half h) of tile (e0, i0) into LDS: 8 DMA of A (2 k-rows of 512 B each), 8 of B.
-// Rows past the data are fetched from row 0 (garbage, zeroed at the MFMA operand or dropped
-// at the store), so every wave issues exactly EF_DMA instructions.
+// k rows past bs come from a zero chunk (their MFMA steps are then exact no-ops); columns past
+// the data come from row 0 (garbage in rows / columns whose results are dropped), so every wave
+// issues exactly EF_DMA instructions.
 PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   typedef __attribute__((address_space(3))) void* lptr;
@@ -53,11 +56,11 @@ PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
     const int d = 4 * (lane & 31);
     const bool kin = k < a.bs;
     const int e = e0 + d, i = i0 + d;
-    const float* sa = a.Ck + (kin && e < a.nr ? (long)k * a.ldk + e : 0);
-    const float* sb = a.Et + (kin && i < a.ldw ? (long)k * a.ldw + i : 0);
+    const void* sa = kin ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
+    const void* sb = kin ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
     const int wv = __builtin_amdgcn_readfirstlane(wave);
-    __builtin_amdgcn_global_load_lds((const void*)sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
   }
 }
 
@@ -84,49 +87,40 @@ PT2Q_DEV void ef_read(uint32_t baseA, uint32_t baseB, float (&a)[2], float (&b)[
 struct EfAcc {
   f32x16 acc[2][2];  // [rm][rn], transposed MFMA: lane <-> e row, registers <-> i columns
 
+  // k-pair S: its operands are in set S % 3; the reads of pair S+1 go to set (S+1) % 3, whose
+  // registers the MFMAs of pair S-2 read long ago (no overwrite of an operand in flight).  The
+  // order reads -> MFMAs -> wait is pinned (the scheduler would sink the reads below the MFMAs).
   template <int S>
-  PT2Q_DEV void step(uint32_t bA, uint32_t bB, float (&a)[2], float (&b)[2], float (&na)[2],
-                     float (&nb)[2], int kleft) {
-    // k rows past bs are garbage in LDS: zero operands make those steps exact no-ops
-    const bool kin = 2 * S + ((threadIdx.x & 63) >> 5) < kleft;
-    float x[2], y[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      x[u] = kin ? a[u] : 0.0f;
-      y[u] = kin ? b[u] : 0.0f;
-    }
-    // the next pair's reads go out before this pair's MFMAs (pinned: the scheduler would
-    // otherwise sink them below the MFMAs and expose the LDS latency every step)
-    if constexpr (S + 1 < EF_KH / 2) ef_read<S + 1>(bA, bB, na, nb);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < 2; ++rn)
-        acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(y[rn], x[rm], acc[rm][rn], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (S + 1 < EF_KH / 2) ef_wait(na, nb);
-  }
-
-  template <int S>
-  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[2], float (&b)[2], float (&na)[2],
-                    float (&nb)[2], int kleft) {
+  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[3][2], float (&b)[3][2]) {
     if constexpr (S < EF_KH / 2) {
-      step<S>(bA, bB, a, b, na, nb, kleft);
-      run<S + 1>(bA, bB, na, nb, a, b, kleft);
+      constexpr int c = S % 3, n = (S + 1) % 3;
+      if constexpr (S + 1 < EF_KH / 2) ef_read<S + 1>(bA, bB, a[n], b[n]);
+      if constexpr (S > 0) {  // pair S-1's operands stay allocated until these reads are out
+        constexpr int p = (S + 2) % 3;
+        asm volatile("" ::"v"(a[p][0]), "v"(a[p][1]), "v"(b[p][0]), "v"(b[p][1]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+        for (int rn = 0; rn < 2; ++rn)
+          acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][rn], a[c][rm], acc[rm][rn], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (S + 1 < EF_KH / 2) ef_wait(a[n], b[n]);
+      run<S + 1>(bA, bB, a, b);
     }
   }
 
-  // the 32 k-pairs of one stage
-  PT2Q_DEV void half(uint32_t stg, int kleft) {
+  // the 32 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
+  PT2Q_DEV void half(uint32_t stg) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
     const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
     const uint32_t bB = stg + EF_PANEL + lk * EF_ROWB + (wc * 64 + li) * 4;
-    float a[2], b[2], na[2], nb[2];
-    ef_read<0>(bA, bB, a, b);
-    ef_wait(a, b);
-    run<0>(bA, bB, a, b, na, nb, kleft);
+    float a[3][2], b[3][2];
+    ef_read<0>(bA, bB, a[0], b[0]);
+    ef_wait(a[0], b[0]);
+    run<0>(bA, bB, a, b);
   }
 };
 
@@ -210,13 +204,13 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
     ef_vmcnt(S1 + (first ? 0 : EF_CV) + EF_CV);  // stage 0 landed
     asm volatile("s_barrier" ::: "memory");
     if (more) ef_rows(a, en, nrow);  // the next tile's Wt rows (2 loads, long before their use)
-    F.half(lds0, a.bs);
+    F.half(lds0);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
     if (more) ef_stage(a, en, in, 0, smem);
     if (a.nh == 2) {
       ef_vmcnt((first ? 0 : EF_CV) + EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
       asm volatile("s_barrier" ::: "memory");
-      F.half(lds0 + EF_STAGE, a.bs - EF_KH);
+      F.half(lds0 + EF_STAGE);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (more) ef_stage(a, en, in, 1, smem + EF_STAGE);
     }
