@@ -198,16 +198,18 @@ __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, 
 
 namespace {
 
-// U[r0.., c0..] (rows x cols) -= U[p0 + k][r0 + i] * U[p0 + k][c0 + j] over the nb rows of
-// block J (chains continue from U, k ascending).
-GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols) {
+// U[r0.., c0..] (rows x cols) -= U[p0 + k][r0 + i] * U[p0 + k][c0 + j] over the nb rows from p0
+// (one or two blocks; chains continue from U, k ascending).  upper: the square trailing
+// triangle; otherwise the full rectangle (the strictly-lower part of U is scratch).
+GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols,
+                       bool upper = true) {
   GemmDesc g{};
   g.M = rows; g.N = cols; g.K = nb;
   g.A = U + (long)p0 * ld + r0; g.lda = ld; g.a_layout = LAY_KMAJOR;
   g.B = U + (long)p0 * ld + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;
   g.in_dtype = PT2Q_F32;
   g.C = U + (long)r0 * ld + c0; g.ldc = ld;
-  g.mode = GEMM_CHAIN_NEG; g.upper = 1; g.mirror = 0;
+  g.mode = GEMM_CHAIN_NEG; g.upper = upper ? 1 : 0; g.mirror = 0;
   return g;
 }
 
@@ -238,8 +240,8 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
                      U, ld, m);
   PT2Q_LAUNCH_CHECK();
   int rc;
-  for (int p0 = 0; p0 < m; p0 += NB) {
-    const int nb = (m - p0 < NB) ? m - p0 : NB;
+  // diagonal factor + panel solve + in-block inverse of the block at p0
+  auto factor = [&](int p0, int nb) -> int {
     hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
     PT2Q_LAUNCH_CHECK();
     const int rest = m - p0 - nb;
@@ -248,10 +250,35 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     hipLaunchKernelGGL(chol_panel_trtri_kernel, dim3(npanel + ninv), dim3(256), 0, st, U, ld, p0, nb,
                        m, Ui, npanel);
     PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  };
+  // Blocks go in pairs (J, J+1): after J only block row J+1 gets J's terms (it is all the next
+  // factor needs); after J+1 the rest of the trailing triangle gets the terms of both blocks in
+  // one rank-128 pass (k ascending, so every chain is the one-block-at-a-time chain), which
+  // halves the passes over the trailing matrix.
+  for (int p0 = 0; p0 < m;) {
+    const int nb = (m - p0 < NB) ? m - p0 : NB;
+    if ((rc = factor(p0, nb)) != PT2Q_OK) return rc;
+    const int rest = m - p0 - nb;
     if (rest <= 0) break;
-    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p0 + nb, rest, p0 + nb, rest),
+    const int p1 = p0 + nb, nb1 = (rest < NB) ? rest : NB, rest1 = rest - nb1;
+    static const char* pair_env = std::getenv("PT2Q_CHOL_PAIR");  // 0: one update per block (A/B)
+    if (rest1 <= 0 || (pair_env && pair_env[0] == '0')) {  // one plain update
+      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, rest, p1, rest),
+                                  trtri_desc(U, Ui, ld, p0, nb, rest), st)) != PT2Q_OK)
+        return rc;
+      p0 = p1;
+      continue;
+    }
+    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, nb1, p1, rest, false),
                                 trtri_desc(U, Ui, ld, p0, nb, rest), st)) != PT2Q_OK)
       return rc;
+    if ((rc = factor(p1, nb1)) != PT2Q_OK) return rc;
+    const int p2 = p1 + nb1;
+    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb + nb1, p2, rest1, p2, rest1),
+                                trtri_desc(U, Ui, ld, p1, nb1, rest1), st)) != PT2Q_OK)
+      return rc;
+    p0 = p2;
   }
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
   GemmDesc g{};

@@ -862,43 +862,92 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
 // Such a GEMM is a pass over C: one 64 x 64 tile per workgroup with every load in flight at once
 // -- both K x 64 operand panels straight into LDS and the C tile into registers -- then K/2
 // f32 MFMAs per wave and one store.  Bit-identical to the generic kernel (same chain order).
-constexpr int RU_T = 64, RU_K = 64;
+constexpr int RU_T = 64, RU_K = 128;
 
-// Operand panel (64 columns d, K rows k) into lds[k][d] (zero outside the matrix / past K).
+// Operand panel (64 columns d, the first KQ >= K rows k) into lds[k][d] (zero outside the matrix
+// / past K); KQ = 64 or 128.
+template <int KQ>
 PT2Q_DEV void ru_panel(const float* base, long ld, int layout, int d0, int DMAX, int K,
-                       float (*lds)[RU_T + 4]) {
+                       float (*lds)[RU_T + 4], bool neg = false) {
+  constexpr int NV = KQ * RU_T / 4 / 256;  // float4 per thread
+  constexpr int KV = KQ / 4;               // float4 per d row (ROWMAJOR)
   const int tid = threadIdx.x;
-  float4 v[4];
-  bool ok[4];
+  float4 v[NV];
+  bool ok[NV];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int q = tid + 256 * e;  // 1024 float4 = 64 x 64
+  for (int e = 0; e < NV; ++e) {
+    const int q = tid + 256 * e;
     int d, k;
     if (layout == LAY_KMAJOR) {
       k = q >> 4;
       d = (q & 15) * 4;
     } else {
-      d = q >> 4;
-      k = (q & 15) * 4;
+      d = q / KV;
+      k = (q % KV) * 4;
     }
     const long off = layout == LAY_KMAJOR ? (long)k * ld + d0 + d : (long)(d0 + d) * ld + k;
     // vectors are whole inside or outside (checked at launch: DMAX % 4 == 0 / K % 4 == 0)
-    ok[e] = layout == LAY_KMAJOR ? (k < K && d0 + d < DMAX) : (d0 + d < DMAX && k < K);
+    ok[e] = k < K && d0 + d < DMAX;
     v[e] = *(const float4*)(base + (ok[e] ? off : 0));
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < NV; ++e) {
     const int q = tid + 256 * e;
-    const float4 x = ok[e] ? v[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 x = ok[e] ? v[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (neg) x = make_float4(-x.x, -x.y, -x.z, -x.w);  // exact: (-a)·b is the chain's term
     if (layout == LAY_KMAJOR) {
       *(float4*)&lds[q >> 4][(q & 15) * 4] = x;
     } else {
-      const int d = q >> 4, k = (q & 15) * 4;
+      const int d = q / KV, k = (q % KV) * 4;
       lds[k][d] = x.x;
       lds[k + 1][d] = x.y;
       lds[k + 2][d] = x.z;
       lds[k + 3][d] = x.w;
     }
+  }
+}
+
+template <int OFF>
+PT2Q_DEV float ru_ld(uint32_t addr) {
+  float r;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// k-pair S of the chain: operands in set S % 4, the pair two ahead is read into set (S+2) % 4,
+// which no MFMA still waiting to issue reads.  LDS reads are asm (hipcc would wait for each one
+// right before its MFMA); the order reads -> MFMA -> wait is pinned.
+template <int S, int NS>
+PT2Q_DEV void ru_chain(f32x16& acc, uint32_t bA, uint32_t bB, float (&a)[4], float (&b)[4]) {
+  constexpr int ROW = 2 * (RU_T + 4) * 4;  // bytes per k-pair
+  if constexpr (S == 0) {
+    a[0] = ru_ld<0>(bA);
+    b[0] = ru_ld<0>(bB);
+    a[1] = ru_ld<ROW>(bA);
+    b[1] = ru_ld<ROW>(bB);
+    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a[0]), "+v"(b[0]));
+  }
+  if constexpr (S < NS) {
+    constexpr int c = S % 4, n2 = (S + 2) % 4;
+    if constexpr (S + 2 < NS) {
+      a[n2] = ru_ld<(S + 2) * ROW>(bA);
+      b[n2] = ru_ld<(S + 2) * ROW>(bB);
+    }
+    if constexpr (S > 0) {  // pair S-1's operands stay allocated until these reads are out
+      constexpr int p = (S + 3) % 4;
+      asm volatile("" ::"v"(a[p]), "v"(b[p]));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c], a[c], acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (S + 1 < NS) {  // pair S+1 landed (pair S+2 may stay in flight)
+      constexpr int c1 = (S + 1) % 4;
+      if constexpr (S + 2 < NS)
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a[c1]), "+v"(b[c1]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[c1]), "+v"(b[c1]));
+    }
+    ru_chain<S + 1, NS>(acc, bA, bB, a, b);
   }
 }
 
@@ -925,18 +974,25 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
       for (int e = 0; e < 4; ++e) F.acc[0][0][4 * q + e] = in ? v[e] : 0.0f;
     }
   }
-  ru_panel((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As);
-  ru_panel((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+  const bool k128 = g.K > 64, neg = g.mode == GEMM_CHAIN_NEG;
+  if (k128) {
+    ru_panel<128>((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
+    ru_panel<128>((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+  } else {
+    ru_panel<64>((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
+    ru_panel<64>((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
-  const float sgn = (g.mode == GEMM_CHAIN_NEG) ? -1.0f : 1.0f;
-  // all 32 k-pairs: the panels are zero past K, and a zero term is an exact no-op on a chain
-#pragma unroll
-  for (int s = 0; s < RU_K / 2; ++s) {
-    const float a = As[2 * s + lk][wr * 32 + li], b = Bs[2 * s + lk][wc * 32 + li];
-    F.acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b, sgn * a, F.acc[0][0], 0, 0, 0);
-  }
+  const uint32_t bA = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)&As[lk][wr * 32 + li];
+  const uint32_t bB = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)&Bs[lk][wc * 32 + li];
+  // 32 or 64 k-pairs (the panels are zero past K: a zero term is an exact no-op on a chain)
+  float a[4], b[4];
+  if (k128)
+    ru_chain<0, RU_K / 2>(F.acc[0][0], bA, bB, a, b);
+  else
+    ru_chain<0, 32>(F.acc[0][0], bA, bB, a, b);
   const int row = F.row_of(i0, 0, 0);
   if (row < g.M) {
 #pragma unroll
