@@ -14,55 +14,19 @@
 
 #include "common.hpp"
 #include "internal.hpp"
+#include "chol_diag.hpp"
 
 namespace {
 
-constexpr int NB = 64;
+using pt2q_chol::NB;
 
-// The diagonal-block factorisation with four waves: wave q keeps rows [16q, 16q+16) of every
-// column in registers (lane c = column c, col[s] = D[16q+s][c]).  Step k: the wave owning row
-// k forms U[k][·] from its registers (U[k][k] = sqrt(D[k][k]) via readlane, U[k][c] =
-// D[k][c]/U[k][k]) and publishes it in LDS (entries c <= k as 0); after ONE barrier every wave
-// applies D[r][c] = fmaf(-U[k][r], U[k][c], D[r][c]) to its rows (an fmaf with a zero factor is
-// an exact no-op, so rows <= k and columns <= k are untouched).  The k loop runs over the four
-// row quarters at run time with 16 unrolled steps inside, which keeps the code small (a fully
-// unrolled 64-step body overflowed the instruction cache and spilled).  Entries below the
-// diagonal are scratch, never written back.  Padding (nb < NB) is an identity block.
+// Diagonal-block factor (chol_diag.hpp) as a kernel of its own: the first block, and any block
+// whose producing update did not run the fused factor.
 __global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int p0, int nb,
                                                         int* info) {
-  __shared__ __attribute__((aligned(16))) float urow[2][NB];
-  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  float col[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int r = 16 * q + s;
-    const bool in = r < nb && c < nb;
-    col[s] = A[in ? (long)(p0 + r) * lda + p0 + c : (long)p0 * lda + p0];  // branch-free loads
-    col[s] = in ? col[s] : ((r == c) ? 1.0f : 0.0f);
-  }
-  for (int kq = 0; kq < 4; ++kq) {
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const int k = 16 * kq + ks;
-      float* ur = urow[ks & 1];
-      if (q == kq) {
-        const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[ks]), k));
-        if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
-        const float ukk = sqrtf(dkk);
-        col[ks] = (c == k) ? ukk : ((c > k) ? col[ks] / ukk : col[ks]);
-        ur[c] = (c > k) ? col[ks] : 0.0f;
-      }
-      __syncthreads();
-      const float ukc = ur[c];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) col[s] = fmaf(-ur[16 * q + s], ukc, col[s]);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int r = 16 * q + s;
-    if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[s];
-  }
+  __shared__ __attribute__((aligned(16))) float urow[2][pt2q_chol::DG][NB];
+  const float* D = A + (long)p0 * lda + p0;
+  pt2q_chol::diag_factor([&](int r, int c) { return D[(long)r * lda + c]; }, A, lda, p0, nb, info, urow);
 }
 
 constexpr int LPR = 4;           // lanes cooperating on one panel column / inverse row
@@ -240,10 +204,12 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
                      U, ld, m);
   PT2Q_LAUNCH_CHECK();
   int rc;
-  // diagonal factor + panel solve + in-block inverse of the block at p0
-  auto factor = [&](int p0, int nb) -> int {
-    hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
-    PT2Q_LAUNCH_CHECK();
+  // panel solve + in-block inverse of the block at p0 (its diagonal factor done: `factored`)
+  auto factor = [&](int p0, int nb, bool factored) -> int {
+    if (!factored) {
+      hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
+      PT2Q_LAUNCH_CHECK();
+    }
     const int rest = m - p0 - nb;
     const int npanel = rest > 0 ? (int)ceil_div((long)rest * LPR, 256) : 0;
     const int ninv = (int)ceil_div((long)(p0 + nb) * LPR, 256);
@@ -255,28 +221,34 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   // Blocks go in pairs (J, J+1): after J only block row J+1 gets J's terms (it is all the next
   // factor needs); after J+1 the rest of the trailing triangle gets the terms of both blocks in
   // one rank-128 pass (k ascending, so every chain is the one-block-at-a-time chain), which
-  // halves the passes over the trailing matrix.
+  // halves the passes over the trailing matrix.  Each update launch also factors the diagonal
+  // block it produces (the workgroup of that tile, from its registers: chol_diag.hpp), so no
+  // launch of its own sits between an update and the next panel.
+  bool factored = false;
   for (int p0 = 0; p0 < m;) {
     const int nb = (m - p0 < NB) ? m - p0 : NB;
-    if ((rc = factor(p0, nb)) != PT2Q_OK) return rc;
+    if ((rc = factor(p0, nb, factored)) != PT2Q_OK) return rc;
     const int rest = m - p0 - nb;
     if (rest <= 0) break;
     const int p1 = p0 + nb, nb1 = (rest < NB) ? rest : NB, rest1 = rest - nb1;
     static const char* pair_env = std::getenv("PT2Q_CHOL_PAIR");  // 0: one update per block (A/B)
     if (rest1 <= 0 || (pair_env && pair_env[0] == '0')) {  // one plain update
       if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, rest, p1, rest),
-                                  trtri_desc(U, Ui, ld, p0, nb, rest), st)) != PT2Q_OK)
+                                  trtri_desc(U, Ui, ld, p0, nb, rest), st, U, ld, p1, nb1, info,
+                                  &factored)) != PT2Q_OK)
         return rc;
       p0 = p1;
       continue;
     }
     if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, nb1, p1, rest, false),
-                                trtri_desc(U, Ui, ld, p0, nb, rest), st)) != PT2Q_OK)
+                                trtri_desc(U, Ui, ld, p0, nb, rest), st, U, ld, p1, nb1, info,
+                                &factored)) != PT2Q_OK)
       return rc;
-    if ((rc = factor(p1, nb1)) != PT2Q_OK) return rc;
-    const int p2 = p1 + nb1;
+    if ((rc = factor(p1, nb1, factored)) != PT2Q_OK) return rc;
+    const int p2 = p1 + nb1, nb2 = (rest1 < NB) ? rest1 : NB;
     if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb + nb1, p2, rest1, p2, rest1),
-                                trtri_desc(U, Ui, ld, p1, nb1, rest1), st)) != PT2Q_OK)
+                                trtri_desc(U, Ui, ld, p1, nb1, rest1), st, U, ld, p2, nb2, info,
+                                &factored)) != PT2Q_OK)
       return rc;
     p0 = p2;
   }

@@ -19,6 +19,7 @@
 
 #include "common.hpp"
 #include "internal.hpp"
+#include "chol_diag.hpp"
 
 namespace {
 
@@ -951,7 +952,17 @@ PT2Q_DEV void ru_chain(f32x16& acc, uint32_t bA, uint32_t bB, float (&a)[4], flo
   }
 }
 
-PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4], float (*Bs)[RU_T + 4]) {
+// diag.A != nullptr: tile 0 of this GEMM is the next diagonal block; the workgroup that updates
+// it factors it right away from its registers (chol_diag.hpp) instead of storing it.
+struct RuDiag {
+  float* A;
+  long lda;
+  int p0, nb;
+  int* info;
+};
+
+PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4], float (*Bs)[RU_T + 4],
+                      const RuDiag& diag = RuDiag{nullptr, 0, 0, 0, nullptr}) {
   int ti, tj;
   if (g.upper) {
     upper_tile(bid, tn, ti, tj);
@@ -994,6 +1005,20 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
   else
     ru_chain<0, 32>(F.acc[0][0], bA, bB, a, b);
   const int row = F.row_of(i0, 0, 0);
+  if (diag.A && bid == 0) {  // the updated diagonal block, through LDS, into the factor
+    __syncthreads();         // every wave is done with the panels: As becomes the D tile
+    float (*D)[RU_T + 1] = (float (*)[RU_T + 1])&As[0][0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = F.col_of(j0, 0, 4 * q) - j0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) D[row - i0][col + e] = F.acc[0][0][4 * q + e];
+    }
+    __syncthreads();
+    pt2q_chol::diag_factor([&](int r, int c) { return D[r][c]; }, diag.A, diag.lda, diag.p0, diag.nb,
+                           diag.info, (float (*)[pt2q_chol::DG][pt2q_chol::NB])&Bs[0][0]);
+    return;
+  }
   if (row < g.M) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1007,12 +1032,13 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
   }
 }
 
-__global__ __launch_bounds__(256) void rank_update2_kernel(GemmDesc g0, int tn0, int n0, GemmDesc g1, int tn1) {
+__global__ __launch_bounds__(256) void rank_update2_kernel(GemmDesc g0, int tn0, int n0, GemmDesc g1, int tn1,
+                                                           RuDiag diag) {
   __shared__ __attribute__((aligned(16))) float As[RU_K][RU_T + 4];
   __shared__ __attribute__((aligned(16))) float Bs[RU_K][RU_T + 4];
   const int b = blockIdx.x;
   if (b < n0)
-    ru_tile(g0, tn0, b, As, Bs);
+    ru_tile(g0, tn0, b, As, Bs, diag);
   else
     ru_tile(g1, tn1, b - n0, As, Bs);
 }
@@ -1051,16 +1077,23 @@ int launch2_t(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
 
 }  // namespace
 
-int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st) {
+int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, float* dA, long dld,
+                      int dp0, int dnb, int* info, bool* fused) {
+  if (fused) *fused = false;
   if (g0.in_dtype != PT2Q_F32 || g1.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
   static const char* ru_env = std::getenv("PT2Q_RANK_UPDATE");  // 0: generic grouped GEMM
   if (ru_ok(g0) && ru_ok(g1) && !(ru_env && ru_env[0] == '0')) {
     int tm0, tn0, tm1, tn1;
     const long n0 = tiles_of<RU_T, RU_T>(g0, tm0, tn0), n1 = tiles_of<RU_T, RU_T>(g1, tm1, tn1);
     if (n0 + n1 <= 0) return PT2Q_OK;
+    // the fused factor needs g0's tile 0 to be exactly the next diagonal block at (dp0, dp0)
+    const bool fuse = dA && n0 > 0 && g0.C == dA + (long)dp0 * dld + dp0 && g0.ldc == dld &&
+                      dnb > 0 && dnb <= RU_T && g0.M >= dnb && g0.N >= dnb;
+    RuDiag d{fuse ? dA : nullptr, dld, dp0, dnb, info};
     hipLaunchKernelGGL(rank_update2_kernel, dim3((unsigned)(n0 + n1)), dim3(256), 0, st, g0, tn0,
-                       (int)n0, g1, tn1);
+                       (int)n0, g1, tn1, d);
     PT2Q_LAUNCH_CHECK();
+    if (fused) *fused = fuse;
     return PT2Q_OK;
   }
   int a, b;

@@ -49,7 +49,11 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
 int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
                    const int* crow, int nr, int bs, hipStream_t st);
 // two independent f32 GEMMs in one launch (either may be empty)
-int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st);
+// dA != nullptr: also factor the diagonal block (dp0, dp0) of dA (nb dnb) in the same launch if
+// g0's first tile is that block; *fused reports whether it did (else launch the factor).
+int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, float* dA = nullptr,
+                      long dld = 0, int dp0 = 0, int dnb = 0, int* info = nullptr,
+                      bool* fused = nullptr);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st);
 size_t pt2q_gram_flags_ints(int m);
