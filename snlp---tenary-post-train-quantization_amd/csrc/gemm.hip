@@ -1121,7 +1121,8 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
 
 size_t pt2q_gram_flags_ints(int m) {
   long T = ceil_div(m, 128);
-  return (size_t)(T * (T + 1) / 2 + 2 + 8);  // tile flags, timeout, unit counter, zero chunk
+  // tile flags, timeout, unit counter, zero chunk; or the 16-bit kernel's
+  return std::max((size_t)(T * (T + 1) / 2 + 2 + 8), pt2q_gram16_flags_ints(m));
 }
 
 // Symmetric Gram C = XᵀX (STORE): balanced persistent kernel when it pays (big K, enough

@@ -299,43 +299,55 @@ struct GxTile {
 };
 
 // g: M = N = m, K = rows, A = X (ld lda), C = G (ldc), mode STORE / ADD / CHAIN_POS.
-// The tile line (column-block major) is cut into NG contiguous groups; group x is worked by
-// workgroups w = x, x + NG, x + 2NG, ... (R of them), which on the round-robin dispatch share an
-// XCD and so its L2 (speed only).  Inside a group, workgroup r takes rows [r*L, (r+1)*L) of the
-// group's line of cnt * Kp rows: tail piece first (chains from the start of its last tile),
-// full tiles, then the head piece of its first tile, continuing the partial that workgroup
-// r-1 (= w - NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
+// D data-parallel waves first: in wave v workgroup w = x + NG*r takes whole tile
+// v*grid + x*R + r, so the R workgroups of one XCD run 32 neighbouring tiles of the order at the
+// same k and share their X panels through that XCD's L2.  The rest of the tile line (stream-K)
+// is cut into NG contiguous groups; group x is worked by workgroups w = x, x + NG, x + 2NG, ...
+// (R of them), which on the round-robin dispatch share an XCD and so its L2 (speed only).
+// Inside a group, team r/P takes rows [team*L, (team+1)*L) of the group's line of cnt * Kp rows
+// (units of P tiles): tail piece first (chains from the start of its last unit), full units,
+// then the head piece of its first unit, continuing the partial that the same member of the
+// previous team (w - P*NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
 template <bool BF16, bool DMA>
 __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ, int SJ, int Kp, long ntile, int NG,
-                                                      int R, int* flags, int* timeout) {
+                                                      int R, int P, int D, int* flags, int* timeout) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[GX_LDS];
   const uint16_t* X = (const uint16_t*)g.A;
   const int w = blockIdx.x;
   const int x = w % NG, r = w / NG;
-  const long t0 = ntile * x / NG, cnt = ntile * (x + 1) / NG - t0;
+  const long base = (long)D * gridDim.x;  // first stream-K tile
+  // P = 2: the line is cut into tile pairs (2j, 2j+1), which share their column block tj, and
+  // workgroups r = 2i, 2i+1 (a team) walk the same stretch of pairs in step, one tile of each
+  // pair apiece, so the X panel of tj is fetched into L2 once for both.
+  const int mem = r % P, team = r / P, nteam = R / P;
+  const long npair = (ntile - base) / P;
+  const long t0 = P * (npair * x / NG), cnt = npair * (x + 1) / NG - npair * x / NG;
   const long W = cnt * Kp;
-  const long L = (R == 0) ? Kp : ((W + R - 1) / R + GX_BK - 1) / GX_BK * GX_BK;
-  const long s = (long)r * L, e = min(s + L, W);
-  if (s >= e) return;
+  const long L = (R == 0) ? Kp : ((W + nteam - 1) / nteam + GX_BK - 1) / GX_BK * GX_BK;
+  const long s = (long)team * L, e = min(s + L, W);
   const int a0 = (int)(s / Kp), k0 = (int)(s % Kp);
   const int a1 = (int)((e - 1) / Kp), k1 = (int)(e - (long)a1 * Kp);
   const bool head = k0 > 0;
   const bool tail = k1 < Kp && !(head && a1 == a0);
   const int f0 = head ? a0 + 1 : a0, f1 = tail ? a1 - 1 : a1;
   const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
-  const int npieces = (tail ? 1 : 0) + nfull + (head ? 1 : 0);
+  const int npieces = s >= e ? 0 : (tail ? 1 : 0) + nfull + (head ? 1 : 0);
   const bool vec4 = ((uintptr_t)g.C % 16 == 0) && (g.ldc % 4 == 0);
-  for (int pc = 0; pc < npieces; ++pc) {
+  for (int pc = -D; pc < npieces; ++pc) {
     int a, kb, ke;
     bool from_partial = false;
-    if (tail && pc == 0) {
-      a = a1; kb = 0; ke = k1;
-    } else if (head && pc == npieces - 1) {
-      a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
+    if (pc < 0) {
+      a = (pc + D) * (int)gridDim.x + x * R + r; kb = 0; ke = Kp;
     } else {
-      a = f0 + pc - (tail ? 1 : 0); kb = 0; ke = Kp;
+      if (tail && pc == 0) {
+        a = a1; kb = 0; ke = k1;
+      } else if (head && pc == npieces - 1) {
+        a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
+      } else {
+        a = f0 + pc - (tail ? 1 : 0); kb = 0; ke = Kp;
+      }
+      a = (int)(base + t0) + P * a + mem;  // global tile index (flags are per tile)
     }
-    a += (int)t0;  // global tile index (flags are per tile)
     int ti, tj;
     gx_tile(a, TI, TJ, SJ, ti, tj);
     const int i0 = ti * GX_BM, j0 = tj * GX_BN;
@@ -435,13 +447,20 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
   int R = cus / NG;
   const bool split = flags && g.mode != GEMM_ADD && !(split_env && split_env[0] == '0') &&
                      R > 0 && ntile >= (long)NG * R;
+  // tile pairs need every column run of the tile order to be even (TI even) and teams of two
+  static const char* pair_env = std::getenv("PT2Q_GRAM_PAIR");
+  int P = (split && TI % 2 == 0 && R % 2 == 0 && !(pair_env && pair_env[0] == '0')) ? 2 : 1;
+  // whole data-parallel waves while at least one tile per workgroup is left for stream-K
+  static const char* dp_env = std::getenv("PT2Q_GRAM_DP");
+  const int D = (split && !(dp_env && dp_env[0] == '0')) ? (int)std::max(0l, ntile / (NG * R) - 1) : 0;
   unsigned grid;
   if (split) {
     grid = (unsigned)(NG * R);
-    if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2), st) != hipSuccess) return PT2Q_E_HIP;
+    if (hipMemsetAsync(flags, 0, sizeof(int) * pt2q_gram16_flags_ints(m), st) != hipSuccess) return PT2Q_E_HIP;
   } else {
     NG = 1;
     R = 0;
+    P = 1;
     grid = (unsigned)ntile;
   }
   (void)W;
@@ -449,10 +468,10 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
   // (fast staging keeps a stage's byte offsets in 32 bits: 64 rows * lda * 2 < 2^32)
   const bool dma = ((uintptr_t)g.A % 16 == 0) && (g.lda % 8 == 0) && (m % 8 == 0) && g.lda < (1l << 25);
   const bool bf = g.in_dtype == PT2Q_BF16;
-  void (*k)(GemmDesc, int, int, int, int, long, int, int, int*, int*) =
+  void (*k)(GemmDesc, int, int, int, int, long, int, int, int, int, int*, int*) =
       bf ? (dma ? gram16x_kernel<true, true> : gram16x_kernel<true, false>)
          : (dma ? gram16x_kernel<false, true> : gram16x_kernel<false, false>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, TJ, SJ, Kp, ntile, NG, R, flags, timeout);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, TJ, SJ, Kp, ntile, NG, R, P, D, flags, timeout);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

@@ -65,11 +65,14 @@ def test_gram_bitexact(pt2q, N, m, dt):
 
 
 @pytest.mark.parametrize("N,m,dt", [(2048, 4096, torch.float16), (1000, 4104, torch.bfloat16),
-                                     (777, 4100, torch.float16), (17000, 2048, torch.float32)])
+                                     (777, 4100, torch.float16), (17000, 2048, torch.float32),
+                                     (1500, 4352, torch.bfloat16), (333, 8192, torch.float16),
+                                     (64, 11008, torch.bfloat16)])
 def test_gram_streamk_bitexact(pt2q, N, m, dt):
     """The balanced persistent Gram (static split of the tile line over one workgroup per CU,
-    chains continued through fp32 partials: 16-bit X splits from m >= 4096) must equal the
-    oracle bit-for-bit, including ragged m / N (m % 8 != 0: register-staged operands)."""
+    chains continued through fp32 partials: 16-bit X splits from m >= 4096; even tile rows: tile
+    pairs worked by teams of two) must equal the oracle bit-for-bit, including ragged m / N
+    (m % 8 != 0: register-staged operands)."""
     orc.set_threads(16)
     X = synth.activations(13 + m, N, m)
     Xd = cuda(X).to(dt)
