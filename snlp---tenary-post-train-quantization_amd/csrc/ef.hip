@@ -29,6 +29,7 @@ constexpr int EF_STAGE = 2 * EF_PANEL;       // A + B
 constexpr int EF_DMA = 16;                   // DMA instructions per wave per stage
 constexpr int EF_CV = 16;                    // C float4 loads (= stores) per lane per tile
 constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropped access)
+constexpr int EF_MAX_NR = 16384;             // remaining columns staged in LDS (16-bit rows)
 
 __device__ uint4 ef_zero16;  // DMA source of the k rows past bs (zero-initialised)
 
@@ -46,22 +47,24 @@ struct EfArgs {
 // k rows past bs come from a zero chunk (their MFMA steps are then exact no-ops); columns past
 // the data come from row 0 (garbage in rows / columns whose results are dropped), so every wave
 // issues exactly EF_DMA instructions.
-PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
+PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, int q) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   typedef __attribute__((address_space(3))) void* lptr;
+  const int kr = (wave * 8 + q) * 2 + (lane >> 5);  // k row inside the stage
+  const int k = h * EF_KH + kr;
+  const int d = 4 * (lane & 31);
+  const bool kin = k < a.bs;
+  const int e = e0 + d, i = i0 + d;
+  const void* sa = kin ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
+  const void* sb = kin ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
+}
+
+PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int kr = (wave * 8 + q) * 2 + (lane >> 5);  // k row inside the stage
-    const int k = h * EF_KH + kr;
-    const int d = 4 * (lane & 31);
-    const bool kin = k < a.bs;
-    const int e = e0 + d, i = i0 + d;
-    const void* sa = kin ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
-    const void* sb = kin ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
-    const int wv = __builtin_amdgcn_readfirstlane(wave);
-    __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
-  }
+  for (int q = 0; q < 8; ++q) ef_stage_q(a, e0, i0, h, stg, q);
 }
 
 template <int OFF>
@@ -90,11 +93,12 @@ struct EfAcc {
   // k-pair S: its operands are in set S % 3; the reads of pair S+1 go to set (S+1) % 3, whose
   // registers the MFMAs of pair S-2 read long ago (no overwrite of an operand in flight).  The
   // order reads -> MFMAs -> wait is pinned (the scheduler would sink the reads below the MFMAs).
-  template <int S>
-  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[3][2], float (&b)[3][2]) {
+  template <int S, class IO>
+  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[3][2], float (&b)[3][2], IO& io) {
     if constexpr (S < EF_KH / 2) {
       constexpr int c = S % 3, n = (S + 1) % 3;
       if constexpr (S + 1 < EF_KH / 2) ef_read<S + 1>(bA, bB, a[n], b[n]);
+      io.template at<S>();
       if constexpr (S > 0) {  // pair S-1's operands stay allocated until these reads are out
         constexpr int p = (S + 2) % 3;
         asm volatile("" ::"v"(a[p][0]), "v"(a[p][1]), "v"(b[p][0]), "v"(b[p][1]));
@@ -107,12 +111,13 @@ struct EfAcc {
           acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][rn], a[c][rm], acc[rm][rn], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (S + 1 < EF_KH / 2) ef_wait(a[n], b[n]);
-      run<S + 1>(bA, bB, a, b);
+      run<S + 1>(bA, bB, a, b, io);
     }
   }
 
   // the 32 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
-  PT2Q_DEV void half(uint32_t stg) {
+  template <class IO>
+  PT2Q_DEV void half(uint32_t stg, IO& io) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
     const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
@@ -120,7 +125,7 @@ struct EfAcc {
     float a[3][2], b[3][2];
     ef_read<0>(bA, bB, a[0], b[0]);
     ef_wait(a[0], b[0]);
-    run<0>(bA, bB, a, b);
+    run<0>(bA, bB, a, b, io);
   }
 };
 
@@ -141,24 +146,42 @@ PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm,
   return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
 }
 
-PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
+PT2Q_DEV void ef_rows(const EfArgs& a, const uint16_t* crow_lds, int e0, int (&wrow)[2]) {
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm) {
     const int e = ef_row(e0, rm);
-    wrow[rm] = e < a.nr ? a.crow[e] : -1;
+    wrow[rm] = e < a.nr ? (int)crow_lds[e] : -1;
   }
 }
 
-PT2Q_DEV void ef_cload(const EfArgs& a, __amdgpu_buffer_rsrc_t rc, const int (&wrow)[2], int i0,
-                       u32x4 (&c)[EF_CV]) {
-#pragma unroll
-  for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-    for (int rn = 0; rn < 2; ++rn)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        c[(rm * 2 + rn) * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
-}
+struct EfNoIO {
+  template <int S>
+  PT2Q_DEV void at() {}
+};
+
+// The Wt traffic of a tile, spread over the first K half of the next one instead of bursting
+// at tile ends (every CU would burst at once): at every even k-pair one store of the previous
+// tile's results and one load of this tile's old values.  Rows of the previous tile are -1
+// before the first tile (stores dropped, counts unchanged).
+struct EfIO {
+  const EfArgs& a;
+  __amdgpu_buffer_rsrc_t rc;
+  const int (&prow)[2];
+  int pi0;
+  const int (&wrow)[2];
+  int i0;
+  const u32x4 (&pend)[EF_CV];
+  u32x4 (&c)[EF_CV];
+
+  template <int S>
+  PT2Q_DEV void at() {
+    if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
+      constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
+      __builtin_amdgcn_raw_buffer_store_b128(pend[j], rc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
+      c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+    }
+  }
+};
 
 // s_waitcnt vmcnt(N) for the small set of counts the schedule needs (immediate operand)
 PT2Q_DEV void ef_vmcnt(int n) {
@@ -172,26 +195,31 @@ PT2Q_DEV void ef_vmcnt(int n) {
 
 __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
+  __shared__ uint16_t crow_lds[EF_MAX_NR];
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   int t = blockIdx.x;
   if (t >= a.ntile) return;
+  for (int e = threadIdx.x; e < a.nr; e += blockDim.x) crow_lds[e] = (uint16_t)a.crow[e];
   auto corner = [&](int t, int& e0, int& i0) {
     e0 = (t / a.ti) * EF_T;
     i0 = (t % a.ti) * EF_T;
   };
   int e0, i0, wrow[2];
   corner(t, e0, i0);
-  ef_rows(a, e0, wrow);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // prologue: this tile's stages, then its old C
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  ef_rows(a, crow_lds, e0, wrow);
   ef_stage(a, e0, i0, 0, smem);
   if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
-  u32x4 c[EF_CV];
-  ef_cload(a, rc, wrow, i0, c);
+  int prow[2] = {-1, -1}, pi0 = 0;
+  u32x4 c[EF_CV], pend[EF_CV];
+#pragma unroll
+  for (int j = 0; j < EF_CV; ++j) pend[j] = u32x4{};
+  // issue order per tile: [stores of the previous tile + this tile's old values, interleaved
+  // with K half 0] [next stage 0] [K half 1] [next stage 1]
   const int S1 = a.nh == 2 ? EF_DMA : 0;
-  // issue order per tile: [stage0] [stage1] [stores of the previous tile] [old C] ...
-  for (bool first = true;; first = false) {
+  for (;;) {
     const int tn = t + (int)gridDim.x;
     const bool more = tn < a.ntile;
     int en = 0, in = 0, nrow[2] = {-1, -1};
@@ -201,41 +229,48 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
       for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
-    ef_vmcnt(S1 + (first ? 0 : EF_CV) + EF_CV);  // stage 0 landed
+    ef_vmcnt(S1);  // stage 0 landed (younger: stage 1)
     asm volatile("s_barrier" ::: "memory");
-    if (more) ef_rows(a, en, nrow);  // the next tile's Wt rows (2 loads, long before their use)
-    F.half(lds0);
+    if (more) ef_rows(a, crow_lds, en, nrow);
+    {
+      EfIO io{a, rc, prow, pi0, wrow, i0, pend, c};
+      F.half(lds0, io);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
     if (more) ef_stage(a, en, in, 0, smem);
     if (a.nh == 2) {
-      ef_vmcnt((first ? 0 : EF_CV) + EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
+      ef_vmcnt(2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
       asm volatile("s_barrier" ::: "memory");
-      F.half(lds0 + EF_STAGE);
+      EfNoIO nio;
+      F.half(lds0 + EF_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (more) ef_stage(a, en, in, 1, smem + EF_STAGE);
     }
-    ef_vmcnt(more ? EF_DMA + S1 : 0);  // the old C landed (younger: the next tile's stages)
+    ef_vmcnt(more ? EF_DMA + S1 : 0);  // the old values landed (younger: the next tile's stages)
 #pragma unroll
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
       for (int rn = 0; rn < 2; ++rn)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const u32x4 o = c[(rm * 2 + rn) * 4 + q];
-          u32x4 w;
+          const int j = (rm * 2 + rn) * 4 + q;
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            w[u] = __float_as_uint(__uint_as_float(o[u]) - F.acc[rm][rn][4 * q + u]);
-          __builtin_amdgcn_raw_buffer_store_b128(w, rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+            pend[j][u] = __float_as_uint(__uint_as_float(c[j][u]) - F.acc[rm][rn][4 * q + u]);
         }
+    prow[0] = wrow[0];
+    prow[1] = wrow[1];
+    pi0 = i0;
     if (!more) break;
     t = tn;
     e0 = en;
     i0 = in;
     wrow[0] = nrow[0];
     wrow[1] = nrow[1];
-    ef_cload(a, rc, wrow, i0, c);
   }
+#pragma unroll
+  for (int j = 0; j < EF_CV; ++j)
+    __builtin_amdgcn_raw_buffer_store_b128(pend[j], rc, ef_coff(a, prow, pi0, j >> 3, (j >> 2) & 1, j & 3), 0, 0);
 }
 
 }  // namespace
@@ -247,7 +282,7 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   if (nr <= 0) return PT2Q_OK;
   const long wt_bytes = wt_rows * ldw * 4;
   if (bs <= 0 || bs > 2 * EF_KH || ldw % 4 || ldk % 4 || (uintptr_t)Ck % 16 || (uintptr_t)Et % 16 ||
-      (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP)
+      (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP || nr > EF_MAX_NR || wt_rows > 65536)
     return PT2Q_E_UNSUPPORTED;
   EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1};
   a.ntile = a.te * a.ti;

@@ -1,4 +1,4 @@
 set -e
-for b in gram16_probe gram16_probe-DGX_PROBE_NO_MFMA gram16_probe-DGX_PROBE_NO_DMA; do
-  for m in 4096 11008; do echo "$b m=$m"; timeout -k 10 120 tools/$b.bin 262144 $m 3; done
-done
+for nr in 3968 2048 512; do timeout -k 10 60 tools/ef_probe.bin 4096 $nr 128 20; done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -m gpu 2>&1 | tail -2
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-n2048 | cut -c1-200
