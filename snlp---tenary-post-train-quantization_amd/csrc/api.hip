@@ -12,9 +12,13 @@ struct Carve {
   char* p;
   size_t left;
   bool ok = true;
+  bool dry = false;  // count only (used bytes in `used`)
+  size_t used = 0;
   template <typename T>
   T* take(size_t count) {
     size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    used += bytes;
+    if (dry) return nullptr;
     if (!p || bytes > left) {
       ok = false;
       return nullptr;
@@ -63,35 +67,18 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
   w.rem[0] = c.take<int>((size_t)m);
   w.rem[1] = c.take<int>((size_t)m);
   w.blk = c.take<int>((size_t)bb);
-  w.counters = c.take<int>((size_t)4 * B);  // [2k, 2k+1] ATQ; [2B+2k, 2B+2k+1] top-k/S1 sync
+  // [2k, 2k+1] ATQ; [2B+2k, 2B+2k+1] top-k/S1 sync; [4B ..) the wbar hand-off counters
+  w.counters = c.take<int>((size_t)4 * B + pt2q_ssr_counter_ints(n));
   w.iters = c.take<int>((size_t)B);
   return c.ok;
 }
 
-size_t blocks_bytes(int n, int m, int b) {
+size_t blocks_bytes(int n, int m, int b) {  // a dry run of carve_blocks
   Carve c{nullptr, 0};
-  // dry run: count
-  size_t total = 0;
-  auto add = [&](size_t bytes) { total += (bytes + 255) & ~(size_t)255; };
-  const long ldw = round_up(n, 64);
-  const int bb = b < m ? b : m;
-  const int B = b < m ? ceil_div(m, b) : 1;
-  add((size_t)m * ldw * 4);
-  add((size_t)m * ldw);
-  add(B > 1 ? (size_t)bb * ldw * 4 : 4);
-  add(B > 1 ? (size_t)bb * m * 4 : 4);
-  add((size_t)B * n * 4);
-  add((size_t)B * n * 4);
-  add((size_t)bb * 4);
-  add(4);
-  add(pt2q_ssr_scratch_floats(n, m) * 4);
-  add((size_t)m * 4);
-  add((size_t)m * 4);
-  add((size_t)bb * 4);
-  add((size_t)4 * B * 4);
-  add((size_t)B * 4);
-  (void)c;
-  return total;
+  c.dry = true;
+  BlockWs w;
+  carve_blocks(c, n, m, b, w);
+  return c.used;
 }
 
 __global__ void i64_to_i32_kernel(const int64_t* a, int n, int* b) {
@@ -115,7 +102,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   // W (n x m) -> Wt (m x ldw, fp32)
   if ((rc = pt2q_launch_transpose_to_f32(W, wdtype, ldw_in, n, m, w.Wt, w.ldw, st)) != PT2Q_OK)
     return rc;
-  if (hipMemsetAsync(w.counters, 0, sizeof(int) * 4 * B, st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(w.counters, 0, sizeof(int) * (4 * B + pt2q_ssr_counter_ints(n)), st) != hipSuccess)
+    return PT2Q_E_HIP;
   if (hipMemsetAsync(iters, 0, sizeof(int) * B, st) != hipSuccess) return PT2Q_E_HIP;
   // rem0 = [0, m)
   if ((rc = pt2q_launch_select_seq(0, 0, 0, m, nullptr, w.blk, w.rem[0], nullptr, st)) != PT2Q_OK)
@@ -133,7 +121,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     const bool s1_in_topk = ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
     if (ssr) {
       if (r > b) {
-        if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st)) != PT2Q_OK)
+        if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B)) !=
+            PT2Q_OK)
           return rc;
         if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st,
                                        s1_in_topk ? A : nullptr, lda, w.S1, w.d,
@@ -341,7 +330,9 @@ extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const 
     float* part = w.ssr;
     float* wn = part + (size_t)ceil_div(m, 128) * n;
     float* simb = sim ? sim : wn + n;
-    if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, w.rem[0], r, part, wn, simb, st)) != PT2Q_OK)
+    int* cnt = w.counters + 4 * ceil_div(m, 128);
+    if (hipMemsetAsync(cnt, 0, sizeof(int) * pt2q_ssr_counter_ints(n), st) != hipSuccess) return PT2Q_E_HIP;
+    if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, w.rem[0], r, part, wn, simb, st, cnt)) != PT2Q_OK)
       return rc;
     if (r > b) {
       if ((rc = pt2q_launch_ssr_topk(simb, w.rem[0], r, b, blk32, nrem32, nullptr, st)) != PT2Q_OK)

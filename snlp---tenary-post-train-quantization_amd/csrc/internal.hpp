@@ -11,8 +11,10 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           const int* rem = nullptr, int nr = 0, float* C = nullptr, long ldc = 0);
 
 // ---- SSR / selection (ssr.hip)
+// cnt (nullable): pt2q_ssr_counter_ints(n) zeroed ints -> one fused wbar launch (self-resetting)
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
-                               float* part, float* wn, float* sim, hipStream_t st);
+                               float* part, float* wn, float* sim, hipStream_t st, int* cnt = nullptr);
+inline int pt2q_ssr_counter_ints(int n) { return (n + 255) / 256 + 1; }
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
                          float* S1 = nullptr, float* d = nullptr, int* sync = nullptr);

@@ -37,6 +37,89 @@ __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, 
   part[(long)c * n + i] = p;
 }
 
+// The three wbar steps in one launch (n <= 4096, n % 4 == 0): every workgroup forms its partial
+// part[c][i] as ssr_wbar_partial_kernel; the last workgroup to finish a 256-row slice sums that
+// slice's partials in chunk order (wbar = sum / r); the last slice to finish forms
+// nw = clamp(sqrt(SUMN fma wbar^2)) and wn = wbar / nw.  Hand-offs: write-through (sc1) stores,
+// drained by every storing wave before the barrier that precedes the counter add, and sc1 loads
+// on the consuming side (no fences).  cnt: nslices + 1 ints, zero before the first launch; the
+// last arrivers put them back to zero.
+__global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, long ldw, int n,
+                                                             const int* rem, int r, float* part,
+                                                             float* wn, int* cnt) {
+  __shared__ long rows[CHUNK];
+  __shared__ int last;
+  const int c = blockIdx.x, nchunks = gridDim.x, nsl = gridDim.y;
+  const int e0 = c * CHUNK, ce = min(r, e0 + CHUNK) - e0;
+  for (int e = threadIdx.x; e < ce; e += blockDim.x) rows[e] = (long)rem[e0 + e] * ldw;
+  __syncthreads();
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  if (i < n) {
+    float p = 0.0f;
+    int e = 0;
+    for (; e + 8 <= ce; e += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = Wt[rows[e + u] + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p = p + v[u];
+    }
+    for (; e < ce; ++e) p = p + Wt[rows[e] + i];
+    __hip_atomic_store(part + (long)c * n + i, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(cnt + blockIdx.y, 1) == nchunks - 1;
+  __syncthreads();
+  if (!last) return;
+  if (i < n) {
+    float t = 0.0f;
+    int k = 0;
+    for (; k + 8 <= nchunks; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = __hip_atomic_load(part + (long)(k + u) * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t = t + v[u];
+    }
+    for (; k < nchunks; ++k)
+      t = t + __hip_atomic_load(part + (long)k * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(wn + i, t / (float)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(cnt + blockIdx.y, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = atomicAdd(cnt + nsl, 1) == nsl - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x >= 64) return;
+  // wave 0: lane t holds elements {256u + 4t + q} (sumn_lane's order) in registers
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wn, 0, n * 4, 0x00020000);
+  const int t = threadIdx.x;
+  f4 v[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (4 * t + 256 * u) * 4, 0, 16));
+  float q = 0.0f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (4 * t + 256 * u < n) {
+      q = fmaf(v[u][0], v[u][0], q);
+      q = fmaf(v[u][1], v[u][1], q);
+      q = fmaf(v[u][2], v[u][2], q);
+      q = fmaf(v[u][3], v[u][3], q);
+    }
+  const float nw = clampmin(sqrtf(bfly64(q)));
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (4 * t + 256 * u < n) *(f4*)(wn + 4 * t + 256 * u) = v[u] / nw;
+  if (t == 0) __hip_atomic_store(cnt + nsl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // wbar[i] = (chunk partials summed in chunk order) / r
 __global__ __launch_bounds__(256) void ssr_wbar_sum_kernel(const float* part, int nchunks, int n,
                                                            int r, float* wbar) {
@@ -623,22 +706,29 @@ size_t pt2q_ssr_scratch_floats(int n, int m) {
 }
 
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
-                               float* part, float* wn, float* sim, hipStream_t st) {
+                               float* part, float* wn, float* sim, hipStream_t st, int* cnt) {
   if (r <= 0 || n <= 0) return PT2Q_E_ARG;
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
-  hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
-                     Wt, ldw, n, rem, r, part);
-  PT2Q_LAUNCH_CHECK();
-  if (n <= SUMN_LDS_MAX) {
-    hipLaunchKernelGGL(ssr_wbar_sumfinal_kernel, dim3(1), dim3(1024), 0, st, part, nchunks, n, r, wn);
+  static const char* fuse_env = std::getenv("PT2Q_WBAR_FUSED");  // 0: three launches
+  if (cnt && n <= 4096 && n % 4 == 0 && !(fuse_env && fuse_env[0] == '0')) {
+    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st, Wt, ldw,
+                       n, rem, r, part, wn, cnt);
     PT2Q_LAUNCH_CHECK();
   } else {
-    hipLaunchKernelGGL(ssr_wbar_sum_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, nchunks,
-                       n, r, wn);
+    hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
+                       Wt, ldw, n, rem, r, part);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), 0, st, wn, n);
-    PT2Q_LAUNCH_CHECK();
+    if (n <= SUMN_LDS_MAX) {
+      hipLaunchKernelGGL(ssr_wbar_sumfinal_kernel, dim3(1), dim3(1024), 0, st, part, nchunks, n, r, wn);
+      PT2Q_LAUNCH_CHECK();
+    } else {
+      hipLaunchKernelGGL(ssr_wbar_sum_kernel, dim3(ceil_div(n, 256)), dim3(256), 0, st, part, nchunks,
+                         n, r, wn);
+      PT2Q_LAUNCH_CHECK();
+      hipLaunchKernelGGL(ssr_wbar_final_kernel, dim3(1), dim3(1024), 0, st, wn, n);
+      PT2Q_LAUNCH_CHECK();
+    }
   }
   hipLaunchKernelGGL(ssr_sim_kernel, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r,
                      wn, sim);
