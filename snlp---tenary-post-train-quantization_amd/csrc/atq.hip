@@ -36,16 +36,17 @@ PT2Q_DEV float round_code(float d, float as, float ras, bool ras_ok) {
 PT2Q_DEV float rcp_approx(float as) { return __builtin_amdgcn_rcpf(as); }
 PT2Q_DEV bool rcp_ok(float as) { return as < 1e30f; }  // as >= 1e-8 by the clamp
 
-template <int NS>
+// FULL: b == 16 * NS (every lane holds NS elements; no per-element range checks)
+template <int NS, bool FULL = false>
 struct Row {
   float w[NS];
   float t[NS];
   int l, b;
-  PT2Q_DEV bool has(int s) const { return l + 16 * s < b; }
+  PT2Q_DEV bool has(int s) const { return FULL || l + 16 * s < b; }
 };
 
-template <int NS>
-PT2Q_DEV float row_sum_w(const Row<NS>& R) {
+template <int NS, bool F>
+PT2Q_DEV float row_sum_w(const Row<NS, F>& R) {
   float p = 0.0f;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -54,8 +55,8 @@ PT2Q_DEV float row_sum_w(const Row<NS>& R) {
 }
 
 // ternary_init, quantizer.py:32-69. Returns alpha0, mu0; sets R.t; returns whether all t == 0.
-template <int NS>
-PT2Q_DEV bool row_init(Row<NS>& R, float wsum, float* alpha0, float* mu0) {
+template <int NS, bool F>
+PT2Q_DEV bool row_init(Row<NS, F>& R, float wsum, float* alpha0, float* mu0) {
   const float fb = (float)R.b;
   float mu = wsum / fb;
   float p = 0.0f;
@@ -83,8 +84,8 @@ PT2Q_DEV bool row_init(Row<NS>& R, float wsum, float* alpha0, float* mu0) {
 }
 
 // build_optimal_grid, quantizer.py:71-108.
-template <int NS>
-PT2Q_DEV void row_grid(const Row<NS>& R, float wsum, float* a, float* m) {
+template <int NS, bool F>
+PT2Q_DEV void row_grid(const Row<NS, F>& R, float wsum, float* a, float* m) {
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -101,8 +102,8 @@ PT2Q_DEV void row_grid(const Row<NS>& R, float wsum, float* a, float* m) {
 }
 
 // flexible_round, quantizer.py:110-134. Returns true if this lane changed a code.
-template <int NS>
-PT2Q_DEV bool row_round(Row<NS>& R, float a, float m) {
+template <int NS, bool F>
+PT2Q_DEV bool row_round(Row<NS, F>& R, float a, float m) {
   float as = clampmin(a);
   const float ras = rcp_approx(as);
   const bool rok = rcp_ok(as);
@@ -119,8 +120,8 @@ PT2Q_DEV bool row_round(Row<NS>& R, float a, float m) {
 
 // iterative_ternary_fitting, quantizer.py:136-175, wave-level stop (see file header).
 // Assumes the block is not all-zero at init (iteration 0 never stops).
-template <int NS>
-PT2Q_DEV int row_itf(Row<NS>& R, float wsum, int max_iter, float* a, float* m) {
+template <int NS, bool F>
+PT2Q_DEV int row_itf(Row<NS, F>& R, float wsum, int max_iter, float* a, float* m) {
   int it = 0;
   bool any = true;
   for (; it < max_iter; ++it) {
@@ -133,8 +134,8 @@ PT2Q_DEV int row_itf(Row<NS>& R, float wsum, int max_iter, float* a, float* m) {
 }
 
 // activation_aware_grid_alignment, quantizer.py:177-248, given S1 (per lane) and d.
-template <int NS>
-PT2Q_DEV void row_aga(const Row<NS>& R, const float (&S1)[NS], float d, float* a, float* m) {
+template <int NS, bool F>
+PT2Q_DEV void row_aga(const Row<NS, F>& R, const float (&S1)[NS], float d, float* a, float* m) {
   float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -170,31 +171,44 @@ struct BlockArgs {
   int* counters;     // [0] zero-init rows, [1] workgroups done
 };
 
-template <int NS>
+template <int NS, bool F = false>
 PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_zero) {
   const int lane = threadIdx.x & 63;
   const int r = lane >> 4, l = lane & 15;
   const int i = row0 + r;
   const bool valid = i < A.n;
-  Row<NS> R;
+  Row<NS, F> R;
   R.l = l;
   R.b = A.b;
+  // branch-free loads in two rounds (block indices, then the gathers), so that each round is
+  // in flight at once instead of one dependent round trip per element; out-of-range lanes read
+  // entry 0 / row 0 and discard it
   int colrow[NS];
   float S1[NS];
+  const int ic = valid ? i : 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    int k = l + 16 * s;
-    colrow[s] = (k < A.b) ? A.blk[k] : 0;
-    R.w[s] = (valid && k < A.b) ? A.Wt[(long)colrow[s] * A.ldw + i] : 0.0f;
-    S1[s] = (A.S1 && k < A.b) ? A.S1[k] : 0.0f;
+    const int k = l + 16 * s;
+    colrow[s] = A.blk[k < A.b ? k : 0];
   }
+  float v[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) v[s] = A.Wt[(long)colrow[s] * A.ldw + ic];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = l + 16 * s;
+    S1[s] = A.S1 ? A.S1[k < A.b ? k : 0] : 0.0f;
+    S1[s] = k < A.b ? S1[s] : 0.0f;
+    R.w[s] = (valid && k < A.b) ? v[s] : 0.0f;
+  }
+  const float dv = A.S1 ? *A.d : 0.0f;
   float wsum = row_sum_w(R);
   float a, m;
   bool zero = row_init(R, wsum, &a, &m);
   if (count_zero && valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
   int it = 0;
   if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
-  if (A.S1) row_aga(R, S1, *A.d, &a, &m);
+  if (A.S1) row_aga(R, S1, dv, &a, &m);
   if (A.iters && lane == 0 && !skip_itf) atomicMax(A.iters, it);
   if (!valid) return;
   if (l == 0) {
@@ -210,11 +224,11 @@ PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count
     }
 }
 
-template <int NS>
+template <int NS, bool F>
 __global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
   const int wave = threadIdx.x >> 6;
   const int row0 = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE;
-  block_rows<NS>(A, row0, false, true);
+  block_rows<NS, F>(A, row0, false, true);
 }
 
 // The whole-block T_init == 0 case (quantizer.py:164 breaks at iteration 0 and returns the init
@@ -672,7 +686,10 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
-    hipLaunchKernelGGL(atq_block_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+    if (b == 16 * NS)
+      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid), dim3(256), 0, st, A);
+    else
+      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid), dim3(256), 0, st, A);
     PT2Q_LAUNCH_CHECK();
     if (Hinv && nr > 0) {  // zero-block repair + EF coefficients in one launch
       CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc};

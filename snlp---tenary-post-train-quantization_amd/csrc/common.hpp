@@ -16,12 +16,33 @@
 // clamp(min=1e-8) with torch semantics (NaN propagates): quantizer.py:66,100,125,240.
 PT2Q_DEV float clampmin(float x) { return (x < 1e-8f) ? 1e-8f : x; }
 
+// The value of lane (this lane ^ K), K in {1, 2, 4, 8}, by DPP inside a row of 16 lanes (no
+// trip through the LDS crossbar as ds_bpermute takes): xor 1 / 2 are quad permutations, xor 8 a
+// row rotation by 8, xor 4 two row shifts by 4 into alternate banks of 4 lanes.  All lanes active.
+template <int K>
+PT2Q_DEV float xor_lane(float p) {
+  const int v = __float_as_int(p);
+  int r;
+  if constexpr (K == 1) {
+    r = __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (K == 2) {
+    r = __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (K == 8) {
+    r = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else {
+    static_assert(K == 4, "xor_lane: K in {1, 2, 4, 8}");
+    r = __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0x5, false);  // banks 0, 2: row_shl:4
+    r = __builtin_amdgcn_update_dpp(r, v, 0x114, 0xF, 0xA, false);  // banks 1, 3: row_shr:4
+  }
+  return __int_as_float(r);
+}
+
 // Butterfly over the 16 lanes of a lane group (xor 8,4,2,1): every lane ends with the same sum.
 PT2Q_DEV float bfly16(float p) {
-  p = p + __shfl_xor(p, 8);
-  p = p + __shfl_xor(p, 4);
-  p = p + __shfl_xor(p, 2);
-  p = p + __shfl_xor(p, 1);
+  p = p + xor_lane<8>(p);
+  p = p + xor_lane<4>(p);
+  p = p + xor_lane<2>(p);
+  p = p + xor_lane<1>(p);
   return p;
 }
 
@@ -29,11 +50,7 @@ PT2Q_DEV float bfly16(float p) {
 PT2Q_DEV float bfly64(float p) {
   p = p + __shfl_xor(p, 32);
   p = p + __shfl_xor(p, 16);
-  p = p + __shfl_xor(p, 8);
-  p = p + __shfl_xor(p, 4);
-  p = p + __shfl_xor(p, 2);
-  p = p + __shfl_xor(p, 1);
-  return p;
+  return bfly16(p);
 }
 
 // SUMN partial for one lane t over a logical vector v[0..n): elements {256u + 4t + q} in
