@@ -46,6 +46,7 @@ struct BlockWs {
   int* blk;
   int* counters;
   int* iters;
+  int* iters_part;
   long ldw;
 };
 
@@ -70,6 +71,7 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
   // [2k, 2k+1] ATQ; [2B+2k, 2B+2k+1] top-k/S1 sync; [4B ..) the wbar hand-off counters
   w.counters = c.take<int>((size_t)4 * B + pt2q_ssr_counter_ints(n));
   w.iters = c.take<int>((size_t)B);
+  w.iters_part = c.take<int>((size_t)ceil_div(n, 16));
   return c.ok;
 }
 
@@ -146,7 +148,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
                                     w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
                                     nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
-                                    st, Hinv, ldhi, nrem, nr, w.Ck, m)) != PT2Q_OK)
+                                    st, Hinv, ldhi, nrem, nr, w.Ck, m, w.iters_part)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
     static const char* ef_env = std::getenv("PT2Q_EF_GEMM");  // 0: the generic GEMM
     rc = (nr > 0 && !(ef_env && ef_env[0] == '0'))

@@ -101,17 +101,35 @@ PT2Q_DEV void row_grid(const Row<NS, F>& R, float wsum, float* a, float* m) {
   *m = (t2 * wsum - ts * swt) / den;
 }
 
-// flexible_round, quantizer.py:110-134. Returns true if this lane changed a code.
+// flexible_round, quantizer.py:110-134. Returns true if this lane changed a code.  The quotients
+// come from the reciprocal first (straight-line code); only when some lane of the wave has one
+// near a threshold (round_code's test) does the wave take the correctly rounded divisions.
 template <int NS, bool F>
 PT2Q_DEV bool row_round(Row<NS, F>& R, float a, float m) {
   float as = clampmin(a);
   const float ras = rcp_approx(as);
   const bool rok = rcp_ok(as);
+  float d[NS], q[NS];
+  bool near = !rok;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    d[s] = R.w[s] - m;
+    q[s] = d[s] * ras;
+    const float aq = fabsf(q[s]);
+    near |= R.has(s) && !(fabsf(aq - 0.5f) > aq * 0x1p-20f);
+  }
+  if (__any(near)) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float aq = fabsf(q[s]);
+      if (!rok || !(fabsf(aq - 0.5f) > aq * 0x1p-20f)) q[s] = d[s] / as;
+    }
+  }
   bool changed = false;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (R.has(s)) {
-      float nt = round_code(R.w[s] - m, as, ras, rok);
+      const float nt = (q[s] > 0.5f) ? 1.0f : ((q[s] < -0.5f) ? -1.0f : 0.0f);
       changed |= (nt != R.t[s]);
       R.t[s] = nt;
     }
@@ -169,10 +187,12 @@ struct BlockArgs {
   long lde;
   int* iters;        // 1 int (atomicMax), nullable
   int* counters;     // [0] zero-init rows, [1] workgroups done
+  int* iters_part;   // per-workgroup iteration maxima (reduced by the next launch), nullable
 };
 
+// Returns the wave's ITF iteration count (wave-uniform).
 template <int NS, bool F = false>
-PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_zero) {
+PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_zero) {
   const int lane = threadIdx.x & 63;
   const int r = lane >> 4, l = lane & 15;
   const int i = row0 + r;
@@ -209,8 +229,7 @@ PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count
   int it = 0;
   if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
   if (A.S1) row_aga(R, S1, dv, &a, &m);
-  if (A.iters && lane == 0 && !skip_itf) atomicMax(A.iters, it);
-  if (!valid) return;
+  if (!valid) return it;
   if (l == 0) {
     A.alpha[i] = a;
     A.mu[i] = m;
@@ -222,13 +241,37 @@ PT2Q_DEV void block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count
       A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
       if (A.Et) A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
     }
+  return it;
 }
 
+// Iteration count of a block: one store per workgroup (iters_part), reduced by the post / fixup
+// launch -- not one atomic per wave on a single word (1024 atomics serialise at the memory side
+// and hold the kernel's end for ~10 us).
 template <int NS, bool F>
 __global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
+  __shared__ int wmax[WAVES];
   const int wave = threadIdx.x >> 6;
   const int row0 = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE;
-  block_rows<NS, F>(A, row0, false, true);
+  const int it = block_rows<NS, F>(A, row0, false, true);
+  if (!A.iters) return;
+  if ((threadIdx.x & 63) == 0) wmax[wave] = it;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (A.iters_part) A.iters_part[blockIdx.x] = mx;
+    else atomicMax(A.iters, mx);
+  }
+}
+
+// *iters = max of the block kernel's per-workgroup maxima, or 0 for an all-zero block (ITF did
+// not run: quantizer.py:164).  Workgroup 0, wave 0 of the launch after the block kernel.
+PT2Q_DEV void finish_iters(const BlockArgs& A, int nparts) {
+  if (!A.iters || !A.iters_part || blockIdx.x != 0 || threadIdx.x >= 64) return;
+  int v = 0;
+  for (int j = threadIdx.x; j < nparts; j += 64) v = max(v, A.iters_part[j]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  if (threadIdx.x == 0) *A.iters = (A.counters[0] == A.n) ? 0 : v;
 }
 
 // The whole-block T_init == 0 case (quantizer.py:164 breaks at iteration 0 and returns the init
@@ -236,10 +279,11 @@ __global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
 // redoes every row without ITF.  (A last-arriving-workgroup repair inside atq_block_kernel cost
 // an agent-scope release fence - an L2 write-back - per workgroup.)
 template <int NS>
-__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A) {
+__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A, int nparts) {
+  finish_iters(A, nparts);
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
-  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  if (A.iters && !A.iters_part && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
   block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
 }
 
@@ -257,6 +301,7 @@ struct CoeffArgs {
 
 template <int NS>
 __global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A, CoeffArgs K, int fix_wgs) {
+  finish_iters(A, fix_wgs);
   const long q = (long)blockIdx.x * 256 + threadIdx.x;
   if (q < (long)K.nr * K.bs) {
     const int k = (int)(q / K.nr), e = (int)(q % K.nr);
@@ -266,7 +311,7 @@ __global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A, CoeffArgs K,
   }
   if ((int)blockIdx.x >= fix_wgs || A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
-  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  if (A.iters && !A.iters_part && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
   block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
 }
 
@@ -671,7 +716,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv, long ldh, const int* rem, int nr,
-                          float* C, long ldc) {
+                          float* C, long ldc, int* iters_part) {
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
@@ -682,7 +727,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
     if (Hinv && nr > 0) return pt2q_launch_ef_coeffs(Hinv, ldh, blk, b, rem, nr, C, ldc, st);
     return PT2Q_OK;
   }
-  BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters};
+  BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part};
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
@@ -697,7 +742,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
       hipLaunchKernelGGL(atq_post_kernel<NS>, dim3(cgrid > grid ? cgrid : grid), dim3(256), 0, st, A,
                          K, grid);
     } else {
-      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid), dim3(256), 0, st, A);
+      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid), dim3(256), 0, st, A, grid);
     }
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;

@@ -8,7 +8,8 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv = nullptr, long ldh = 0,
-                          const int* rem = nullptr, int nr = 0, float* C = nullptr, long ldc = 0);
+                          const int* rem = nullptr, int nr = 0, float* C = nullptr, long ldc = 0,
+                          int* iters_part = nullptr);  // ceil(n/16) ints of scratch, nullable
 
 // ---- SSR / selection (ssr.hip)
 // cnt (nullable): pt2q_ssr_counter_ints(n) zeroed ints -> one fused wbar launch (self-resetting)
