@@ -24,7 +24,7 @@ using pt2q_chol::NB;
 // whose producing update did not run the fused factor.
 __global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int p0, int nb,
                                                         int* info) {
-  __shared__ __attribute__((aligned(16))) float urow[2][pt2q_chol::DG][NB];
+  __shared__ __attribute__((aligned(16))) float urow[3][pt2q_chol::DG][NB];
   const float* D = A + (long)p0 * lda + p0;
   pt2q_chol::diag_factor([&](int r, int c) { return D[(long)r * lda + c]; }, A, lda, p0, nb, info, urow);
 }

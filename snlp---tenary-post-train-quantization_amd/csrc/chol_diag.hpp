@@ -8,18 +8,38 @@ namespace pt2q_chol {
 constexpr int NB = 64;
 constexpr int DG = 4;  // rows per barrier
 
-// The diagonal-block factorisation with four waves: wave q keeps rows [16q, 16q+16) of every
-// column in registers (lane c = column c, col[s] = D[16q+s][c]).  Rows are finalised in groups
-// of four (one barrier per group instead of per row): the wave owning the group forms its rows
-// one after another -- U[k][k] = sqrt(D[k][k]) via readlane, U[k][c] = D[k][c]/U[k][k] -- and,
-// before the next row of the group, applies row k's update to the group's later rows itself
-// (U[k][r] by readlane); it publishes the four rows in LDS (entries c <= k as 0).  After the
+// The diagonal-block factorisation with four waves.  Rows are finalised in 16 groups of four
+// (one barrier per group); group g (rows 4g .. 4g+3) belongs to wave g % 4, which keeps them in
+// registers (lane c = column c; slot s of wave q holds row rowof(q, s) = 4(4(s/4) + q) + s%4).
+// The owner forms its group's rows one after another -- U[k][k] = sqrt(D[k][k]) via readlane,
+// U[k][c] = D[k][c]/U[k][k] -- applying each row's term to the group's later rows itself
+// (U[k][r] by readlane), and publishes the four rows in LDS (entries c <= k as 0).  After the
 // barrier every wave applies D[r][c] = fmaf(-U[k][r], U[k][c], D[r][c]) for the four rows in
-// order to its other rows (an fmaf with a zero factor is an exact no-op, so rows <= k and
-// columns <= k are untouched).  Each element thus gets exactly the row updates of the
-// one-row-at-a-time order, k ascending.  Entries below the diagonal are scratch, never written
-// back.  Padding (nb < NB) is an identity block.  load(r, c) gives D[r][c] for r, c < nb;
-// urow: 2 * DG * NB floats of LDS.  Writes U (r <= c < nb) to A at (p0, p0).
+// order to its rows (an fmaf with a zero factor is an exact no-op, so rows <= k and columns
+// <= k are untouched) -- except that the owner of the next group first updates only that group
+// and defers the rest to after the next barrier, so that the chain from one group to the next
+// is one barrier, sixteen fmas and the group itself.  Each element still gets exactly the row
+// updates of the one-row-at-a-time order, k ascending.  Entries below the diagonal are scratch,
+// never written back.  Padding (nb < NB) is an identity block.  load(r, c) gives D[r][c] for
+// r, c < nb; urow: 3 * DG * NB floats of LDS (a group's rows stay readable for two barriers).
+// Writes U (r <= c < nb) to A at (p0, p0).
+PT2Q_DEV int diag_rowof(int q, int s) { return 4 * (4 * (s >> 2) + q) + (s & 3); }
+
+// this wave's slots s in [s_lo, s_hi) (excluding [x_lo, x_hi)) get group ur's four row updates
+PT2Q_DEV void diag_apply(float (&col)[16], const float (*ur)[NB], int q, int c, int s_lo, int s_hi,
+                         int x_lo, int x_hi) {
+#pragma unroll
+  for (int t = 0; t < DG; ++t) {
+    const float ukc = ur[t][c];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool in = s >= s_lo && s < s_hi && !(s >= x_lo && s < x_hi);
+      const float x = fmaf(-ur[t][diag_rowof(q, s)], ukc, col[s]);
+      col[s] = in ? x : col[s];
+    }
+  }
+}
+
 template <class Load>
 PT2Q_DEV void diag_factor(Load load, float* A, long lda, int p0, int nb, int* info,
                           float (*urow)[DG][NB]) {
@@ -27,50 +47,49 @@ PT2Q_DEV void diag_factor(Load load, float* A, long lda, int p0, int nb, int* in
   float col[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    const int r = 16 * q + s;
+    const int r = diag_rowof(q, s);
     const bool in = r < nb && c < nb;
     col[s] = load(in ? r : 0, in ? c : 0);  // branch-free loads
     col[s] = in ? col[s] : ((r == c) ? 1.0f : 0.0f);
   }
-  for (int kq = 0; kq < 4; ++kq) {
+  int pend = -1;  // a group whose updates this wave has so far applied to its next group only
 #pragma unroll
-    for (int kg = 0; kg < 16 / DG; ++kg) {
-      const int ks0 = DG * kg, k0 = 16 * kq + ks0;
-      float(*ur)[NB] = urow[kg & 1];
-      const bool own = q == kq;
-      if (own) {
-#pragma unroll
-        for (int t = 0; t < DG; ++t) {
-          const int ks = ks0 + t, k = k0 + t;
-          const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[ks]), k));
-          if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
-          const float ukk = sqrtf(dkk);
-          col[ks] = (c == k) ? ukk : ((c > k) ? col[ks] / ukk : col[ks]);
-          const float ukc = (c > k) ? col[ks] : 0.0f;
-          ur[t][c] = ukc;
-#pragma unroll
-          for (int t2 = t + 1; t2 < DG; ++t2) {  // row k's term for the group's later rows
-            const float ukr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ukc), k0 + t2));
-            col[ks0 + t2] = fmaf(-ukr, ukc, col[ks0 + t2]);
-          }
-        }
-      }
-      __syncthreads();
+  for (int g = 0; g < 16; ++g) {
+    const int s0 = 4 * (g >> 2), k0 = 4 * g;  // the owner's slots of group g, its first row
+    float(*ur)[NB] = urow[g % 3];
+    if (q == (g & 3)) {
 #pragma unroll
       for (int t = 0; t < DG; ++t) {
-        const float ukc = ur[t][c];
+        const int ks = s0 + t, k = k0 + t;
+        const float dkk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(col[ks]), k));
+        if (c == 0 && k < nb && !(dkk > 0.0f)) atomicCAS(info, 0, p0 + k + 1);
+        const float ukk = sqrtf(dkk);
+        col[ks] = (c == k) ? ukk : ((c > k) ? col[ks] / ukk : col[ks]);
+        const float ukc = (c > k) ? col[ks] : 0.0f;
+        ur[t][c] = ukc;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const bool grp = own && s >= ks0 && s < ks0 + DG;  // done by the owner above
-          const float x = fmaf(-ur[t][16 * q + s], ukc, col[s]);
-          col[s] = grp ? col[s] : x;
+        for (int t2 = t + 1; t2 < DG; ++t2) {  // row k's term for the group's later rows
+          const float ukr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ukc), k0 + t2));
+          col[s0 + t2] = fmaf(-ukr, ukc, col[s0 + t2]);
         }
       }
+    }
+    __syncthreads();
+    if (pend >= 0) {  // the deferred rest of group pend (= g - 1), before group g's updates
+      diag_apply(col, urow[pend % 3], q, c, 0, 16, s0, s0 + 4);
+      pend = -1;
+    }
+    const int gn = g + 1, sn = 4 * (gn >> 2);
+    if (gn < 16 && q == (gn & 3)) {  // the next owner: its next group now, the rest later
+      diag_apply(col, ur, q, c, sn, sn + 4, 0, 0);
+      pend = g;
+    } else {
+      diag_apply(col, ur, q, c, 0, 16, q == (g & 3) ? s0 : 0, q == (g & 3) ? s0 + 4 : 0);
     }
   }
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    const int r = 16 * q + s;
+    const int r = diag_rowof(q, s);
     if (r <= c && c < nb) A[(long)(p0 + r) * lda + p0 + c] = col[s];
   }
 }
