@@ -341,7 +341,7 @@ constexpr int TOPK_HPAD = 257;  // per-wave histogram stride (bank-spread)
 // b picks are then ranked among themselves.  Writes blk (selection order), newrem (ascending,
 // reorder.py:139-141), perm_out (int64, nullable).  With G != nullptr (variant M, b <= 128)
 // the same workgroup then forms S1/d for AGA from the raw Gram over the block it just selected.
-// LDS: region0 (max(r + 16*257, b*(b+1)) words: values + wave histograms, later the S1 gather),
+// LDS: region0 (max(r + 32*257, b*(b+1)) words: values + two banks of wave histograms, later the S1 gather),
 // r flag bytes, scan ints, b picks / their values / block indices / partial sums.
 constexpr int S1_ROWS = TOPK_THREADS / 128;  // S1 rows per helper workgroup
 
@@ -349,20 +349,34 @@ constexpr int S1_ROWS = TOPK_THREADS / 128;  // S1 rows per helper workgroup
 // rows of G[blk][blk] in parallel and sum each in l order; the last one to finish forms d in j
 // order (the s1_block order).  Workgroup 0 is dispatched first and waits on nobody, so the
 // spin cannot deadlock.  sync[0]: pick published; sync[1]: helpers done.
+#ifdef TOPK_STAMPS  // tools/topk_probe.hip: phase timestamps (thread 0 of each workgroup)
+__device__ long long topk_stamps[64][16];
+#define TOPK_STAMP(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 64) topk_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
+#else
+#define TOPK_STAMP(i)
+#endif
+
 PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* S1, float* d,
                         int* sync, float* gb) {
   const int tid = threadIdx.x, nh = gridDim.x - 1;
+  // hand-offs (pick -> helpers, S1 -> the last helper): write-through (sc1) stores drained
+  // before the flag / counter, sc1 loads on the consuming side, no fences
   if (tid == 0) {
     long spins = 0;
     while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
            ++spins < (1l << 26))
       __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
+  TOPK_STAMP(8);
   const int jj = tid >> 7, l = tid & 127;
   const int j = (blockIdx.x - 1) * S1_ROWS + jj;
-  if (j < b && l < b) gb[jj * 129 + l] = G[(long)blk[j] * ldg + blk[l]];
+  if (j < b && l < b) {
+    const int bj = __hip_atomic_load(&blk[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int bl = __hip_atomic_load(&blk[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gb[jj * 129 + l] = G[(long)bj * ldg + bl];
+  }
   __syncthreads();
   if (l == 0 && j < b) {
     const float* row = gb + jj * 129;
@@ -376,18 +390,16 @@ PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* 
       for (int u = 0; u < 8; ++u) s = s + t[u];
     }
     for (; q < b; ++q) s = s + row[q];
-    S1[j] = s;
+    __hip_atomic_store(&S1[j], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    last = atomicAdd(&sync[1], 1) == nh - 1;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
+  TOPK_STAMP(9);
+  if (tid == 0) last = atomicAdd(&sync[1], 1) == nh - 1;
   __syncthreads();
   if (!last) return;
-  if (tid < b) gb[tid] = S1[tid];
+  if (tid < b) gb[tid] = __hip_atomic_load(&S1[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (tid == 0) {
     float dd = 0.0f;
@@ -414,52 +426,73 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
   int* bl = (int*)(pv + b);             // b block indices (selection order)
   float* s1 = (float*)(bl + b);
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6;
+  TOPK_STAMP(0);
   for (int e = tid; e < r; e += nt) vals[e] = orderable(sim[e]);
   uint32_t prefix = 0, pmask = 0;
   int kk = b;  // rank (1-based) of v* among the values matching prefix
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 16 * TOPK_HPAD; i += nt) hist[i] = 0;
-    __syncthreads();
-    int* hw = hist + wv * TOPK_HPAD;
-    for (int e = tid; e < r; e += nt) {
-      const uint32_t u = vals[e];
-      if ((u & pmask) == prefix) atomicAdd(&hw[(u >> shift) & 255], 1);
+  // Two banks of 16 per-wave histograms: a pass counts into one while clearing the other, and
+  // wave 0 merges + scans in one go -- two barriers per pass.  res: the pass results, in two
+  // alternating slots (read after the pass's second barrier, rewritten two passes later).
+  for (int i = tid; i < 32 * TOPK_HPAD; i += nt) hist[i] = 0;
+  __syncthreads();
+  TOPK_STAMP(4);
+  int* res = sc + 70;
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    const int shift = 24 - 8 * p;
+    int* hcur = hist + (p & 1) * 16 * TOPK_HPAD;
+    int* hnext = hist + ((p + 1) & 1) * 16 * TOPK_HPAD;
+    int* hw = hcur + wv * TOPK_HPAD;
+    // similarities crowd into one bin in the high passes: a wave whose active lanes all share
+    // a bin adds once (same-word LDS atomics of 64 lanes would serialise), others per lane
+    for (int base = 0; base < r; base += nt) {
+      const int e = base + tid;
+      const uint32_t u = e < r ? vals[e] : 0u;
+      const bool act = e < r && (u & pmask) == prefix;
+      const int bin = (int)((u >> shift) & 255);
+      const uint64_t am = __ballot(act);
+      if (am) {
+        const int leader = __ffsll((unsigned long long)am) - 1;
+        const int lb = __shfl(bin, leader);
+        const uint64_t same = __ballot(act && bin == lb);
+        if (same == am) {
+          if (lane == leader) atomicAdd(&hw[lb], __popcll(am));
+        } else if (act) {
+          atomicAdd(&hw[bin], 1);
+        }
+      }
     }
-    __syncthreads();
-    int* hm = hist + 16 * TOPK_HPAD;  // merged histogram
-    if (tid < 256) {
-      int t = 0;
-#pragma unroll
-      for (int w = 0; w < TOPK_THREADS / 64; ++w) t += hist[w * TOPK_HPAD + tid];
-      hm[tid] = t;
-    }
+    if (p + 1 < 4)
+      for (int i = tid; i < 16 * TOPK_HPAD; i += nt) hnext[i] = 0;
     __syncthreads();
     if (wv == 0) {  // lane l owns bins 255-4l .. 252-4l (descending)
-      int c[4], s = 0;
+      int c[4] = {0, 0, 0, 0}, s = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        c[q] = hm[255 - 4 * lane - q];
-        s += c[q];
-      }
+      for (int w = 0; w < TOPK_THREADS / 64; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] += hcur[w * TOPK_HPAD + 255 - 4 * lane - q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += c[q];
       const int incl = wave_incl_scan(s);
       int run = incl - s;
       if (run < kk && kk <= incl) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           if (run < kk && kk <= run + c[q]) {
-            sc[70] = 255 - 4 * lane - q;
-            sc[71] = kk - run;
+            res[2 * (p & 1)] = 255 - 4 * lane - q;
+            res[2 * (p & 1) + 1] = kk - run;
           }
           run += c[q];
         }
       }
     }
     __syncthreads();
-    prefix |= (uint32_t)sc[70] << shift;
+    if (p == 0) TOPK_STAMP(5);
+    prefix |= (uint32_t)res[2 * (p & 1)] << shift;
     pmask |= 255u << shift;
-    kk = sc[71];
-    __syncthreads();
+    kk = res[2 * (p & 1) + 1];
   }
+  TOPK_STAMP(1);
   // prefix = v*; the first kk positions holding v* are picked, with every value above it
   const int per = (r + nt - 1) / nt;
   const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
@@ -474,6 +507,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
     cs += s;
     cu += !s;
   }
+  TOPK_STAMP(2);
   // one scan for both compactions (r < 2^16): picks and the unselected remainder, ascending
   const int both = block_excl_scan((cs << 16) | cu, sc, &tot);
   int os = both >> 16, ou = both & 0xFFFF;
@@ -486,33 +520,38 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
     }
   }
   __syncthreads();
-  // rank of pick t: picks above it in (value desc, position asc); picks are position-ascending
-  for (int t = tid; t < b; t += nt) {
-    const uint32_t ut = pv[t];
-    int rank = 0, s = 0;
-    for (; s + 8 <= b; s += 8) {
-      uint32_t us[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) us[u] = pv[s + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) rank += (us[u] > ut) | ((us[u] == ut) & (s + u < t));
+  TOPK_STAMP(3);
+  // rank of pick t: picks above it in (value desc, position asc); picks are position-ascending.
+  // Eight threads per pick, each over every eighth other pick, then summed across the eight.
+  for (int t0 = 0; t0 < b; t0 += nt / 8) {
+    const int t = t0 + tid / 8, sub = tid & 7;
+    int rank = 0;
+    if (t < b) {
+      const uint32_t ut = pv[t];
+      for (int s = sub; s < b; s += 8) {
+        const uint32_t us = pv[s];
+        rank += (us > ut) | ((us == ut) & (s < t));
+      }
     }
-    for (; s < b; ++s) rank += (pv[s] > ut) | ((pv[s] == ut) & (s < t));
-    const int j = rem[pick[t]];
-    blk[rank] = j;
-    if (perm_out) perm_out[rank] = j;
+    rank += __shfl_xor(rank, 4);
+    rank += __shfl_xor(rank, 2);
+    rank += __shfl_xor(rank, 1);
+    if (t < b && sub == 0) {
+      const int j = rem[pick[t]];
+      __hip_atomic_store(&blk[rank], j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: helpers read it
+      if (perm_out) perm_out[rank] = j;
+    }
   }
   (void)lane;
   (void)bl;
   (void)s1;
-  if (G) {  // publish the pick to the S1 helpers
+  TOPK_STAMP(6);
+  if (G) {  // publish the pick to the S1 helpers (every storing wave drained first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __hip_atomic_store(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) __hip_atomic_store(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  TOPK_STAMP(7);
 }
 
 // Sequential block (use_ssr=False: main.py:167-169, gptq.py:135-137) or "take the rest"
@@ -742,7 +781,7 @@ int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* bl
   if (G && b > 128) return PT2Q_E_ARG;
   if (b <= 0 || b > r || r >= 65536) return PT2Q_E_UNSUPPORTED;
   if (G && !sync) return PT2Q_E_ARG;  // sync: 2 ints the caller zeroed before this launch
-  const int region0 = (r + 17 * TOPK_HPAD + 3) & ~3;  // >= S1_ROWS * 129 for the helpers
+  const int region0 = (r + 32 * TOPK_HPAD + 3) & ~3;  // >= S1_ROWS * 129 for the helpers
   const size_t lds = (size_t)region0 * 4 + (size_t)((r + 15) & ~15) + 80 * sizeof(int) +
                      (size_t)b * 4 * sizeof(int);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
