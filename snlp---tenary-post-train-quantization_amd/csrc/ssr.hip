@@ -11,6 +11,8 @@
 
 namespace {
 
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
 constexpr int CHUNK = 128;  // canonical wbar chunk (rem entries per partial sum)
 
 // part[c][i] = sum over rem[c*128 .. c*128+127] (ascending) of Wt[rem[e]][i]
@@ -53,19 +55,23 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   const int e0 = c * CHUNK, ce = min(r, e0 + CHUNK) - e0;
   for (int e = threadIdx.x; e < ce; e += blockDim.x) rows[e] = (long)rem[e0 + e] * ldw;
   __syncthreads();
-  const int i = blockIdx.y * 256 + threadIdx.x;
+  // four consecutive rows i per thread (float4; n % 4 == 0), each its own chain over e
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(part, 0, nchunks * n * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(wn, 0, n * 4, 0x00020000);
+  const int i = (blockIdx.y * 256 + threadIdx.x) * 4;
   if (i < n) {
-    float p = 0.0f;
+    f4 p = {0.0f, 0.0f, 0.0f, 0.0f};
     int e = 0;
     for (; e + 8 <= ce; e += 8) {
-      float v[8];
+      f4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = Wt[rows[e + u] + i];
+      for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(Wt + rows[e + u] + i);
 #pragma unroll
       for (int u = 0; u < 8; ++u) p = p + v[u];
     }
-    for (; e < ce; ++e) p = p + Wt[rows[e] + i];
-    __hip_atomic_store(part + (long)c * n + i, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (; e < ce; ++e) p = p + *(const f4*)(Wt + rows[e] + i);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, p), rp, (c * n + i) * 4, 0, 16);  // sc1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -73,19 +79,18 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   __syncthreads();
   if (!last) return;
   if (i < n) {
-    float t = 0.0f;
+    f4 t = {0.0f, 0.0f, 0.0f, 0.0f};
     int k = 0;
     for (; k + 8 <= nchunks; k += 8) {
-      float v[8];
+      f4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        v[u] = __hip_atomic_load(part + (long)(k + u) * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rp, ((k + u) * n + i) * 4, 0, 16));
 #pragma unroll
       for (int u = 0; u < 8; ++u) t = t + v[u];
     }
-    for (; k < nchunks; ++k)
-      t = t + __hip_atomic_load(part + (long)k * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(wn + i, t / (float)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (; k < nchunks; ++k) t = t + __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rp, (k * n + i) * 4, 0, 16));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, t / (float)r), rw, i * 4, 0, 16);  // sc1
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -97,8 +102,7 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   if (!last) return;
   if (threadIdx.x >= 64) return;
   // wave 0: lane t holds elements {256u + 4t + q} (sumn_lane's order) in registers
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(wn, 0, n * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = rw;
   const int t = threadIdx.x;
   f4 v[16];
 #pragma unroll
@@ -750,8 +754,8 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
   static const char* fuse_env = std::getenv("PT2Q_WBAR_FUSED");  // 0: three launches
-  if (cnt && n <= 4096 && n % 4 == 0 && !(fuse_env && fuse_env[0] == '0')) {
-    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st, Wt, ldw,
+  if (cnt && n <= 4096 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && !(fuse_env && fuse_env[0] == '0')) {
+    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 1024)), dim3(256), 0, st, Wt, ldw,
                        n, rem, r, part, wn, cnt);
     PT2Q_LAUNCH_CHECK();
   } else {
