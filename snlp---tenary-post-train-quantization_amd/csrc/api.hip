@@ -119,8 +119,11 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     const int nr = r - bs;
     int* rem = w.rem[cur];
     int* nrem = w.rem[cur ^ 1];
-    // variant M with blocks <= 128: the top-k workgroup also forms S1/d (no separate launch)
-    const bool s1_in_topk = ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
+    // variant M with blocks <= 128: the ATQ launch also forms S1/d (no separate launch; off
+    // the critical path of the rows, which need it only for their AGA)
+    static const char* s1_env = std::getenv("PT2Q_S1_IN_ATQ");  // 0: in the top-k launch
+    const bool s1_in_atq = aga == PT2Q_AGA_ACT && bs <= 128 && !(s1_env && s1_env[0] == '0');
+    const bool s1_in_topk = !s1_in_atq && ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
     if (ssr) {
       if (r > b) {
         if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B)) !=
@@ -140,7 +143,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     }
     const float* S1 = nullptr;
     if (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_HESS) {
-      if (!s1_in_topk &&
+      if (!s1_in_topk && !s1_in_atq &&
           (rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK)
         return rc;
       S1 = w.S1;
@@ -148,7 +151,9 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
                                     w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
                                     nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
-                                    st, Hinv, ldhi, nrem, nr, w.Ck, m, w.iters_part)) != PT2Q_OK)
+                                    st, Hinv, ldhi, nrem, nr, w.Ck, m, w.iters_part,
+                                    s1_in_atq ? A : nullptr, lda,
+                                    s1_in_atq ? w.counters + 2 * B + 2 * k : nullptr)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
     static const char* ef_env = std::getenv("PT2Q_EF_GEMM");  // 0: the generic GEMM
     rc = (nr > 0 && !(ef_env && ef_env[0] == '0'))

@@ -188,6 +188,15 @@ struct BlockArgs {
   int* iters;        // 1 int (atomicMax), nullable
   int* counters;     // [0] zero-init rows, [1] workgroups done
   int* iters_part;   // per-workgroup iteration maxima (reduced by the next launch), nullable
+  // S1/d formed inside the launch (variant M, b <= 128): nS1 leading workgroups gather
+  // S1 = G[blk][blk]·1 and d into S1w / dw and raise s1sync[0]; the row workgroups wait for it
+  // only before their AGA.  nS1 = 0: S1 / d come ready from an earlier launch.
+  const float* G;
+  long ldg;
+  int nS1;
+  int* s1sync;       // [0] ready flag, [1] S1 workgroups done (zero before the launch)
+  float* S1w;
+  float* dw;
 };
 
 // Returns the wave's ITF iteration count (wave-uniform).
@@ -214,20 +223,37 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   float v[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) v[s] = A.Wt[(long)colrow[s] * A.ldw + ic];
+  const bool s1_now = A.S1 && A.nS1 == 0;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int k = l + 16 * s;
-    S1[s] = A.S1 ? A.S1[k < A.b ? k : 0] : 0.0f;
+    S1[s] = s1_now ? A.S1[k < A.b ? k : 0] : 0.0f;
     S1[s] = k < A.b ? S1[s] : 0.0f;
     R.w[s] = (valid && k < A.b) ? v[s] : 0.0f;
   }
-  const float dv = A.S1 ? *A.d : 0.0f;
+  float dv = s1_now ? *A.d : 0.0f;
   float wsum = row_sum_w(R);
   float a, m;
   bool zero = row_init(R, wsum, &a, &m);
   if (count_zero && valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
   int it = 0;
   if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
+  if (A.S1 && A.nS1 > 0) {  // S1 / d from this launch's leading workgroups (write-through)
+    if ((threadIdx.x & 63) == 0) {
+      long spins = 0;
+      while (__hip_atomic_load(&A.s1sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+             ++spins < (1l << 26))
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int k = l + 16 * s;
+      const float x = __hip_atomic_load(&A.S1w[k < A.b ? k : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S1[s] = k < A.b ? x : 0.0f;
+    }
+    dv = __hip_atomic_load(A.dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (A.S1) row_aga(R, S1, dv, &a, &m);
   if (!valid) return it;
   if (l == 0) {
@@ -247,18 +273,72 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
 // Iteration count of a block: one store per workgroup (iters_part), reduced by the post / fixup
 // launch -- not one atomic per wave on a single word (1024 atomics serialise at the memory side
 // and hold the kernel's end for ~10 us).
+// S1[j] = l-ascending sum of G[blk_j][blk_l], d = j-ascending sum of S1 (the s1_block order):
+// 8 rows j per workgroup gathered into LDS, one lane sums each; the last S1 workgroup forms d
+// and raises the flag.  Write-through stores drained before the counter / flag, sc1 loads.
+// (Measured slower: rows forming d themselves with no last-workgroup stage; one workgroup for
+// all of S1 -- its per-lane serial sums take longer than the hand-off they save.)
+PT2Q_DEV float s1_serial_sum(const float* v, int b) {  // ((v0 + v1) + v2) ..., loads batched
+  float s = 0.0f;
+  int q = 0;
+  for (; q + 8 <= b; q += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = v[q + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = s + t[u];
+  }
+  for (; q < b; ++q) s = s + v[q];
+  return s;
+}
+
+PT2Q_DEV void atq_s1_part(const BlockArgs& A) {
+  __shared__ float gb[8][129];
+  __shared__ int last;
+  const int tid = threadIdx.x, jj = tid >> 5, ln = tid & 31;
+  const int j = blockIdx.x * 8 + jj;
+  if (j < A.b) {
+    const long bj = (long)A.blk[j] * A.ldg;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int l = ln + 32 * u;
+      if (l < A.b) gb[jj][l] = A.G[bj + A.blk[l]];
+    }
+  }
+  __syncthreads();
+  if (ln == 0 && j < A.b)
+    __hip_atomic_store(&A.S1w[j], s1_serial_sum(gb[jj], A.b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&A.s1sync[1], 1) == A.nS1 - 1;
+  __syncthreads();
+  if (!last) return;
+  if (tid < A.b) gb[0][tid] = __hip_atomic_load(&A.S1w[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(A.dw, s1_serial_sum(gb[0], A.b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&A.s1sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int NS, bool F>
 __global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
+  if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
+    atq_s1_part(A);
+    return;
+  }
   __shared__ int wmax[WAVES];
   const int wave = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE;
+  const int rb = (int)blockIdx.x - A.nS1;
+  const int row0 = rb * ROWS_PER_WG + wave * ROWS_PER_WAVE;
   const int it = block_rows<NS, F>(A, row0, false, true);
   if (!A.iters) return;
   if ((threadIdx.x & 63) == 0) wmax[wave] = it;
   __syncthreads();
   if (threadIdx.x == 0) {
     const int mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-    if (A.iters_part) A.iters_part[blockIdx.x] = mx;
+    if (A.iters_part) A.iters_part[rb] = mx;
     else atomicMax(A.iters, mx);
   }
 }
@@ -716,7 +796,8 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv, long ldh, const int* rem, int nr,
-                          float* C, long ldc, int* iters_part) {
+                          float* C, long ldc, int* iters_part, const float* G, long ldg,
+                          int* s1sync) {
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
@@ -727,14 +808,16 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
     if (Hinv && nr > 0) return pt2q_launch_ef_coeffs(Hinv, ldh, blk, b, rem, nr, C, ldc, st);
     return PT2Q_OK;
   }
-  BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part};
+  const int nS1 = (G && S1 && s1sync && b <= 128) ? ceil_div(b, 8) : 0;
+  BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part,
+              G, ldg, nS1, s1sync, (float*)S1, (float*)d};
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
     if (b == 16 * NS)
-      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid + nS1), dim3(256), 0, st, A);
     else
-      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid + nS1), dim3(256), 0, st, A);
     PT2Q_LAUNCH_CHECK();
     if (Hinv && nr > 0) {  // zero-block repair + EF coefficients in one launch
       CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc};
