@@ -70,12 +70,10 @@ PT2Q_DEV void load_diag_block(float (*Dus)[NB + 4], float* dg, const float* A, l
 // Panel rows [p0, p0+nb) for columns i >= p0+nb: forward substitution against the factored
 // diagonal block, continuing each element's chain from the already-updated A value.  Four
 // lanes share a column (16 rows each); the lane owning row k divides and broadcasts x_k.
-PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
-                         float (*Dus)[NB + 4], float* dg) {
+PT2Q_DEV void chol_panel_load(const float* A, long lda, int p0, int nb, int m, int bid, float (&x)[SEG]) {
   const int i = p0 + nb + (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
   const int sub = threadIdx.x & (LPR - 1);
   const bool valid = i < m;
-  float x[SEG];
 #pragma unroll
   for (int s = 0; s < SEG; ++s) {
     int k = sub * SEG + s;
@@ -83,14 +81,34 @@ PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
     x[s] = A[in ? (long)(p0 + k) * lda + i : (long)p0 * lda + p0];  // branch-free loads
     x[s] = in ? x[s] : 0.0f;
   }
+}
+
+PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
+                         float (*Dus)[NB + 4], float* dg, float (&x)[SEG]) {
+  const int i = p0 + nb + (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
+  const int sub = threadIdx.x & (LPR - 1);
+  const bool valid = i < m;
+  // row k+1 of the diagonal block and dg[k+1] are read during step k (software pipeline: the
+  // LDS latency stays off the divide -> broadcast -> fma chain)
+  float cur[SEG], nxt[SEG];
+  float dcur = dg[0], dnxt = 0.0f;
+#pragma unroll
+  for (int s = 0; s < SEG; ++s) cur[s] = Dus[0][sub * SEG + s];
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int owner = k / SEG, ks = k % SEG;
-    const float xk = quad_bcast(x[ks] / dg[k], owner);
-    x[ks] = (sub == owner) ? xk : x[ks];
-    const float* row = &Dus[k][sub * SEG];
+    if (k + 1 < NB) {
 #pragma unroll
-    for (int s = 0; s < SEG; ++s) x[s] = fmaf(-row[s], xk, x[s]);
+      for (int s = 0; s < SEG; ++s) nxt[s] = Dus[k + 1][sub * SEG + s];
+      dnxt = dg[k + 1];
+    }
+    const float xk = quad_bcast(x[ks] / dcur, owner);
+    x[ks] = (sub == owner) ? xk : x[ks];
+#pragma unroll
+    for (int s = 0; s < SEG; ++s) x[s] = fmaf(-cur[s], xk, x[s]);
+#pragma unroll
+    for (int s = 0; s < SEG; ++s) cur[s] = nxt[s];
+    dcur = dnxt;
   }
   if (!valid) return;
 #pragma unroll
@@ -104,12 +122,10 @@ PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
 // Ui[k][c0..] holds the running chains for k < c0 (zero otherwise).  Four lanes share a row.
 // For rows inside the block, columns left of the diagonal start at zero and only ever receive
 // zero terms, so they need no mask until the final store.
-PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float (*Dus)[NB + 4],
-                            float* dg) {
+PT2Q_DEV void trtri_load(const float* Ui, long ldi, int c0, int nb, int bid, float (&acc)[SEG]) {
   const int k = (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
   const int sub = threadIdx.x & (LPR - 1);
   const bool valid = k < c0 + nb;
-  float acc[SEG];
 #pragma unroll
   for (int s = 0; s < SEG; ++s) {
     int q = sub * SEG + s;
@@ -117,16 +133,34 @@ PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float 
     acc[s] = Ui[in ? (long)k * ldi + c0 + q : 0];  // branch-free loads
     acc[s] = in ? acc[s] : 0.0f;
   }
+}
+
+PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float (*Dus)[NB + 4],
+                            float* dg, float (&acc)[SEG]) {
+  const int k = (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
+  const int sub = threadIdx.x & (LPR - 1);
+  const bool valid = k < c0 + nb;
   const int jb = (k > c0) ? k - c0 : 0;  // first in-block j (local)
+  float cur[SEG], nxt[SEG];  // software-pipelined rows, as in chol_panel
+  float dcur = dg[0], dnxt = 0.0f;
+#pragma unroll
+  for (int s = 0; s < SEG; ++s) cur[s] = Dus[0][sub * SEG + s];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int owner = j / SEG, js = j % SEG;
-    const float mine = (c0 + j == k) ? 1.0f / dg[j] : -acc[js] / dg[j];
+    if (j + 1 < NB) {
+#pragma unroll
+      for (int s = 0; s < SEG; ++s) nxt[s] = Dus[j + 1][sub * SEG + s];
+      dnxt = dg[j + 1];
+    }
+    const float mine = (c0 + j == k) ? 1.0f / dcur : -acc[js] / dcur;
     const float xj = quad_bcast(mine, owner);
     acc[js] = (sub == owner) ? xj : acc[js];
-    const float* row = &Dus[j][sub * SEG];
 #pragma unroll
-    for (int s = 0; s < SEG; ++s) acc[s] = fmaf(xj, row[s], acc[s]);
+    for (int s = 0; s < SEG; ++s) acc[s] = fmaf(xj, cur[s], acc[s]);
+#pragma unroll
+    for (int s = 0; s < SEG; ++s) cur[s] = nxt[s];
+    dcur = dnxt;
   }
   if (!valid) return;
 #pragma unroll
@@ -143,12 +177,18 @@ __global__ __launch_bounds__(256) void chol_panel_trtri_kernel(float* U, long ld
                                                                int m, float* Ui, int npanel) {
   __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
   __shared__ float dg[NB];
+  const bool panel = (int)blockIdx.x < npanel;
+  float x[SEG];  // this thread's chains, loaded together with the diagonal block
+  if (panel)
+    chol_panel_load(U, ld, p0, nb, m, blockIdx.x, x);
+  else
+    trtri_load(Ui, ld, p0, nb, blockIdx.x - npanel, x);
   load_diag_block(Dus, dg, U, ld, p0, nb);
   __syncthreads();
-  if ((int)blockIdx.x < npanel)
-    chol_panel(U, ld, p0, nb, m, blockIdx.x, Dus, dg);
+  if (panel)
+    chol_panel(U, ld, p0, nb, m, blockIdx.x, Dus, dg, x);
   else
-    trtri_inblock(Ui, ld, p0, nb, blockIdx.x - npanel, Dus, dg);
+    trtri_inblock(Ui, ld, p0, nb, blockIdx.x - npanel, Dus, dg, x);
 }
 
 __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m) {
