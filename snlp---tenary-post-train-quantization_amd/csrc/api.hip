@@ -296,12 +296,15 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
   if ((rc = pt2q_gram(X, xdtype, N, m, ldx, G, m, 0, gflags,
                      pt2q_gram_flags_ints(m) * sizeof(int), stream)) != PT2Q_OK)
     return rc;
-  if ((rc = pt2q_launch_prepare_hessian(G, m, m, N, percdamp, H, m, damp, st)) != PT2Q_OK) return rc;
-  // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G).
+  // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G), so
+  // it is written in that form at once (strictly lower part zero; no separate copy pass).
   // Hinv only feeds the error feedback; a single block (per-channel, b >= m) has none, so the
   // factorisation would be dead work: skip it and report success.
+  const bool upper = b < m && m <= SUMN_LDS_MAX;
+  if ((rc = pt2q_launch_prepare_hessian(G, m, m, N, percdamp, H, m, damp, st, upper)) != PT2Q_OK) return rc;
   if (b < m) {
-    if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st)) != PT2Q_OK) return rc;
+    if ((rc = pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st, upper)) != PT2Q_OK)
+      return rc;
   } else if (hipMemsetAsync(info_dev, 0, sizeof(int), st) != hipSuccess) {
     return PT2Q_E_HIP;
   }

@@ -236,13 +236,15 @@ GemmDesc trtri_desc(const float* U, float* Ui, long ld, int c0, int nb, int rest
 // Uinv = U^-1 is built right-looking by column blocks as soon as rows of block J are final, so
 // no second stream (and no cross-queue dependency in a captured graph) is needed.
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
-                                 float* U, float* Ui, int* info, hipStream_t st) {
+                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form) {
   const long ld = m;  // U and Ui are packed m x m
   if (hipMemsetAsync(info, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
   if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
-  hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
-                     U, ld, m);
-  PT2Q_LAUNCH_CHECK();
+  if (!(h_upper_form && H == U && ldh == ld)) {  // (else H already is the upper work matrix)
+    hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
+                       U, ld, m);
+    PT2Q_LAUNCH_CHECK();
+  }
   int rc;
   // panel solve + in-block inverse of the block at p0 (its diagonal factor done: `factored`)
   auto factor = [&](int p0, int nb, bool factored) -> int {

@@ -75,8 +75,8 @@ int pt2q_launch_transpose_i8(const int8_t* src, long lds, int rows, int cols, vo
 int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, float* dst, long ldd,
                               hipStream_t st);
 int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
-                                float* H, long ldh, float* damp, hipStream_t st);
+                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only = false);
 
 // ---- Cholesky (chol.hip)
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
-                                 float* U, float* Ui, int* info, hipStream_t st);
+                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form = false);

@@ -63,6 +63,35 @@ __global__ __launch_bounds__(1024) void hess_damp_kernel(float* H, long ldh, int
   for (int i = threadIdx.x; i < m; i += blockDim.x) H[(long)i * ldh + i] = H[(long)i * ldh + i] + dmp;
 }
 
+// damp from the diagonal alone: h_ii = G_ii / fn (hess_scale's rounding), then the same SUMN
+// and scaling as hess_damp_kernel.  *damp_dev feeds hess_fill_kernel (and the caller).
+__global__ __launch_bounds__(1024) void hess_diag_damp_kernel(const float* G, long ldg, int m, float fn,
+                                                              float percdamp, float* damp_dev) {
+  __shared__ float tot;
+  __shared__ float stage[SUMN_LDS_MAX];
+  for (int i = threadIdx.x; i < m; i += blockDim.x) stage[i] = G[(long)i * ldg + i] / fn;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float p = sumn_lane<false>(stage, m, 1, threadIdx.x);
+    p = bfly64(p);
+    if (threadIdx.x == 0) tot = percdamp * (p / (float)m);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *damp_dev = tot;
+}
+
+// H = G / fn with damp on the diagonal (hess_scale + hess_damp in one pass); upper_only: the
+// strictly lower part is written as zero (H then is the Cholesky work matrix as is).
+__global__ void hess_fill_kernel(const float* G, long ldg, int m, float fn, const float* damp_dev,
+                                 float* H, long ldh, int upper_only) {
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long)m * m) return;
+  int r = (int)(q / m), c = (int)(q % m);
+  float h = G[(long)r * ldg + c] / fn;
+  if (r == c) h = h + *damp_dev;
+  H[(long)r * ldh + c] = (upper_only && c < r) ? 0.0f : h;
+}
+
 // gptq.py:213-228: out[:, perm[k*b + t]] = alpha[:,k] * T[:, col] + mu[:,k]
 template <typename TT>
 __global__ void dequant_kernel(const float* alpha, const float* mu, const TT* T,
@@ -163,7 +192,17 @@ int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, fl
 }
 
 int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
-                                float* H, long ldh, float* damp, hipStream_t st) {
+                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only) {
+  if (damp && m <= SUMN_LDS_MAX) {  // damp from the diagonal, then one pass over G
+    hipLaunchKernelGGL(hess_diag_damp_kernel, dim3(1), dim3(1024), 0, st, G, ldg, m, (float)nsamples,
+                       percdamp, damp);
+    PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(hess_fill_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg, m,
+                       (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
+  if (upper_only) return PT2Q_E_UNSUPPORTED;
   hipLaunchKernelGGL(hess_scale_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg,
                      m, (float)nsamples, H, ldh);
   PT2Q_LAUNCH_CHECK();
