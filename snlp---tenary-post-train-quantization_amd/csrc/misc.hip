@@ -92,6 +92,26 @@ __global__ void hess_fill_kernel(const float* G, long ldg, int m, float fn, cons
   H[(long)r * ldh + c] = (upper_only && c < r) ? 0.0f : h;
 }
 
+// hess_fill_kernel four columns per thread (m, ldg, ldh multiples of 4, 16-byte aligned)
+__global__ void hess_fill4_kernel(const float* G, long ldg, int m, float fn, const float* damp_dev,
+                                  float* H, long ldh, int upper_only) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int m4 = m / 4;
+  if (q >= (long)m * m4) return;
+  const int r = (int)(q / m4), c0 = 4 * (int)(q % m4);
+  const f4 g = *(const f4*)(G + (long)r * ldg + c0);
+  const float dmp = *damp_dev;
+  f4 h;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float x = g[u] / fn;
+    if (r == c0 + u) x = x + dmp;
+    h[u] = (upper_only && c0 + u < r) ? 0.0f : x;
+  }
+  *(f4*)(H + (long)r * ldh + c0) = h;
+}
+
 // gptq.py:213-228: out[:, perm[k*b + t]] = alpha[:,k] * T[:, col] + mu[:,k]
 template <typename TT>
 __global__ void dequant_kernel(const float* alpha, const float* mu, const TT* T,
@@ -197,8 +217,12 @@ int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, 
     hipLaunchKernelGGL(hess_diag_damp_kernel, dim3(1), dim3(1024), 0, st, G, ldg, m, (float)nsamples,
                        percdamp, damp);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(hess_fill_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg, m,
-                       (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
+    if (m % 4 == 0 && ldg % 4 == 0 && ldh % 4 == 0 && (uintptr_t)G % 16 == 0 && (uintptr_t)H % 16 == 0)
+      hipLaunchKernelGGL(hess_fill4_kernel, dim3(ceil_div((long)m * (m / 4), 256)), dim3(256), 0, st, G,
+                         ldg, m, (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
+    else
+      hipLaunchKernelGGL(hess_fill_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg, m,
+                         (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }
