@@ -33,6 +33,33 @@ __global__ __launch_bounds__(256) void transpose_kernel(const TS* src, long lds,
   }
 }
 
+// 16-bit src -> f32 dst transpose through a 64 x 64 LDS tile: 16-byte loads (8 elements) and
+// 16-byte stores (4 rows of one column).  Requires cols % 8 == 0, rows % 4 == 0, lds % 8 == 0,
+// ldd % 4 == 0 and 16-byte aligned bases; ragged tile edges are masked.
+template <typename TS>
+__global__ __launch_bounds__(256) void transpose16_kernel(const TS* src, long lds, int rows, int cols,
+                                                          float* dst, long ldd) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tid = threadIdx.x;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = p * 32 + tid / 8, c = (tid % 8) * 8;
+    const bool in = r0 + r < rows && c0 + c < cols;
+    uint4 v = in ? *(const uint4*)(src + (long)(r0 + r) * lds + c0 + c) : uint4{0, 0, 0, 0};
+    const TS* e = (const TS*)&v;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) tile[r][c + u] = ld_f32<TS>(e + u);
+  }
+  __syncthreads();
+  typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int idx = p * 256 + tid, c = idx / 16, r = (idx % 16) * 4;
+    if (c0 + c < cols && r0 + r < rows)
+      *(f4*)(dst + (long)(c0 + c) * ldd + r0 + r) = f4{tile[r][c], tile[r + 1][c], tile[r + 2][c], tile[r + 3][c]};
+  }
+}
+
 __global__ void hess_scale_kernel(const float* G, long ldg, int m, float fn, float* H, long ldh) {
   long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (long)m * m) return;
@@ -170,6 +197,18 @@ __global__ void fill_kernel(float* out, long count, uint64_t base, float scale, 
 
 int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,
                                  float* dst, long ldd, hipStream_t st) {
+  if ((dtype == PT2Q_F16 || dtype == PT2Q_BF16) && cols % 8 == 0 && rows % 4 == 0 && lds % 8 == 0 &&
+      ldd % 4 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0) {
+    dim3 g64(ceil_div(cols, 64), ceil_div(rows, 64));
+    if (dtype == PT2Q_F16)
+      hipLaunchKernelGGL(transpose16_kernel<_Float16>, g64, dim3(256), 0, st, (const _Float16*)src, lds,
+                         rows, cols, dst, ldd);
+    else
+      hipLaunchKernelGGL(transpose16_kernel<uint16_t>, g64, dim3(256), 0, st, (const uint16_t*)src, lds,
+                         rows, cols, dst, ldd);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   dim3 grid(ceil_div(cols, 32), ceil_div(rows, 32));
   switch (dtype) {
     case PT2Q_F32:
