@@ -60,6 +60,31 @@ __global__ __launch_bounds__(256) void transpose16_kernel(const TS* src, long ld
   }
 }
 
+// int8 transpose through a 64 x 64 LDS tile: one 16-byte load and one 16-byte store per thread.
+// Requires rows, cols, lds, ldd multiples of 16 and 16-byte aligned bases.
+__global__ __launch_bounds__(256) void transpose_i8x16_kernel(const int8_t* src, long lds, int rows,
+                                                              int cols, int8_t* dst, long ldd) {
+  __shared__ int8_t tile[64][64 + 4];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tid = threadIdx.x;
+  {
+    const int r = tid / 4, c = (tid % 4) * 16;
+    const bool in = r0 + r < rows && c0 + c < cols;
+    const uint4 v = in ? *(const uint4*)(src + (long)(r0 + r) * lds + c0 + c) : uint4{0, 0, 0, 0};
+    const int8_t* e = (const int8_t*)&v;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) tile[r][c + u] = e[u];
+  }
+  __syncthreads();
+  const int c = tid / 4, r = (tid % 4) * 16;
+  if (c0 + c < cols && r0 + r < rows) {
+    uint4 v;
+    int8_t* e = (int8_t*)&v;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) e[u] = tile[r + u][c];
+    *(uint4*)(dst + (long)(c0 + c) * ldd + r0 + r) = v;
+  }
+}
+
 __global__ void hess_scale_kernel(const float* G, long ldg, int m, float fn, float* H, long ldh) {
   long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (long)m * m) return;
@@ -233,7 +258,11 @@ int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows,
 int pt2q_launch_transpose_i8(const int8_t* src, long lds, int rows, int cols, void* dst,
                              int ddtype, long ldd, hipStream_t st) {
   dim3 grid(ceil_div(cols, 32), ceil_div(rows, 32));
-  if (ddtype == PT2Q_I8)
+  if (ddtype == PT2Q_I8 && rows % 16 == 0 && cols % 16 == 0 && lds % 16 == 0 && ldd % 16 == 0 &&
+      (uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0)
+    hipLaunchKernelGGL(transpose_i8x16_kernel, dim3(ceil_div(cols, 64), ceil_div(rows, 64)), dim3(256), 0,
+                       st, src, lds, rows, cols, (int8_t*)dst, ldd);
+  else if (ddtype == PT2Q_I8)
     hipLaunchKernelGGL((transpose_kernel<int8_t, int8_t>), grid, dim3(256), 0, st, src, lds, rows,
                        cols, (int8_t*)dst, ldd);
   else if (ddtype == PT2Q_F32)

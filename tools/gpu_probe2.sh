@@ -1,1 +1,3 @@
-for i in 1 2; do for b in gram16_probe gram16_probe_old; do echo -n "$b "; timeout -k 10 120 tools/$b.bin 262144 4096 5 | head -1; done; done
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+for t in 6 1; do PT2Q_GEMM_TILE=$t timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/lauum$t -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-n2048 > /dev/null 2>&1 || exit 1; done
