@@ -13,7 +13,8 @@
  *     (no host synchronisation, no allocation), so a caller may capture it into a hipGraph.
  *   - Matrices are row-major with explicit leading dimensions (in elements).
  *   - Return value: PT2Q_OK or an error code; launch-time argument errors only.  Numerical
- *     status discovered on the device (Cholesky breakdown) is written to `info_dev`.
+ *     status discovered on the device (Cholesky breakdown) is written to `info_dev`; a stalled
+ *     cross-workgroup wait is written to the workspace status word (PT2Q_E_STALL).
  *   - Arithmetic follows the PT2Q contract: results are bit-identical to the CPU
  *     oracle (oracle/pt2q_oracle.c) for every input.
  */
@@ -34,6 +35,15 @@ extern "C" {
 #define PT2Q_E_UNSUPPORTED 3
 #define PT2Q_E_HIP 4
 #define PT2Q_E_WORKSPACE 5
+#define PT2Q_E_STALL 6     /* reported through the workspace status word (below), not returned */
+
+/* Status word.  pt2q_gram (with a workspace), pt2q_quantize_layer, pt2q_quantize_blocks and
+ * pt2q_ssr_select reserve the FIRST PT2Q_STATUS_BYTES of their workspace for an int status word,
+ * zeroed on the call's stream.  Kernels that wait on another workgroup's hand-off (stream-K
+ * Gram partials, the in-launch S1/d and top-k hand-offs) give up after a bounded number of polls
+ * (seconds) and then set a non-zero bit there instead of continuing silently: after the stream
+ * completes, a non-zero word means the outputs are invalid (PT2Q_E_STALL). */
+#define PT2Q_STATUS_BYTES 256
 
 /* element types */
 #define PT2Q_F32 0

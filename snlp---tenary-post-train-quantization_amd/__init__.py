@@ -18,9 +18,9 @@ from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_
                           quantize_decoder_layer)
 from .ternary import (TernaryLinear, load_quantized_model, replace_linear_with_ternary,
                       save_quantized_model)
-from .engine import (LayerGraph, LayerOutput, LayerWorkspace, cholesky_inverse, dequantize, fill_synthetic,
-                     gram, hessian_inverse, pack_ternary, prepare_hessian, quantize_blocks,
-                     quantize_layer, quantize_shared, unpack_ternary)
+from .engine import (LayerGraph, LayerOutput, LayerWorkspace, UnitRun, UnitWorkspace, cholesky_inverse,
+                     dequantize, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
+                     quantize_blocks, quantize_layer, quantize_shared, quantize_unit, unpack_ternary)
 
 __version__ = "0.1.0"
 __all__ = [
@@ -31,4 +31,5 @@ __all__ = [
     "unpack_ternary", "fill_synthetic", "hessian_inverse", "quantize_shared", "GramAccumulator",
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
     "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
+    "UnitRun", "UnitWorkspace", "quantize_unit",
 ]

@@ -13,6 +13,9 @@ SO_PATH = os.path.join(_DIR, "libpt2q.so")
 
 PT2Q_OK = 0
 PT2Q_E_NOT_SPD = 2
+PT2Q_E_STALL = 6
+STATUS_BYTES = 256  # the status word at the head of a workspace (include/pt2q.h)
+STALL_BITS = {0x1: "Gram partial-tile hand-off", 0x2: "ATQ S1/d hand-off", 0x4: "top-k pick hand-off"}
 F32, F16, BF16, I8 = 0, 1, 2, 3
 FLAG_SSR = 0x1
 AGA_NONE, AGA_ACT, AGA_HESS = 0x0, 0x10, 0x20
@@ -82,6 +85,24 @@ def version():
 def check(rc, what=""):
     if rc != PT2Q_OK:
         raise Pt2qError(f"{what}: {_h.pt2q_strerror(rc).decode()} (status {rc})")
+
+
+def status_view(ws):
+    """The int32 status word at the head of a workspace tensor (device; no synchronisation)."""
+    return ws[:4].view(torch.int32)
+
+
+def raise_stall(status: int, what=""):
+    if status:
+        parts = ", ".join(v for k, v in STALL_BITS.items() if status & k) or hex(status)
+        raise Pt2qError(f"{what}: {_h.pt2q_strerror(PT2Q_E_STALL).decode()} [{parts}] "
+                        f"(status {PT2Q_E_STALL})")
+
+
+def check_status(ws, what=""):
+    """Raise if a kernel of the last call on this workspace gave up a cross-workgroup wait
+    (synchronises with the device: one 4-byte read)."""
+    raise_stall(int(status_view(ws).item()), what)
 
 
 def dtype_code(t):

@@ -53,14 +53,34 @@ def get_llm_layers(model: nn.Module, model_type: str = "llama"):
 
 
 class GramAccumulator:
-    """An m x m fp32 Gram fed batch by batch; bit-identical to XᵀX of the concatenated rows."""
+    """An m x m fp32 Gram fed batch by batch; bit-identical to XᵀX of the concatenated rows.
+
+    The 16-bit MFMA Gram advances each fp32 chain in groups of 8 rows, so a batch may only be
+    continued from a row count that is a multiple of 8: the (< 8) remainder rows of a 16-bit
+    batch are held back and lead the next batch's first group (flushed when `G` is read).
+    Stall reports of the streamed Gram launches are OR-ed into a device word and checked once,
+    when `G` is read."""
 
     def __init__(self, m: int, device):
         self.m = m
         self.device = torch.device(device)
-        self.G = torch.zeros((m, m), dtype=torch.float32, device=self.device)
+        self._G = torch.zeros((m, m), dtype=torch.float32, device=self.device)
         self.nsamples = 0
+        self._rows_in_G = 0
+        self._pend: Optional[torch.Tensor] = None
         self._ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), self.device)
+        self._stall = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def _run(self, X: torch.Tensor):
+        mode = "continue" if self._rows_in_G else False
+        engine.gram(X, self._G, accumulate=mode, workspace=self._ws, check=False)
+        torch.bitwise_or(self._stall, _lib.status_view(self._ws), out=self._stall)
+        self._rows_in_G += X.shape[0]
+
+    def _flush(self):
+        if self._pend is not None:
+            pend, self._pend = self._pend, None
+            self._run(pend)
 
     def add(self, X: torch.Tensor):
         X = X.reshape(-1, X.shape[-1])
@@ -69,9 +89,35 @@ class GramAccumulator:
         X = X.to(self.device)
         if X.shape[0] == 0:
             return
-        mode = "continue" if self.nsamples else False
-        engine.gram(X, self.G, accumulate=mode, workspace=self._ws)
         self.nsamples += X.shape[0]
+        if X.dtype not in (torch.float16, torch.bfloat16):
+            self._flush()  # f32 chains advance row by row: any split is exact
+            self._run(X)
+            return
+        if self._pend is not None:
+            if self._pend.dtype != X.dtype:
+                self._flush()
+            else:
+                need = 8 - self._pend.shape[0]
+                head = torch.cat([self._pend, X[:need]])
+                X = X[need:]
+                self._pend = None
+                if head.shape[0] < 8:
+                    self._pend = head
+                    return
+                self._run(head)
+        k = X.shape[0] // 8 * 8
+        if k:
+            self._run(X[:k])
+        if k < X.shape[0]:
+            self._pend = X[k:].clone()
+
+    @property
+    def G(self) -> torch.Tensor:
+        """The finished Gram (flushes held rows; raises Pt2qError if a Gram launch stalled)."""
+        self._flush()
+        _lib.raise_stall(int(self._stall.item()), "GramAccumulator")
+        return self._G
 
 
 class GramCapture:

@@ -1,12 +1,55 @@
 // Exported C ABI of libpt2q (include/pt2q.h): argument checks, workspace carving and the
 // per-layer launch schedule.  All launches are stream-ordered; nothing here synchronises or
 // allocates, so a caller may capture a whole layer into a hipGraph.
+#include <stdlib.h>
 #include <string.h>
+
+#include <climits>
 
 #include "common.hpp"
 #include "internal.hpp"
 
 namespace {
+
+// Development overrides (tools/ probes only), read once at library load -- see Pt2qTuning.
+Pt2qTuning load_tuning() {
+  Pt2qTuning t;
+  auto geti = [](const char* k, int& v) {
+    if (const char* e = std::getenv(k)) v = std::atoi(e);
+  };
+  auto getb = [](const char* k, bool& v) {
+    if (const char* e = std::getenv(k)) v = e[0] != '0';
+  };
+  geti("PT2Q_GRAM_SUPER", t.gram_super);
+  geti("PT2Q_GRAM_GROUPS", t.gram_groups);
+  getb("PT2Q_GRAM_STREAMK", t.gram_split);
+  getb("PT2Q_GRAM_PAIR", t.gram_pair);
+  getb("PT2Q_GRAM_DP", t.gram_dp);
+  getb("PT2Q_GRAM_DMA", t.gram_dma);
+  geti("PT2Q_GRAM_SEGLEN", t.gram_seglen);
+  geti("PT2Q_GEMM_TILE", t.gemm_tile);
+  getb("PT2Q_RANK_UPDATE", t.rank_update);
+  getb("PT2Q_CHOL_PAIR", t.chol_pair);
+  getb("PT2Q_WBAR_FUSED", t.wbar_fused);
+  getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
+  getb("PT2Q_EF_GEMM", t.ef_kernel);
+  if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
+    const long c = std::atol(e);
+    if (c >= 0) t.spin_cap_long = t.spin_cap_short = c;
+  }
+  return t;
+}
+
+}  // namespace
+
+const Pt2qTuning& pt2q_tuning() {
+  static const Pt2qTuning t = load_tuning();
+  return t;
+}
+
+namespace {
+
+const Pt2qTuning& g_tuning_at_load = pt2q_tuning();  // forces the read at dlopen
 
 struct Carve {
   char* p;
@@ -33,6 +76,7 @@ struct Carve {
 inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
 
 struct BlockWs {
+  int* status;  // the call's status word (stall reports)
   float* Wt;
   int8_t* Tt;
   float* Et;
@@ -47,10 +91,15 @@ struct BlockWs {
   int* counters;
   int* iters;
   int* iters_part;
+  float* hb;  // variant G, blocks > 128: the gathered H[blk][blk] and S = H_bbᵀH_bb (bb x bb)
+  float* hS;
   long ldw;
 };
 
-bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
+// variant G's AGA matrix for blocks wider than one workgroup's LDS holds (> 128 columns)
+inline bool hess_wide(int flags, int bb) { return (flags & PT2Q_AGA_MASK) == PT2Q_AGA_HESS && bb > 128; }
+
+bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w, int flags = 0) {
   const long ldw = round_up(n, 64);
   const int bb = b < m ? b : m;
   const int B = b < m ? ceil_div(m, b) : 1;
@@ -72,15 +121,44 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w) {
   w.counters = c.take<int>((size_t)4 * B + pt2q_ssr_counter_ints(n));
   w.iters = c.take<int>((size_t)B);
   w.iters_part = c.take<int>((size_t)ceil_div(n, 16));
+  w.hb = w.hS = nullptr;
+  if (hess_wide(flags, bb)) {
+    w.hb = c.take<float>((size_t)bb * bb);
+    w.hS = c.take<float>((size_t)bb * bb);
+  }
   return c.ok;
 }
 
-size_t blocks_bytes(int n, int m, int b) {  // a dry run of carve_blocks
+size_t blocks_bytes(int n, int m, int b, int flags = 0) {  // a dry run of carve_blocks
   Carve c{nullptr, 0};
   c.dry = true;
   BlockWs w;
-  carve_blocks(c, n, m, b, w);
+  carve_blocks(c, n, m, b, w, flags);
   return c.used;
+}
+
+// hb[t][j] = A[blk[t]][blk[j]] (bs x bs, ld bs): variant G's X_block = H[blk][:, blk] (gptq.py:147)
+__global__ void gather_block_kernel(const float* A, long lda, const int* blk, int bs, float* hb) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, t = blockIdx.y;
+  if (j < bs) hb[(long)t * bs + j] = A[(long)blk[t] * lda + blk[j]];
+}
+
+// S1 = (H_bbᵀH_bb)·1, d = 1ᵀS1 for blocks > 128 columns (quantizer.py:202-218 with X = H_bb):
+// S on the f32 MFMA GEMM (t-ascending fmaf chains, as aga_s1_kernel's src 2), then the row sums
+// in l order and d in j order (pt2q_launch_aga_s1 src 1 on S itself).
+int hess_block_s1(const float* A, long lda, const int* blk, int bs, BlockWs& w, hipStream_t st) {
+  hipLaunchKernelGGL(gather_block_kernel, dim3(ceil_div(bs, 256), bs), dim3(256), 0, st, A, lda, blk, bs, w.hb);
+  PT2Q_LAUNCH_CHECK();
+  GemmDesc g{};
+  g.M = bs; g.N = bs; g.K = bs;
+  g.A = w.hb; g.lda = bs; g.a_layout = LAY_KMAJOR;  // (j, t) = hb[t][j]
+  g.B = w.hb; g.ldb = bs; g.b_layout = LAY_KMAJOR;  // (t, l) = hb[t][l]
+  g.in_dtype = PT2Q_F32;
+  g.C = w.hS; g.ldc = bs;
+  g.mode = GEMM_STORE;
+  int rc = pt2q_launch_gemm(g, st);
+  if (rc != PT2Q_OK) return rc;
+  return pt2q_launch_aga_s1(1, w.hS, bs, nullptr, bs, w.S1, w.d, st);
 }
 
 __global__ void i64_to_i32_kernel(const int64_t* a, int n, int* b) {
@@ -121,8 +199,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     int* nrem = w.rem[cur ^ 1];
     // variant M with blocks <= 128: the ATQ launch also forms S1/d (no separate launch; off
     // the critical path of the rows, which need it only for their AGA)
-    static const char* s1_env = std::getenv("PT2Q_S1_IN_ATQ");  // 0: in the top-k launch
-    const bool s1_in_atq = aga == PT2Q_AGA_ACT && bs <= 128 && !(s1_env && s1_env[0] == '0');
+    const bool s1_in_atq = aga == PT2Q_AGA_ACT && bs <= 128 && pt2q_tuning().s1_in_atq;
     const bool s1_in_topk = !s1_in_atq && ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
     if (ssr) {
       if (r > b) {
@@ -131,7 +208,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
           return rc;
         if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st,
                                        s1_in_topk ? A : nullptr, lda, w.S1, w.d,
-                                       w.counters + 2 * B + 2 * k)) != PT2Q_OK)
+                                       w.counters + 2 * B + 2 * k, w.status)) != PT2Q_OK)
           return rc;
       } else {
         if ((rc = pt2q_launch_select_seq(1, 0, bs, m, rem, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
@@ -143,9 +220,12 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     }
     const float* S1 = nullptr;
     if (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_HESS) {
-      if (!s1_in_topk && !s1_in_atq &&
-          (rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK)
+      if (hess_wide(flags, bs)) {
+        if ((rc = hess_block_s1(A, lda, w.blk, bs, w, st)) != PT2Q_OK) return rc;
+      } else if (!s1_in_topk && !s1_in_atq &&
+                 (rc = pt2q_launch_aga_s1(aga == PT2Q_AGA_ACT ? 1 : 2, A, lda, w.blk, bs, w.S1, w.d, st)) != PT2Q_OK) {
         return rc;
+      }
       S1 = w.S1;
     }
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, S1, w.d, max_iter,
@@ -153,10 +233,9 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
                                     nr > 0 ? w.Et : nullptr, w.ldw, iters + k, w.counters + 2 * k,
                                     st, Hinv, ldhi, nrem, nr, w.Ck, m, w.iters_part,
                                     s1_in_atq ? A : nullptr, lda,
-                                    s1_in_atq ? w.counters + 2 * B + 2 * k : nullptr)) != PT2Q_OK)
+                                    s1_in_atq ? w.counters + 2 * B + 2 * k : nullptr, w.status)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
-    static const char* ef_env = std::getenv("PT2Q_EF_GEMM");  // 0: the generic GEMM
-    rc = (nr > 0 && !(ef_env && ef_env[0] == '0'))
+    rc = (nr > 0 && pt2q_tuning().ef_kernel)
              ? pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st)
              : PT2Q_E_UNSUPPORTED;
     if (rc != PT2Q_OK && rc != PT2Q_E_UNSUPPORTED) return rc;
@@ -183,6 +262,15 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
 
 bool dtype_ok(int dt) { return dt == PT2Q_F32 || dt == PT2Q_F16 || dt == PT2Q_BF16; }
 
+// The status word every workspace-taking call reserves first (PT2Q_STATUS_BYTES), zeroed on the
+// call's stream before any kernel that may report into it.
+int* take_status(Carve& c, hipStream_t st, int& rc) {
+  int* s = c.take<int>(PT2Q_STATUS_BYTES / sizeof(int));
+  rc = PT2Q_OK;
+  if (s && hipMemsetAsync(s, 0, sizeof(int), st) != hipSuccess) rc = PT2Q_E_HIP;
+  return s;
+}
+
 }  // namespace
 
 extern "C" const char* pt2q_version(void) { return "pt2q-mi355x 0.1.0 (gfx950)"; }
@@ -195,6 +283,7 @@ extern "C" const char* pt2q_strerror(int status) {
     case PT2Q_E_UNSUPPORTED: return "unsupported shape/configuration";
     case PT2Q_E_HIP: return "HIP runtime error";
     case PT2Q_E_WORKSPACE: return "workspace too small";
+    case PT2Q_E_STALL: return "a cross-workgroup wait timed out (results invalid)";
   }
   return "unknown status";
 }
@@ -204,24 +293,24 @@ extern "C" size_t pt2q_cholesky_workspace_bytes(int m) {
 }
 
 extern "C" size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags) {
-  (void)flags;
   if (n <= 0 || m <= 0 || b <= 0) return 0;
   size_t mm = ((size_t)m * m * 4 + 255) & ~(size_t)255;
-  return blocks_bytes(n, m, b) + 4 * mm + 2 * 256 + pt2q_gram_workspace_bytes(m);
+  return PT2Q_STATUS_BYTES + blocks_bytes(n, m, b, flags) + 4 * mm + 2 * 256 + pt2q_gram_workspace_bytes(m);
 }
 
 extern "C" size_t pt2q_ssr_workspace_bytes(int n, int m) {
-  return blocks_bytes(n, m, 128);
+  return PT2Q_STATUS_BYTES + blocks_bytes(n, m, 128);
 }
 
 extern "C" size_t pt2q_gram_workspace_bytes(int m) {
-  return m > 0 ? (pt2q_gram_flags_ints(m) * sizeof(int) + 255) & ~(size_t)255 : 0;
+  return m > 0 ? PT2Q_STATUS_BYTES + ((pt2q_gram_flags_ints(m) * sizeof(int) + 255) & ~(size_t)255) : 0;
 }
 
 extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G,
                          int64_t ldg, int accumulate, void* workspace, size_t workspace_bytes,
                          void* stream) {
-  if ((!X && N > 0) || !G || N < 0 || m <= 0 || !dtype_ok(xdtype) || ldx < m || ldg < m)
+  if ((!X && N > 0) || !G || N < 0 || N > INT_MAX || m <= 0 || !dtype_ok(xdtype) || ldx < m ||
+      ldg < m)
     return PT2Q_E_ARG;
   GemmDesc g{};
   g.M = m; g.N = m; g.K = (int)N;
@@ -232,9 +321,16 @@ extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ld
   if (accumulate < 0 || accumulate > 2) return PT2Q_E_ARG;
   g.mode = accumulate == 2 ? GEMM_CHAIN_POS : accumulate ? GEMM_ADD : GEMM_STORE;
   g.upper = 1; g.mirror = 1;
-  int* flags = (workspace && workspace_bytes >= pt2q_gram_flags_ints(m) * sizeof(int))
-                   ? (int*)workspace : nullptr;
-  return pt2q_launch_gram(g, flags, (hipStream_t)stream);
+  // workspace: [status word][split flags]; without it every tile is one chain (nothing waits)
+  int *status = nullptr, *flags = nullptr;
+  if (workspace && workspace_bytes >= pt2q_gram_workspace_bytes(m)) {
+    Carve c{(char*)workspace, workspace_bytes};
+    int rc;
+    status = take_status(c, (hipStream_t)stream, rc);
+    if (rc != PT2Q_OK) return rc;
+    flags = c.take<int>(pt2q_gram_flags_ints(m));
+  }
+  return pt2q_launch_gram(g, flags, (hipStream_t)stream, status);
 }
 
 extern "C" int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples,
@@ -262,14 +358,17 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
                                     int tdtype, int64_t* perm, int* iters_dev, void* workspace,
                                     size_t workspace_bytes, void* stream) {
   if (!W || !Hinv || !alpha || !mu || !T || !perm || n <= 0 || m <= 0 || b <= 0 ||
-      !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0)
+      !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0 || ldw < m ||
+      ldhi < m)
     return PT2Q_E_ARG;
   int aga = flags & PT2Q_AGA_MASK;
-  if (aga != PT2Q_AGA_NONE && !A) return PT2Q_E_ARG;
-  if (aga == PT2Q_AGA_HESS && (b < m ? b : m) > 128) return PT2Q_E_UNSUPPORTED;
+  if (aga != PT2Q_AGA_NONE && (!A || lda < m)) return PT2Q_E_ARG;
   Carve c{(char*)workspace, workspace_bytes};
   BlockWs w;
-  if (!carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
+  int rc;
+  w.status = take_status(c, (hipStream_t)stream, rc);
+  if (rc != PT2Q_OK) return rc;
+  if (!carve_blocks(c, n, m, b, w, flags)) return PT2Q_E_WORKSPACE;
   return run_blocks(W, wdtype, ldw, n, m, b, flags, A, lda, Hinv, ldhi, max_iter, alpha, mu, T,
                     tdtype, perm, iters_dev, w, (hipStream_t)stream);
 }
@@ -281,9 +380,13 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
                                    int* info_dev, void* workspace, size_t workspace_bytes,
                                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!W || !X || !info_dev || N <= 0 || m <= 0 || n <= 0 || b <= 0 || !dtype_ok(xdtype))
+  if (!W || !X || !info_dev || N <= 0 || N > INT_MAX || m <= 0 || n <= 0 || b <= 0 ||
+      !dtype_ok(xdtype) || !dtype_ok(wdtype) || ldx < m || ldw < m)
     return PT2Q_E_ARG;
   Carve c{(char*)workspace, workspace_bytes};
+  int rc;
+  int* status = take_status(c, st, rc);
+  if (rc != PT2Q_OK) return rc;
   float* G = c.take<float>((size_t)m * m);
   float* H = c.take<float>((size_t)m * m);
   float* Ui = c.take<float>((size_t)m * m);
@@ -292,10 +395,18 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
   int* gflags = c.take<int>(pt2q_gram_flags_ints(m));
   BlockWs w;
   if (!c.ok || !carve_blocks(c, n, m, b, w)) return PT2Q_E_WORKSPACE;
-  int rc;
-  if ((rc = pt2q_gram(X, xdtype, N, m, ldx, G, m, 0, gflags,
-                     pt2q_gram_flags_ints(m) * sizeof(int), stream)) != PT2Q_OK)
-    return rc;
+  w.status = status;
+  {
+    GemmDesc g{};
+    g.M = m; g.N = m; g.K = (int)N;
+    g.A = X; g.lda = ldx; g.a_layout = LAY_KMAJOR;
+    g.B = X; g.ldb = ldx; g.b_layout = LAY_KMAJOR;
+    g.in_dtype = xdtype;
+    g.C = G; g.ldc = m;
+    g.mode = GEMM_STORE;
+    g.upper = 1; g.mirror = 1;
+    if ((rc = pt2q_launch_gram(g, gflags, st, status)) != PT2Q_OK) return rc;
+  }
   // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G), so
   // it is written in that form at once (strictly lower part zero; no separate copy pass).
   // Hinv only feeds the error feedback; a single block (per-channel, b >= m) has none, so the
@@ -323,12 +434,14 @@ extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const 
                                int b, int64_t* blk, int64_t* newrem, float* sim, void* workspace,
                                size_t workspace_bytes, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!W || !rem || !blk || n <= 0 || m <= 0 || r <= 0 || r > m || b <= 0) return PT2Q_E_ARG;
+  if (!W || !rem || !blk || n <= 0 || m <= 0 || r <= 0 || r > m || b <= 0 || ldw < m) return PT2Q_E_ARG;
   if (r > b && !newrem) return PT2Q_E_ARG;
   Carve c{(char*)workspace, workspace_bytes};
   BlockWs w;
-  if (!carve_blocks(c, n, m, 128, w)) return PT2Q_E_WORKSPACE;
   int rc;
+  w.status = take_status(c, st, rc);
+  if (rc != PT2Q_OK) return rc;
+  if (!carve_blocks(c, n, m, 128, w)) return PT2Q_E_WORKSPACE;
   if ((rc = pt2q_launch_transpose_to_f32(W, PT2Q_F32, ldw, n, m, w.Wt, w.ldw, st)) != PT2Q_OK) return rc;
   hipLaunchKernelGGL(i64_to_i32_kernel, dim3(ceil_div(r, 256)), dim3(256), 0, st, rem, r, w.rem[0]);
   PT2Q_LAUNCH_CHECK();

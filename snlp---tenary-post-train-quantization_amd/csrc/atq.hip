@@ -197,6 +197,8 @@ struct BlockArgs {
   int* s1sync;       // [0] ready flag, [1] S1 workgroups done (zero before the launch)
   float* S1w;
   float* dw;
+  int* status;       // stall reports (nullable)
+  long cap;          // polls before a wait gives up
 };
 
 // Returns the wave's ITF iteration count (wave-uniform).
@@ -239,12 +241,7 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   int it = 0;
   if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
   if (A.S1 && A.nS1 > 0) {  // S1 / d from this launch's leading workgroups (write-through)
-    if ((threadIdx.x & 63) == 0) {
-      long spins = 0;
-      while (__hip_atomic_load(&A.s1sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-             ++spins < (1l << 26))
-        __builtin_amdgcn_s_sleep(2);
-    }
+    if ((threadIdx.x & 63) == 0) wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, A.status, STALL_ATQ_S1);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -797,7 +794,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv, long ldh, const int* rem, int nr,
                           float* C, long ldc, int* iters_part, const float* G, long ldg,
-                          int* s1sync) {
+                          int* s1sync, int* status) {
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
@@ -810,7 +807,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   }
   const int nS1 = (G && S1 && s1sync && b <= 128) ? ceil_div(b, 8) : 0;
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part,
-              G, ldg, nS1, s1sync, (float*)S1, (float*)d};
+              G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_short};
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;

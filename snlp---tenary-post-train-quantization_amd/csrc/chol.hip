@@ -273,8 +273,7 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     const int rest = m - p0 - nb;
     if (rest <= 0) break;
     const int p1 = p0 + nb, nb1 = (rest < NB) ? rest : NB, rest1 = rest - nb1;
-    static const char* pair_env = std::getenv("PT2Q_CHOL_PAIR");  // 0: one update per block (A/B)
-    if (rest1 <= 0 || (pair_env && pair_env[0] == '0')) {  // one plain update
+    if (rest1 <= 0 || !pt2q_tuning().chol_pair) {  // one plain update
       if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, rest, p1, rest),
                                   trtri_desc(U, Ui, ld, p0, nb, rest), st, U, ld, p1, nb1, info,
                                   &factored)) != PT2Q_OK)

@@ -91,6 +91,60 @@ constexpr int SUMN_LDS_MAX = 12288;  // floats staged in LDS by block_sumn_lds u
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---- Launch configuration fixed at library load.
+// The production path has no tunables; these development overrides (PT2Q_* environment
+// variables, used only by the tools/ probes) are read ONCE when libpt2q.so is loaded, never in a
+// launch path.  Defaults are the measured best configuration.
+struct Pt2qTuning {
+  int gram_super = 0;          // PT2Q_GRAM_SUPER: 16-bit Gram super-block side (0: by m)
+  int gram_groups = 8;         // PT2Q_GRAM_GROUPS: XCD groups of the 16-bit Gram split
+  bool gram_split = true;      // PT2Q_GRAM_STREAMK=0: one chain per tile, no split
+  bool gram_pair = true;       // PT2Q_GRAM_PAIR=0: no tile-pair teams
+  bool gram_dp = true;         // PT2Q_GRAM_DP=0: no data-parallel waves
+  bool gram_dma = true;        // PT2Q_GRAM_DMA=0: f32-kernel family without LDS-DMA
+  int gram_seglen = 0;         // PT2Q_GRAM_SEGLEN: f32 stream-K segment override
+  int gemm_tile = 0;           // PT2Q_GEMM_TILE: 1 = 128x128, 6 = 64x64
+  bool rank_update = true;     // PT2Q_RANK_UPDATE=0: generic grouped GEMM for Cholesky updates
+  bool chol_pair = true;       // PT2Q_CHOL_PAIR=0: one trailing update per block
+  bool wbar_fused = true;      // PT2Q_WBAR_FUSED=0: three SSR-mean launches
+  bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
+  bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM
+  // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
+  // seconds, before they give up and report PT2Q_E_STALL.  PT2Q_DEBUG_SPIN_CAP overrides both
+  // (0: every hand-off reports a stall -- tests force the reporting path with it).
+  long spin_cap_long = 1l << 28;   // Gram partial-tile hand-offs (a long chain may be in flight)
+  long spin_cap_short = 1l << 26;  // in-launch hand-offs (S1 / d, top-k picks)
+};
+const Pt2qTuning& pt2q_tuning();  // api.hip
+
+// ---- Stall reporting.
+// Every call that takes a workspace reserves its first PT2Q_STATUS_BYTES (pt2q.h) for a status
+// word (int, zeroed by the call).  A wait on another workgroup that gives up ORs its bit into that
+// word instead of carrying on silently; the host reads it after the stream completes and raises
+// PT2Q_E_STALL (_lib.check_status).
+enum : int { STALL_GRAM = 0x1, STALL_ATQ_S1 = 0x2, STALL_TOPK = 0x4 };
+
+// Poll *flag until it is >= v.  Returns false (and marks *status) if the wait gave up after `cap`
+// polls.  Call from one thread; the caller orders the data it then reads (fence / sc1 loads).
+// cap == 0 is the test setting: every hand-off reports a stall, ready or not, so the reporting
+// path is exercised deterministically.
+template <int SLEEP>
+PT2Q_DEV bool wait_flag_ge(const int* flag, int v, long cap, int* status, int bit) {
+  if (cap == 0) {
+    if (status) atomicOr(status, bit);
+    return false;
+  }
+  long spins = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
+    if (++spins > cap) {
+      if (status) atomicOr(status, bit);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(SLEEP);
+  }
+  return true;
+}
+
 #define PT2Q_LAUNCH_CHECK()                                      \
   do {                                                           \
     if (hipGetLastError() != hipSuccess) return PT2Q_E_HIP;      \

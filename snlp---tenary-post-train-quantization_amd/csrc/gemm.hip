@@ -415,14 +415,14 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemmDesc g0, int tm0, int tn
 // resident.  Units taken together share a K range, so the X panels they read are shared in L2.
 template <typename TIn, bool VEC>
 __global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, int nseg, int seglen,
-                                                           int* flags, int* timeout) {
+                                                           int* flags, int* counter, int* status,
+                                                           long cap) {
   constexpr int BM = 128, BN = 128;
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
   __shared__ long s_unit;
   const int ntile = T * (T + 1) / 2;
   const long units = (long)ntile * nseg;
-  int* counter = timeout + 1;
   for (;;) {
     if (threadIdx.x == 0) s_unit = atomicAdd(counter, 1);
     __syncthreads();
@@ -447,14 +447,7 @@ __global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, in
       });
     } else {
       if (threadIdx.x == 0) {
-        long spins = 0;
-        while (__hip_atomic_load(&flags[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < seg) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1l << 28)) {
-            atomicExch(timeout, 1);
-            break;
-          }
-        }
+        wait_flag_ge<2>(&flags[tl], seg, cap, status, STALL_GRAM);  // gives up loudly
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -641,7 +634,7 @@ __device__ unsigned long long g16_prof[4];
 // The only dependency is on workgroup w-1, which the in-order dispatcher starts first.
 template <bool BF16>
 __global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, int Kp, long L,
-                                                             int* flags, int* timeout,
+                                                             int* flags, int* status, long cap,
                                                              const uint16_t* zeros) {
   constexpr int BM = 128, BN = 128;
   // ONE __shared__ object: a second one beside the DMA staging makes hipcc wait vmcnt(0)
@@ -689,14 +682,7 @@ __global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, 
       F.for_each(i0, j0, [&](float& v, int, int) { v = 0.0f; });
     } else {
       if (from_partial && threadIdx.x == 0) {
-        long spins = 0;
-        while (__hip_atomic_load(&flags[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 1) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > (1l << 28)) {
-            atomicExch(timeout, 1);
-            break;
-          }
-        }
+        wait_flag_ge<2>(&flags[a], 1, cap, status, STALL_GRAM);  // gives up loudly
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -787,9 +773,9 @@ int launch_dt(const GemmDesc& g, hipStream_t st) {
   };
   const double slots = 256.0;
   long c128 = count(128), c64 = count(64);
-  static const char* force = std::getenv("PT2Q_GEMM_TILE");
-  if (force && force[0] == '1') return launch_t<128, 128, TIn>(g, st);
-  if (force && force[0] == '6') return launch_t<64, 64, TIn>(g, st);
+  const int force = pt2q_tuning().gemm_tile;
+  if (force == 1) return launch_t<128, 128, TIn>(g, st);
+  if (force == 6) return launch_t<64, 64, TIn>(g, st);
   // efficiency = useful tiles / (rounds * slots); 64x64 tiles cost 1/4 of a 128x128 tile
   double r128 = std::ceil(c128 / slots), r64 = std::ceil(c64 / slots);
   double t128 = r128 * 4.0, t64 = r64 * 1.0 * 1.15;  // 64x64: ~15% lower per-tile efficiency
@@ -798,7 +784,8 @@ int launch_dt(const GemmDesc& g, hipStream_t st) {
 }
 
 template <typename TIn>
-int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
+int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st, int* status) {
+  const Pt2qTuning& tu = pt2q_tuning();
   const int T = ceil_div(g.M, 128);
   const int ntile = T * (T + 1) / 2;
   if (ntile > nflags) return PT2Q_E_WORKSPACE;
@@ -806,9 +793,8 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   auto kern = vec_ok<128, 128, TIn>(g) ? gram_streamk_kernel<TIn, true> : gram_streamk_kernel<TIn, false>;
   // 16-bit inputs with 16-byte rows: the LDS-DMA kernel (PT2Q_GRAM_DMA=0 disables)
-  static const char* dma_env = std::getenv("PT2Q_GRAM_DMA");
-  const bool dma = sizeof(TIn) == 2 && vec_ok<128, 128, TIn>(g) && !(dma_env && dma_env[0] == '0');
-  void (*kern16)(GemmDesc, int, int, long, int*, int*, const uint16_t*) =
+  const bool dma = sizeof(TIn) == 2 && vec_ok<128, 128, TIn>(g) && tu.gram_dma;
+  void (*kern16)(GemmDesc, int, int, long, int*, int*, long, const uint16_t*) =
       std::is_same<TIn, uint16_t>::value ? gram16_streamk_kernel<true> : gram16_streamk_kernel<false>;
   if (dma) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern16, 256, 0) != hipSuccess || per_cu < 1)
@@ -833,14 +819,14 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
       seglen = len;
     }
   }
-  // flags: ntile tile flags, timeout, unit counter, then 16 zero bytes (aligned) for the DMA
-  static const char* seg_env = std::getenv("PT2Q_GRAM_SEGLEN");  // tuning override
-  if (seg_env && std::atoi(seg_env) >= 64) {
-    seglen = std::atoi(seg_env) / (2 * BK) * (2 * BK);
+  // flags: ntile tile flags, status, unit counter, then 16 zero bytes (aligned) for the DMA
+  if (tu.gram_seglen >= 64) {
+    seglen = tu.gram_seglen / (2 * BK) * (2 * BK);
     nseg = ceil_div(g.K, seglen);
   }
   if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2 + 8), st) != hipSuccess) return PT2Q_E_HIP;
-  int* timeout = flags + ntile;
+  if (!status) status = flags + ntile;
+  int* counter = flags + ntile + 1;
   if (dma) {
     const uint16_t* zeros = (const uint16_t*)(((uintptr_t)(flags + ntile + 2) + 15) & ~(uintptr_t)15);
     // static split: P16 workgroups, each L >= Kp rows of the tile-major work line
@@ -849,9 +835,10 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st) {
     const long Wt = (long)ntile * Kp;
     const long L = ((Wt + P16 - 1) / P16 + G16_BK - 1) / G16_BK * G16_BK;
     hipLaunchKernelGGL(kern16, dim3((unsigned)ceil_div(Wt, L)), dim3(256), 0, st, g, T, Kp, L, flags,
-                       timeout, zeros);
+                       status, tu.spin_cap_long, zeros);
   } else {
-    hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, timeout);
+    hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, counter, status,
+                       tu.spin_cap_long);
   }
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
@@ -1081,8 +1068,7 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
                       int dp0, int dnb, int* info, bool* fused) {
   if (fused) *fused = false;
   if (g0.in_dtype != PT2Q_F32 || g1.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
-  static const char* ru_env = std::getenv("PT2Q_RANK_UPDATE");  // 0: generic grouped GEMM
-  if (ru_ok(g0) && ru_ok(g1) && !(ru_env && ru_env[0] == '0')) {
+  if (ru_ok(g0) && ru_ok(g1) && pt2q_tuning().rank_update) {
     int tm0, tn0, tm1, tn1;
     const long n0 = tiles_of<RU_T, RU_T>(g0, tm0, tn0), n1 = tiles_of<RU_T, RU_T>(g1, tm1, tn1);
     if (n0 + n1 <= 0) return PT2Q_OK;
@@ -1121,27 +1107,26 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
 
 size_t pt2q_gram_flags_ints(int m) {
   long T = ceil_div(m, 128);
-  // tile flags, timeout, unit counter, zero chunk; or the 16-bit kernel's
+  // tile flags, status, unit counter, zero chunk; or the 16-bit kernel's
   return std::max((size_t)(T * (T + 1) / 2 + 2 + 8), pt2q_gram16_flags_ints(m));
 }
 
 // Symmetric Gram C = XᵀX (STORE): balanced persistent kernel when it pays (big K, enough
 // tiles), else the one-tile-per-workgroup GEMM.  flags: pt2q_gram_flags_ints(m) ints or NULL.
-int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st) {
-  if (g.in_dtype == PT2Q_F16 || g.in_dtype == PT2Q_BF16) return pt2q_launch_gram16(g, flags, st);
+int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st, int* status) {
+  if (g.in_dtype == PT2Q_F16 || g.in_dtype == PT2Q_BF16) return pt2q_launch_gram16(g, flags, st, status);
   const int T = ceil_div(g.M, 128);
   const long ntile = (long)T * (T + 1) / 2;
-  static const char* mode = std::getenv("PT2Q_GRAM_STREAMK");
-  const bool allow = !(mode && mode[0] == '0');
+  const bool allow = pt2q_tuning().gram_split;
   if (flags && allow && (g.mode == GEMM_STORE || g.mode == GEMM_CHAIN_POS) && g.upper && g.mirror && g.M == g.N &&
       ntile >= 128 && g.K >= 16384) {
     switch (g.in_dtype) {
       case PT2Q_F32:
-        return launch_streamk<float>(g, flags, (int)ntile, st);
+        return launch_streamk<float>(g, flags, (int)ntile, st, status);
       case PT2Q_F16:
-        return launch_streamk<_Float16>(g, flags, (int)ntile, st);
+        return launch_streamk<_Float16>(g, flags, (int)ntile, st, status);
       case PT2Q_BF16:
-        return launch_streamk<uint16_t>(g, flags, (int)ntile, st);
+        return launch_streamk<uint16_t>(g, flags, (int)ntile, st, status);
     }
   }
   return pt2q_launch_gemm(g, st);

@@ -310,7 +310,8 @@ struct GxTile {
 // previous team (w - P*NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
 template <bool BF16, bool DMA>
 __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ, int SJ, int Kp, long ntile, int NG,
-                                                      int R, int P, int D, int* flags, int* timeout) {
+                                                      int R, int P, int D, int* flags, int* status,
+                                                      long cap) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[GX_LDS];
   const uint16_t* X = (const uint16_t*)g.A;
   const int w = blockIdx.x;
@@ -353,14 +354,7 @@ __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ
     const int i0 = ti * GX_BM, j0 = tj * GX_BN;
     GxTile F;
     if (from_partial && threadIdx.x == 0) {
-      long spins = 0;
-      while (__hip_atomic_load(&flags[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 1) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1l << 28)) {
-          atomicExch(timeout, 1);
-          break;
-        }
-      }
+      wait_flag_ge<2>(&flags[a], 1, cap, status, STALL_GRAM);  // gives up loudly (status word)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -427,32 +421,26 @@ size_t pt2q_gram16_flags_ints(int m) { return (size_t)gx_ntile(m) + 2; }
 // 16-bit Gram, every shape and mode.  flags (nullable, >= pt2q_gram16_flags_ints(m) ints):
 // scratch for the split; without it (or in ADD mode, whose C holds the old values) every tile
 // is one chain on one workgroup.
-int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
+int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st, int* status) {
   if (g.in_dtype != PT2Q_F16 && g.in_dtype != PT2Q_BF16) return PT2Q_E_ARG;
   if (g.M != g.N || g.A != g.B || g.lda != g.ldb) return PT2Q_E_ARG;
+  const Pt2qTuning& tu = pt2q_tuning();
   const int m = g.M;
   const int TI = ceil_div(m, GX_BM), TJ = ceil_div(m, GX_BN);
-  static const char* sj_env = std::getenv("PT2Q_GRAM_SUPER");  // tuning override
   // super-block side ~ the square one XCD's share of the triangle covers
-  const int SJ = sj_env ? std::max(1, std::atoi(sj_env)) : (m <= 6144 ? 4 : 8);
+  const int SJ = tu.gram_super > 0 ? tu.gram_super : (m <= 6144 ? 4 : 8);
   const long ntile = gx_ntile(m);
   const int Kp = std::max(1, ceil_div(g.K, GX_BK)) * GX_BK;  // K = 0: one all-zero stage
-  const long W = ntile * Kp;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  static const char* split_env = std::getenv("PT2Q_GRAM_STREAMK");
-  static const char* ng_env = std::getenv("PT2Q_GRAM_GROUPS");  // tuning override
   // split when there are more tiles than CUs: NG XCD groups of R workgroups (one per CU)
-  int NG = ng_env ? std::max(1, std::atoi(ng_env)) : 8;
+  int NG = std::max(1, tu.gram_groups);
   int R = cus / NG;
-  const bool split = flags && g.mode != GEMM_ADD && !(split_env && split_env[0] == '0') &&
-                     R > 0 && ntile >= (long)NG * R;
+  const bool split = flags && g.mode != GEMM_ADD && tu.gram_split && R > 0 && ntile >= (long)NG * R;
   // tile pairs need every column run of the tile order to be even (TI even) and teams of two
-  static const char* pair_env = std::getenv("PT2Q_GRAM_PAIR");
-  int P = (split && TI % 2 == 0 && R % 2 == 0 && !(pair_env && pair_env[0] == '0')) ? 2 : 1;
+  int P = (split && TI % 2 == 0 && R % 2 == 0 && tu.gram_pair) ? 2 : 1;
   // whole data-parallel waves while at least one tile per workgroup is left for stream-K
-  static const char* dp_env = std::getenv("PT2Q_GRAM_DP");
-  const int D = (split && !(dp_env && dp_env[0] == '0')) ? (int)std::max(0l, ntile / (NG * R) - 1) : 0;
+  const int D = (split && tu.gram_dp) ? (int)std::max(0l, ntile / (NG * R) - 1) : 0;
   unsigned grid;
   if (split) {
     grid = (unsigned)(NG * R);
@@ -463,15 +451,16 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st) {
     P = 1;
     grid = (unsigned)ntile;
   }
-  (void)W;
-  int* timeout = split ? flags + ntile : nullptr;
+  // the status word: the caller's, else a word of the flag area (zeroed above)
+  if (!status && split) status = flags + ntile;
   // (fast staging keeps a stage's byte offsets in 32 bits: 64 rows * lda * 2 < 2^32)
   const bool dma = ((uintptr_t)g.A % 16 == 0) && (g.lda % 8 == 0) && (m % 8 == 0) && g.lda < (1l << 25);
   const bool bf = g.in_dtype == PT2Q_BF16;
-  void (*k)(GemmDesc, int, int, int, int, long, int, int, int, int, int*, int*) =
+  void (*k)(GemmDesc, int, int, int, int, long, int, int, int, int, int*, int*, long) =
       bf ? (dma ? gram16x_kernel<true, true> : gram16x_kernel<true, false>)
          : (dma ? gram16x_kernel<false, true> : gram16x_kernel<false, false>);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, TJ, SJ, Kp, ntile, NG, R, P, D, flags, timeout);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, st, g, TI, TJ, SJ, Kp, ntile, NG, R, P, D, flags, status,
+                     tu.spin_cap_long);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

@@ -12,7 +12,8 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           int* iters_part = nullptr,  // ceil(n/16) ints of scratch, nullable
                           // variant M, b <= 128: S1/d (into S1, d) formed inside the launch from
                           // the raw Gram G; s1sync: 2 zeroed ints
-                          const float* G = nullptr, long ldg = 0, int* s1sync = nullptr);
+                          const float* G = nullptr, long ldg = 0, int* s1sync = nullptr,
+                          int* status = nullptr);  // status word (stall reporting), nullable
 
 // ---- SSR / selection (ssr.hip)
 // cnt (nullable): pt2q_ssr_counter_ints(n) zeroed ints -> one fused wbar launch (self-resetting)
@@ -21,7 +22,8 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
 inline int pt2q_ssr_counter_ints(int n) { return (n + 255) / 256 + 1; }
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
-                         float* S1 = nullptr, float* d = nullptr, int* sync = nullptr);
+                         float* S1 = nullptr, float* d = nullptr, int* sync = nullptr,
+                         int* status = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
                            int* newrem, int64_t* perm_out, hipStream_t st);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
@@ -61,10 +63,11 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
                       long dld = 0, int dp0 = 0, int dnb = 0, int* info = nullptr,
                       bool* fused = nullptr);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
-int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st);
+// status (nullable): the caller's status word for stall reports (else a word of the flag area)
+int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);
 size_t pt2q_gram_flags_ints(int m);
 // 16-bit-input Gram on the 16-bit MFMA (gram16.hip): every shape, STORE / ADD / CHAIN_POS
-int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st);
+int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);
 size_t pt2q_gram16_flags_ints(int m);
 
 // ---- misc (misc.hip)

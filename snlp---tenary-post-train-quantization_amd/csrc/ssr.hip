@@ -362,16 +362,11 @@ __device__ long long topk_stamps[64][16];
 #endif
 
 PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* S1, float* d,
-                        int* sync, float* gb) {
+                        int* sync, float* gb, int* status, long cap) {
   const int tid = threadIdx.x, nh = gridDim.x - 1;
   // hand-offs (pick -> helpers, S1 -> the last helper): write-through (sc1) stores drained
   // before the flag / counter, sc1 loads on the consuming side, no fences
-  if (tid == 0) {
-    long spins = 0;
-    while (__hip_atomic_load(&sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
-           ++spins < (1l << 26))
-      __builtin_amdgcn_s_sleep(1);
-  }
+  if (tid == 0) wait_flag_ge<1>(&sync[0], 1, cap, status, STALL_TOPK);
   __syncthreads();
   TOPK_STAMP(8);
   const int jj = tid >> 7, l = tid & 127;
@@ -416,10 +411,11 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
                                                                 int b, int* blk, int* newrem,
                                                                 int64_t* perm_out, const float* G,
                                                                 long ldg, float* S1, float* d,
-                                                                int region0, int* sync) {
+                                                                int region0, int* sync, int* status,
+                                                                long cap) {
   extern __shared__ uint32_t vals[];
   if (blockIdx.x > 0) {
-    s1_helper(G, ldg, blk, b, S1, d, sync, (float*)vals);
+    s1_helper(G, ldg, blk, b, S1, d, sync, (float*)vals, status, cap);
     return;
   }
   int* hist = (int*)(vals + r);
@@ -753,8 +749,7 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   if (r <= 0 || n <= 0) return PT2Q_E_ARG;
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
-  static const char* fuse_env = std::getenv("PT2Q_WBAR_FUSED");  // 0: three launches
-  if (cnt && n <= 4096 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && !(fuse_env && fuse_env[0] == '0')) {
+  if (cnt && n <= 4096 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && pt2q_tuning().wbar_fused) {
     hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 1024)), dim3(256), 0, st, Wt, ldw,
                        n, rem, r, part, wn, cnt);
     PT2Q_LAUNCH_CHECK();
@@ -781,7 +776,7 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
 
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G, long ldg, float* S1,
-                         float* d, int* sync) {
+                         float* d, int* sync, int* status) {
   if (G && b > 128) return PT2Q_E_ARG;
   if (b <= 0 || b > r || r >= 65536) return PT2Q_E_UNSUPPORTED;
   if (G && !sync) return PT2Q_E_ARG;  // sync: 2 ints the caller zeroed before this launch
@@ -791,7 +786,8 @@ int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* bl
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   const int grid = G ? 1 + ceil_div(b, S1_ROWS) : 1;
   hipLaunchKernelGGL(ssr_topk_kernel, dim3(grid), dim3(TOPK_THREADS), lds, st, sim, rem, r, b, blk,
-                     newrem, perm_out, G, ldg, S1, d, region0, sync);
+                     newrem, perm_out, G, ldg, S1, d, region0, sync, status,
+                     pt2q_tuning().spin_cap_short);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

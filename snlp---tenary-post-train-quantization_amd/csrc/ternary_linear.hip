@@ -206,10 +206,33 @@ extern "C" int pt2q_ternary_pack(const int8_t* T, int64_t ldt, int n, int m, con
   return PT2Q_OK;
 }
 
+namespace {
+// Launch plan shared by the workspace query and the launcher: K split so that decode-sized calls
+// still put ~2 workgroups on every CU (prefill-sized calls get splits = 1), and token tiles per
+// wave (each dequantised operand reused across up to 4 MFMA token tiles).
+struct TlPlan {
+  int splits, kchunk, NT;
+};
+TlPlan tl_plan(int tokens, int n, int m) {
+  const int P = (int)pt2q_ternary_linear_positions(m);
+  const int tiles = ceil_div(n, 128) * ceil_div(tokens, tokens >= 512 ? 128 : (tokens >= 128 ? 64 : 32));
+  const int nkb = P / TL_PB;
+  int splits = 1;
+  while (splits < 16 && tiles * splits < 512 && nkb / (splits * 2) >= 2) splits *= 2;
+  TlPlan p;
+  p.kchunk = ceil_div(nkb, splits) * TL_PB;
+  p.splits = ceil_div(P, p.kchunk);
+  p.NT = tokens >= 512 ? 4 : (tokens >= 128 ? 2 : 1);
+  return p;
+}
+}  // namespace
+
 extern "C" size_t pt2q_ternary_linear_workspace_bytes(int tokens, int n, int m) {
+  if (tokens <= 0 || n <= 0 || m <= 0) return 0;
   const size_t P = pt2q_ternary_linear_positions(m);
-  const int splits = 16;  // upper bound used by the launcher
-  return ((size_t)tokens * P * 2 + 255) / 256 * 256 + (size_t)splits * tokens * n * 4 + 256;
+  const TlPlan pl = tl_plan(tokens, n, m);
+  // gathered activations (tokens x P 16-bit) + the split partial sums (splits x tokens x n fp32)
+  return ((size_t)tokens * P * 2 + 255) / 256 * 256 + (size_t)pl.splits * tokens * n * 4 + 256;
 }
 
 extern "C" int pt2q_ternary_linear(const void* x, int xdtype, int tokens, int64_t ldx, int n, int m,
@@ -233,15 +256,8 @@ extern "C" int pt2q_ternary_linear(const void* x, int xdtype, int tokens, int64_
   hipLaunchKernelGGL(tl_gather_x_kernel, dim3(ceil_div((long)tokens * P, 256)), dim3(256), 0, st,
                      (const uint16_t*)x, (long)ldx, tokens, gather, P, xs);
   PT2Q_LAUNCH_CHECK();
-  // K split so that decode-sized calls still put ~2 workgroups on every CU
-  const int tiles = ceil_div(n, 128) * ceil_div(tokens, tokens >= 512 ? 128 : (tokens >= 128 ? 64 : 32));
-  const int nkb = P / TL_PB;
-  int splits = 1;
-  while (splits < 16 && tiles * splits < 512 && nkb / (splits * 2) >= 2) splits *= 2;
-  const int kchunk = ceil_div(nkb, splits) * TL_PB;
-  splits = ceil_div(P, kchunk);
-  // token tiles per wave: reuse each dequantised operand across up to 4 MFMA token tiles
-  const int NT = tokens >= 512 ? 4 : (tokens >= 128 ? 2 : 1);
+  const TlPlan pl = tl_plan(tokens, n, m);
+  const int splits = pl.splits, kchunk = pl.kchunk, NT = pl.NT;
   dim3 grid(ceil_div(n, 128), ceil_div(tokens, 32 * NT), splits);
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, codes, P, alpha, mu, B, bse, xs, tokens, n,

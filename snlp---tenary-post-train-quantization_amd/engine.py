@@ -37,14 +37,19 @@ class LayerOutput:
 
 
 def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate=False,
-         workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+         workspace: Optional[torch.Tensor] = None, check: bool = True) -> torch.Tensor:
     """XᵀX (main.py:128), X (N, m) or (B, L, m).
 
     accumulate=False: G = XᵀX.  True: G = G + XᵀX (gptq.py:75 add_batch).  "continue": every
     entry's fp32 chain resumes from G, so a Gram streamed batch by batch is bit-identical to one
     Gram of the concatenated rows (the captured-and-concatenated X of main.py:293) — for fp16 /
     bf16 activations, whose 16-bit MFMA chain advances in groups of 8 rows, when every batch
-    but the last has a multiple of 8 rows."""
+    but the last has a multiple of 8 rows (calibration.GramAccumulator carries the remainder
+    rows itself, so ragged batches keep the guarantee).
+
+    check=True reads the workspace status word afterwards (one host synchronisation) and raises
+    Pt2qError if a stream-K hand-off timed out; check=False leaves that to the caller
+    (`_lib.check_status(workspace)`)."""
     X = _float_input(X.reshape(-1, X.shape[-1]))
     N, m = X.shape
     if G is None:
@@ -57,6 +62,8 @@ def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate=False,
     _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), N, m, m, _lib.ptr(G), m,
                                     mode, _lib.ptr(ws), ws.numel(),
                                     _lib.stream_of(X.device)), "pt2q_gram")
+    if check:
+        _lib.check_status(ws, "pt2q_gram")
     return G
 
 
@@ -108,6 +115,7 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: torch.Tens
         _lib.dtype_code(T), _lib.ptr(perm), _lib.ptr(iters), _lib.ptr(ws), ws.numel(),
         _lib.stream_of(dev))
     _lib.check(rc, "pt2q_quantize_blocks")
+    _lib.check_status(ws, "pt2q_quantize_blocks")
     return LayerOutput(alpha, mu, T, perm, iters)
 
 
@@ -136,6 +144,116 @@ def quantize_shared(Ws, G: torch.Tensor, nsamples: int, block_size: int = 128,
     return outs
 
 
+class UnitWorkspace:
+    """Device buffers for repeated work units of one input width m (bench / model loops): the
+    Gram, damped Hessian and inverse, the Gram and Cholesky scratch, and one block-loop workspace
+    per output width n.  Buffers are reused call after call (stream-ordered), nothing is freed."""
+
+    def __init__(self, m: int, device, block_size: int = 128, flags=_lib.FLAG_SSR | _lib.AGA_ACT):
+        dev = torch.device(device)
+        self.m, self.device, self.block_size, self.flags = m, dev, block_size, flags
+        self.G = torch.empty((m, m), dtype=torch.float32, device=dev)
+        self.H = torch.empty_like(self.G)
+        self.Hinv = torch.empty_like(self.G)
+        self.damp = torch.empty(1, dtype=torch.float32, device=dev)
+        self.gram_ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), dev)
+        self.chol_ws = _lib.workspace(_lib.lib().pt2q_cholesky_workspace_bytes(m), dev)
+        self._blocks = {}
+
+    def blocks(self, n: int) -> torch.Tensor:
+        if n not in self._blocks:
+            self._blocks[n] = _lib.workspace(
+                _lib.lib().pt2q_layer_workspace_bytes(n, self.m, self.block_size, self.flags), self.device)
+        return self._blocks[n]
+
+
+class UnitRun:
+    """Outputs of quantize_unit whose device status has not been read yet (see finish())."""
+
+    def __init__(self, outs, info, statuses, redo):
+        self.outs, self.info, self.statuses, self._redo = outs, info, statuses, redo
+        self.spd = None
+
+    def finish(self):
+        """One host read of the Cholesky status and every stall word; raises Pt2qError on a
+        stall, and re-runs the unit with pinv (main.py:140-141) if the Hessian was not SPD."""
+        if self.spd is not None:
+            return self.outs
+        vals = torch.cat([self.info.reshape(1)] + [s.reshape(1) for s in self.statuses]).cpu().tolist()
+        for v in vals[1:]:
+            _lib.raise_stall(int(v), "quantize_unit")
+        self.spd = vals[0] == 0
+        if not self.spd:
+            self.outs = self._redo()
+        for o in self.outs:
+            o.spd = self.spd
+        return self.outs
+
+
+def quantize_unit(Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor] = None,
+                  nsamples: Optional[int] = None, block_size: int = 128, use_ssr: bool = True,
+                  percdamp: float = 0.01, max_iter: int = 100, t_dtype=torch.int8,
+                  workspace: Optional[UnitWorkspace] = None, defer: bool = False):
+    """One work unit of the model loop (main.py:289-299 for linears that read the same input:
+    q/k/v, gate/up, or a single linear): Gram of X (or a given raw Gram G over `nsamples` rows),
+    damping, Cholesky inverse, then each weight's block loop, all stream-ordered with NO host
+    synchronisation.  Results are bit-identical to quantize_layer(W, X) per linear.
+
+    defer=False reads the status once at the end and returns [LayerOutput]; defer=True returns a
+    UnitRun whose finish() does that read later (a model loop checks once per step)."""
+    Ws = [_float_input(W) for W in Ws]
+    m = Ws[0].shape[1]
+    dev = Ws[0].device
+    ws = workspace if workspace is not None and workspace.m == m else UnitWorkspace(m, dev, block_size)
+    L = _lib.lib()
+    statuses = []
+    if X is not None:
+        X = _float_input(X.reshape(-1, X.shape[-1]))
+        nsamples = X.shape[0]
+        _lib.check(L.pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), nsamples, m, m, _lib.ptr(ws.G), m, 0,
+                               _lib.ptr(ws.gram_ws), ws.gram_ws.numel(), _lib.stream_of(dev)),
+                   "pt2q_gram")
+        statuses.append(_lib.status_view(ws.gram_ws).clone())
+        Gm = ws.G
+    else:
+        if G is None or nsamples is None:
+            raise ValueError("quantize_unit needs X, or G and nsamples")
+        Gm = G.contiguous().float()
+    st = _lib.stream_of(dev)
+    _lib.check(L.pt2q_prepare_hessian(_lib.ptr(Gm), m, m, int(nsamples), float(percdamp),
+                                      _lib.ptr(ws.H), m, _lib.ptr(ws.damp), st), "pt2q_prepare_hessian")
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(L.pt2q_cholesky_inverse(_lib.ptr(ws.H), m, m, _lib.ptr(ws.Hinv), m, _lib.ptr(ws.chol_ws),
+                                       ws.chol_ws.numel(), _lib.ptr(info), st), "pt2q_cholesky_inverse")
+    flags = (_lib.FLAG_SSR if use_ssr else 0) | _lib.AGA_ACT
+    outs = []
+    for W in Ws:
+        n = W.shape[0]
+        B = num_blocks(m, block_size)
+        out = LayerOutput(torch.empty((n, B), dtype=torch.float32, device=dev),
+                          torch.empty((n, B), dtype=torch.float32, device=dev),
+                          torch.empty((n, m), dtype=t_dtype, device=dev),
+                          torch.empty(m, dtype=torch.int64, device=dev),
+                          torch.zeros(B, dtype=torch.int32, device=dev))
+        bws = ws.blocks(n)
+        rc = L.pt2q_quantize_blocks(
+            _lib.ptr(W), _lib.dtype_code(W), m, n, m, int(block_size), flags, _lib.ptr(Gm), m,
+            _lib.ptr(ws.Hinv), m, int(max_iter), _lib.ptr(out.alpha), _lib.ptr(out.mu), _lib.ptr(out.T),
+            _lib.dtype_code(out.T), _lib.ptr(out.perm), _lib.ptr(out.iters), _lib.ptr(bws), bws.numel(), st)
+        _lib.check(rc, "pt2q_quantize_blocks")
+        statuses.append(_lib.status_view(bws).clone())
+        outs.append(out)
+    def redo():  # main.py:140-141: pinv of the damped Hessian, then the block loops again
+        # (the shared workspace may hold a later unit by now: rebuild G from the caller's tensors)
+        Gr = gram(X) if X is not None else G.contiguous().float()
+        Hinv = torch.linalg.pinv(prepare_hessian(Gr, nsamples, percdamp)[0])
+        return [quantize_blocks(W, Gr, Hinv, block_size, use_ssr, _lib.AGA_ACT, max_iter, t_dtype)
+                for W in Ws]
+
+    run = UnitRun(outs, info, statuses, redo)
+    return run if defer else run.finish()
+
+
 class LayerWorkspace:
     """Reusable device workspace for repeated layers of one shape (bench / model loops)."""
 
@@ -145,8 +263,12 @@ class LayerWorkspace:
         self.shape = (n, m, block_size)
 
     def gram_view(self, m):
-        # pt2q_quantize_layer carves the raw Gram first (256-byte aligned base)
-        return self.buf[: m * m * 4].view(torch.float32).view(m, m)
+        # pt2q_quantize_layer carves the status word first, then the raw Gram (256-byte aligned)
+        o = _lib.STATUS_BYTES
+        return self.buf[o: o + m * m * 4].view(torch.float32).view(m, m)
+
+    def status(self):
+        return _lib.status_view(self.buf)
 
 
 def quantize_layer(W: torch.Tensor, X: torch.Tensor, block_size: int = 128, use_ssr: bool = True,
@@ -155,8 +277,9 @@ def quantize_layer(W: torch.Tensor, X: torch.Tensor, block_size: int = 128, use_
                    outputs: Optional[LayerOutput] = None) -> LayerOutput:
     """Variant M whole layer (main.py:102-230) as one fused launch sequence (pt2q_quantize_layer).
 
-    check_spd=False skips the single host read of the Cholesky status (benchmark loops; the
-    caller must then check `info` itself)."""
+    check_spd=False skips the single host read of the Cholesky and stall status (benchmark
+    loops; the caller must then check `outputs.info` and `workspace.status()` itself, e.g.
+    `check_layer_status`)."""
     W = _float_input(W)
     X = _float_input(X.reshape(-1, X.shape[-1]))
     n, m = W.shape
@@ -181,7 +304,8 @@ def quantize_layer(W: torch.Tensor, X: torch.Tensor, block_size: int = 128, use_
         _lib.stream_of(dev))
     _lib.check(rc, "pt2q_quantize_layer")
     outputs.info = info
-    if check_spd and int(info.item()) != 0:
+    outputs.status = workspace.status()
+    if check_spd and not check_layer_status(outputs, "pt2q_quantize_layer"):
         # main.py:140-141: Cholesky failed -> pinv of the damped Hessian; the raw Gram is intact.
         G = workspace.gram_view(m).clone()
         H, _ = prepare_hessian(G, N, percdamp)
@@ -190,6 +314,15 @@ def quantize_layer(W: torch.Tensor, X: torch.Tensor, block_size: int = 128, use_
         out.spd = False
         return out
     return outputs
+
+
+def check_layer_status(out: LayerOutput, what="layer") -> bool:
+    """One host read of the Cholesky status and the stall word of a quantize_layer call.
+    Raises Pt2qError on a stall; returns True when the Hessian was positive definite."""
+    info, status = (int(v) for v in torch.stack([out.info.reshape(-1)[0],
+                                                 out.status.reshape(-1)[0]]).cpu())
+    _lib.raise_stall(status, what)
+    return info == 0
 
 
 class LayerGraph:
@@ -228,7 +361,8 @@ class LayerGraph:
         return self.out
 
     def spd(self) -> bool:
-        return int(self.out.info.item()) == 0
+        """Cholesky status of the last replay; raises Pt2qError if a hand-off stalled."""
+        return check_layer_status(self.out, "LayerGraph")
 
 
 def dequantize(alpha, mu, T, perm, block_size):

@@ -55,6 +55,52 @@ def test_argument_errors_without_device(pt2q):
                               None) == E_ARG
 
 
+def test_argument_bounds_without_device(pt2q):
+    """Lengths that would overflow the kernels' 32-bit row counts and leading dimensions shorter
+    than a row are rejected before any device work (fake non-null pointers are never touched)."""
+    lib = pt2q._lib.lib()
+    E_ARG = 1
+    p = ctypes.c_void_p(4096)
+    F16, I8 = 1, 3
+    assert lib.pt2q_gram(p, F16, 2**31, 64, 64, p, 64, 0, None, 0, None) == E_ARG
+    assert lib.pt2q_gram(p, F16, 100, 64, 32, p, 64, 0, None, 0, None) == E_ARG
+    assert lib.pt2q_gram(p, F16, 100, 64, 64, p, 63, 0, None, 0, None) == E_ARG
+
+    def layer(ldw=64, N=100, ldx=64):
+        return lib.pt2q_quantize_layer(p, 0, ldw, 16, 64, p, F16, N, ldx, 32, 0x11, 0.01, 100, p, p,
+                                       p, I8, p, None, p, p, 1 << 30, None)
+    assert layer(ldw=63) == E_ARG
+    assert layer(ldx=32) == E_ARG
+    assert layer(N=2**31) == E_ARG
+    assert lib.pt2q_quantize_blocks(p, 0, 63, 16, 64, 32, 0x11, p, 64, p, 64, 100, p, p, p, I8, p,
+                                    None, p, 1 << 30, None) == E_ARG
+    assert lib.pt2q_quantize_blocks(p, 0, 64, 16, 64, 32, 0x11, p, 32, p, 64, 100, p, p, p, I8, p,
+                                    None, p, 1 << 30, None) == E_ARG
+    assert lib.pt2q_ssr_select(p, 63, 16, 64, p, 64, 32, p, p, None, p, 1 << 30, None) == E_ARG
+
+
+def test_workspace_sizes(pt2q):
+    lib = pt2q._lib.lib()
+    st = pt2q._lib.STATUS_BYTES
+    assert st == 256
+    assert lib.pt2q_strerror(pt2q._lib.PT2Q_E_STALL).decode().startswith("a cross-workgroup wait")
+    # every workspace-taking call reserves the status word first
+    assert lib.pt2q_gram_workspace_bytes(4096) >= st + 272 * 4
+    assert lib.pt2q_ssr_workspace_bytes(4096, 4096) > st + 4096 * 4096 * 5
+    # variant G blocks wider than 128 columns carry the gathered H_bb and S = H_bbᵀH_bb
+    m = 1000
+    g = lib.pt2q_layer_workspace_bytes(200, m, m, 0x20)
+    a = lib.pt2q_layer_workspace_bytes(200, m, m, 0x10)
+    assert g - a >= 2 * m * m * 4
+    # ternary inference: a prefill-sized call needs only its own split (1) of partial sums, not
+    # the decode bound of 16 (4096 tokens through an 11008 x 4096 projection: <= ~215 MB)
+    P = lib.pt2q_ternary_linear_positions(4096)
+    pre = lib.pt2q_ternary_linear_workspace_bytes(4096, 11008, 4096)
+    assert pre <= 4096 * P * 2 + 4096 * 11008 * 4 + 512
+    dec = lib.pt2q_ternary_linear_workspace_bytes(1, 4096, 4096)
+    assert dec >= P * 2 + 2 * 4096 * 4  # decode splits K
+
+
 def test_ops_refuse_cpu_tensors(pt2q):
     import torch
     with pytest.raises(pt2q._lib.Pt2qError):

@@ -17,7 +17,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("splits,m,dt", [((100, 37, 200), 96, torch.float32),
                                          ((1000, 3000, 16384), 2048, torch.float16),
-                                         ((64, 192, 2048), 256, torch.bfloat16)])
+                                         ((64, 192, 2048), 256, torch.bfloat16),
+                                         # ragged 16-bit batches: the accumulator carries the
+                                         # (< 8) remainder rows into the next batch's first group
+                                         ((13, 100, 7, 1, 333, 5), 256, torch.float16),
+                                         ((3, 2, 1, 1, 701), 200, torch.bfloat16),
+                                         ((5, 64, 3), 96, torch.float32)])
 def test_gram_continue_equals_concatenated(pt2q, splits, m, dt):
     X = synth.activations(21 + m, sum(splits), m)
     Xd = cuda(X).to(dt)

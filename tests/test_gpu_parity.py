@@ -415,3 +415,26 @@ def test_layer_headline_shape_bitexact(pt2q):
     assert np.array_equal(np.sort(p), np.arange(4096))
     T = host(out.T)
     assert set(np.unique(T)) <= {-1, 0, 1}
+
+
+@pytest.mark.parametrize("n,m,N,bs,ssr", [(384, 640, 1024, 256, True),    # blocks wider than 128
+                                          (256, 300, 512, 512, True),     # per-channel: bs >= m
+                                          (200, 700, 800, 700, False)])
+def test_gptq_wide_blocks_vs_oracle(pt2q, n, m, N, bs, ssr):
+    """Variant G with blocks wider than 128 columns: S = H_bbᵀH_bb on the f32 MFMA
+    GEMM, S1 / d in the aga_s1 order; bit-exact vs the oracle's s1_from_hess_block."""
+    W = synth.weights(600 + n, n, m)
+    X = synth.activations(601 + m, N, m, outliers=False)
+    lin = torch.nn.Linear(m, n, bias=False).to(DEV)
+    lin.weight.data = cuda(W)
+    gq = pt2q.GPTQ(lin, bs, 0.01)
+    for c in np.array_split(X, 2):
+        gq.add_batch(cuda(c))
+    alpha, mu, T, perm = gq.quantize(use_ssr=ssr)
+    Hs = np.zeros((m, m), np.float32)
+    for c in np.array_split(X, 2):
+        orc.gram_accumulate(Hs, c)
+    ref = orc.quantize_layer_g(W, Hs, N, block_size=bs, use_ssr=ssr)
+    np.testing.assert_array_equal(host(perm), ref["perm"])
+    np.testing.assert_array_equal(host(T), ref["T"])
+    assert bits_equal(host(alpha), ref["alpha"]) and bits_equal(host(mu), ref["mu"])
