@@ -1,24 +1,33 @@
-"""Benchmark: weight-columns quantized/s for the PT²-LLM ternary PTQ layer loop on MI355X.
+"""Benchmark: weight-columns quantized/s for the PT²-LLM ternary PTQ engine on MI355X.
 
-Workload (BASELINE.json metric "weight-columns quantized/sec (and s/layer) at d=4096"): one
-Llama-2-7B q_proj-shaped linear (4096 x 4096, fp16 weights) per GPU per step, calibrated on
-N = 262144 activation rows (the reference CLI default 128 samples x 2048 tokens, fp16,
-synthetic with 1 % x20 outlier channels), variant M (main.py:102-230): Gram -> damping ->
-Cholesky inverse -> 32 blocks of [SSR select -> ATQ init/ITF/AGA -> error feedback].
-Arithmetic: the Gram of the fp16 activations runs on the fp16 MFMA (f32 accumulate; the oracle
-restates its rounding); everything after it is fp32.  Inputs are resident in HBM
-before timing.
+Default workload (BASELINE.json metric "weight-columns quantized/sec (and s/layer) at d=4096;
+1/2/4/8 MI355X", config C4 "Llama-2-7B fp16, full ATQ+SSR pipeline, layers sharded across
+8×MI355X via RCCL/xGMI"): one step quantises EVERY linear of a Llama-2-7B-shaped model (32
+decoder layers x {q,k,v,o 4096x4096; gate,up 11008x4096; down 4096x11008} = 224 linears,
+1,269,760 weight columns), each calibrated on N = 262144 activation rows (the reference CLI
+default 128 samples x 2048 tokens), variant M (main.py:102-230 per linear, main.py:257-304 over
+the model).  Linears that read the same input (q/k/v, gate/up) form one work unit sharing one
+Gram and one Cholesky inverse (128 units).  With N GPUs (torchrun, one rank per GPU) the units
+are split longest-processing-time first (sharding.assign_lpt) — the total work is fixed, so the
+scaling is STRONG — and every rank's results (2-bit packed codes, scales, permutation) are
+gathered to rank 0 over RCCL inside the timed step.
 
-N>1 (torchrun, one rank per GPU): every rank quantises its own layer (weak scaling) and the
-results (2-bit packed codes, scales, permutation) are gathered to rank 0 over RCCL inside the
-timed step.
+Data: synthetic, resident in HBM before timing (fp16 weights, counter-hash, std 0.02; fp16
+activations, unit variance with 1 % x20 outlier channels).  One activation tensor per input
+width is shared by the units of that width on a rank; every unit still computes its own Gram.
+
+`extra` carries the single-layer numbers (s/layer and cols/s of the 4096x4096 q_proj layer at
+N = 262144 and N = 2048, one hipGraph replay each).  `--workload layer` times that single layer
+per rank instead (weak scaling, the round-1 bench line).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -29,55 +38,123 @@ import pt2q_loader  # noqa: E402
 pt2q = pt2q_loader.load()
 from pt2q import sharding  # noqa: E402
 
-MI355X_F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md:42 (dense f32 MFMA)
-MI355X_F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md:43 (dense fp16/bf16 MFMA, no sparsity)
-MI355X_HBM_PEAK_GBS = 8000.0
+MI355X_F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md (dense f32 MFMA)
+MI355X_F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md (dense fp16/bf16 MFMA, no sparsity)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=int, default=4096)
-    p.add_argument("--m", type=int, default=4096)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--workload", choices=["model", "layer"], default="model")
+    p.add_argument("--layers", type=int, default=32, help="decoder layers of the model workload")
+    p.add_argument("--hidden", type=int, default=4096)
+    p.add_argument("--inter", type=int, default=11008)
+    p.add_argument("--n", type=int, default=4096, help="layer workload: d_out")
+    p.add_argument("--m", type=int, default=4096, help="layer workload: d_in")
     p.add_argument("--tokens", type=int, default=262144)
     p.add_argument("--block-size", type=int, default=128)
     p.add_argument("--io-dtype", choices=["fp16", "fp32", "bf16"], default="fp16")
     p.add_argument("--no-ssr", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--eager", action="store_true", help="launch eagerly instead of hipGraph replay")
-    p.add_argument("--cpu-sample-rows", type=int, default=4096)
-    p.add_argument("--no-n2048", action="store_true",
-                   help="skip the secondary N=2048 timing (profiling: keeps only headline launches)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the single-layer / Gram extras (profiling: keeps only the step's launches)")
     return p.parse_args()
 
 
-def cpu_baseline(n, m, tokens, sample_rows, block_size, use_ssr):
-    """The CPU oracle (oracle/, C + OpenMP, kind "port") on a bounded sample of the same layer:
-    Cholesky/inverse and the whole block loop timed in full; the Gram timed on `sample_rows` of
-    the `tokens` activation rows and scaled linearly (its work is 2·N·m², exactly linear in N)."""
+def log(rank, msg):
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_model_name():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle, "port")
+
+def cpu_baseline(units, N, block_size, use_ssr, hidden):
+    """The CPU oracle (oracle/pt2q_oracle.c, plain C + OpenMP, kind "port") timed on bounded
+    samples of the d x d layer and scaled to the workload by each stage's exact work law (Gram
+    ∝ N·m², Cholesky inverse ∝ m³, block loop ∝ n·m² at a fixed block size — SSR, ATQ and the
+    error feedback are all row-local): on all host cores, and on one core with smaller samples."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
     from oracle import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    orc.set_threads(threads)
-    W = synth.weights(7, n, m)
-    X = synth.activations(8, sample_rows, m)
-    t0 = time.perf_counter()
-    G = orc.gram(X)
-    t_gram = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    H, _ = orc.prepare_hessian(G, sample_rows)
-    Hinv, _ = orc.cholesky_inverse(H)
-    orc.quantize_blocks(W, G, Hinv, block_size, use_ssr, 1)
-    t_rest = time.perf_counter() - t0
-    t_layer = t_gram * (tokens / sample_rows) + t_rest
-    return {"value": m / t_layer, "unit": "cols/s", "cores": orc.get_threads(), "kind": "port",
-            "sample": (f"oracle/pt2q_oracle.c on one {n}x{m} layer: Gram over {sample_rows} of "
-                       f"{tokens} rows ({t_gram:.2f}s, scaled x{tokens / sample_rows:.0f}), "
-                       f"Cholesky-inverse + {-(-m // block_size)}-block loop in full ({t_rest:.2f}s)"),
-            "s_per_layer": t_layer}
+    d = hidden
+    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    cols = sharding.units_cols(units)
+
+    def scaled(tg, rows, tc, cm, tb, brow):
+        tot = 0.0
+        for _, lins, Nu in units:
+            m = lins[0][2]
+            tot += tg * (Nu / rows) * (m / d) ** 2 + tc * (m / cm) ** 3
+            tot += sum(tb * (n / brow) * (m / d) ** 2 for _, n, _ in lins)
+        return tot, tg * (N / rows) + tc * (d / cm) ** 3 + tb * (d / brow)
+
+    def timed(threads, fn):
+        orc.set_threads(threads)
+        t0 = time.perf_counter()
+        r = fn()
+        dt = time.perf_counter() - t0
+        orc.set_threads(cores)
+        return r, dt
+
+    # all cores: Gram over 4096 rows, the full Cholesky inverse, the full block loop
+    rows = 4096
+    X = synth.activations(8, rows, d)
+    W = synth.weights(7, d, d)
+    G, tg = timed(cores, lambda: orc.gram(X))
+    H, _ = orc.prepare_hessian(G, rows)
+    (Hinv, _), tc = timed(cores, lambda: orc.cholesky_inverse(H))
+    _, tb = timed(cores, lambda: orc.quantize_blocks(W, G, Hinv, block_size, use_ssr, 1))
+    tot, layer = scaled(tg, rows, tc, d, tb, d)
+    res = {"value": cols / tot, "unit": "cols/s", "cores": cores, "kind": "port",
+           "sample": (f"oracle/pt2q_oracle.c, {cores} threads, on the {d}x{d} layer: Gram over {rows} "
+                      f"of {N} rows ({tg:.2f}s), Cholesky inverse ({tc:.2f}s), "
+                      f"{-(-d // block_size)}-block loop in full ({tb:.2f}s); the workload's "
+                      f"{len(units)} units = these stages scaled by N*m^2, m^3, n*m^2"),
+           "s_per_layer": layer, "s_workload": tot, "cpu_model": cpu_model_name()}
+    # one core: smaller samples of the same stages
+    rows1, cm1, br1 = 128, 2048, 256
+    _, tg1 = timed(1, lambda: orc.gram(X[:rows1]))
+    Hs = np.ascontiguousarray(H[:cm1, :cm1])  # a leading principal block of an SPD matrix is SPD
+    _, tc1 = timed(1, lambda: orc.cholesky_inverse(Hs))
+    _, tb1 = timed(1, lambda: orc.quantize_blocks(W[:br1], G, Hinv, block_size, use_ssr, 1))
+    tot1, layer1 = scaled(tg1, rows1, tc1, cm1, tb1, br1)
+    res["one_core"] = {"value": cols / tot1, "unit": "cols/s", "cores": 1, "kind": "port",
+                       "s_per_layer": layer1, "s_workload": tot1,
+                       "sample": (f"1 thread: Gram over {rows1} rows ({tg1:.2f}s), Cholesky inverse "
+                                  f"of order {cm1} ({tc1:.2f}s, x(m/{cm1})^3), block loop on {br1} "
+                                  f"of {d} rows ({tb1:.2f}s, x n/{br1}); same work-law scaling")}
+    return res
+
+
+# ------------------------------------------------------------------ helpers
+
+def gram_time_ms(X, m, reps=3):
+    """Average launch time of the symmetric Gram on X, HIP events on the launch stream (torch's
+    current stream, which pt2q_gram uses)."""
+    G = torch.empty((m, m), dtype=torch.float32, device=X.device)
+    ws = torch.empty(pt2q._lib.lib().pt2q_gram_workspace_bytes(m), dtype=torch.uint8, device=X.device)
+    pt2q.gram(X, G, workspace=ws, check=False)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        pt2q.gram(X, G, workspace=ws, check=False)
+    ev1.record()
+    torch.cuda.synchronize()
+    pt2q._lib.check_status(ws, "gram timing")
+    return ev0.elapsed_time(ev1) / reps
 
 
 def load_traffic():
@@ -86,6 +163,62 @@ def load_traffic():
         with open(path) as f:
             return json.load(f)
     return None
+
+
+class ModelStep:
+    """This rank's share of the model: resident inputs, per-width workspaces, one step."""
+
+    def __init__(self, a, rank, world, dev, io):
+        self.units = sharding.llama_units(a.layers, a.hidden, a.inter, a.tokens)
+        self.shards = sharding.assign_lpt([sharding.unit_cost(u) for u in self.units], world)
+        self.mine = self.shards[rank]
+        self.bs, self.ssr = a.block_size, not a.no_ssr
+        self.X, self.W, self.ws = {}, {}, {}
+        self.index = {u[0]: i for i, u in enumerate(self.units)}
+        for i in self.mine:
+            name, lins, N = self.units[i]
+            m = lins[0][2]
+            if m not in self.X:
+                self.X[m] = pt2q.fill_synthetic((N, m), 2000 + 97 * rank + m, std=1.0, outliers=True,
+                                                device=dev).to(io)
+                self.ws[m] = pt2q.UnitWorkspace(m, dev, self.bs)
+            for k, (p, n, _) in enumerate(lins):
+                self.W[(i, p)] = pt2q.fill_synthetic((n, m), 100_000 + 16 * i + k, std=0.02,
+                                                     device=dev).to(io)
+        torch.cuda.synchronize()
+
+    def provider(self, unit):
+        i = self.index[unit[0]]
+        _, lins, _ = unit
+        return self.X[lins[0][2]], {p: self.W[(i, p)] for p, _, _ in lins}
+
+    def run_unit(self, Ws, X):
+        return pt2q.quantize_unit(Ws, X, block_size=self.bs, use_ssr=self.ssr,
+                                  workspace=self.ws[X.shape[1]], defer=True)
+
+    def step(self):
+        res, _ = sharding.quantize_units_sharded(self.units, self.provider, run_unit=self.run_unit,
+                                                 pack=True, dst=0)
+        return res
+
+
+class LayerStep:
+    """One n x m layer per rank (weak scaling), a hipGraph replay; results gathered at N > 1."""
+
+    def __init__(self, a, rank, world, dev, io):
+        self.world = world
+        self.Wl = pt2q.fill_synthetic((a.n, a.m), 1000 + rank, std=0.02, device=dev).to(io)
+        self.Xl = pt2q.fill_synthetic((a.tokens, a.m), 2000 + rank, std=1.0, outliers=True, device=dev).to(io)
+        self.graph = pt2q.LayerGraph(self.Wl, self.Xl, a.block_size, not a.no_ssr)
+        self.units = [("layer", [("proj", a.n, a.m)], a.tokens)] * world
+
+    def step(self):
+        out = self.graph.replay()
+        if self.world > 1:
+            packed, _ = pt2q.pack_ternary(out.T)
+            sharding.gather_results({f"rank{dist.get_rank()}": {"T2": packed, "alpha": out.alpha,
+                                                                "mu": out.mu, "perm": out.perm}})
+        return out
 
 
 def main():
@@ -98,43 +231,26 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[a.io_dtype]
-    n, m, N, bs = a.n, a.m, a.tokens, a.block_size
+    N, bs, d = a.tokens, a.block_size, a.hidden
     use_ssr = not a.no_ssr
 
-    # synthetic, resident inputs (one independent layer per rank)
-    W = pt2q.fill_synthetic((n, m), 1000 + rank, std=0.02, device=dev).to(io)
-    X = pt2q.fill_synthetic((N, m), 2000 + rank, std=1.0, outliers=True, device=dev).to(io)
-    torch.cuda.synchronize()
-    ws = pt2q.LayerWorkspace(n, m, bs, dev)
-    B = -(-m // bs)
-    outs = pt2q.LayerOutput(torch.empty((n, B), device=dev), torch.empty((n, B), device=dev),
-                            torch.empty((n, m), dtype=torch.int8, device=dev),
-                            torch.empty(m, dtype=torch.int64, device=dev),
-                            torch.zeros(B, dtype=torch.int32, device=dev))
-    graph = None if a.eager else pt2q.LayerGraph(W, X, bs, use_ssr)
-
-    def step():
-        if graph is not None:
-            out = graph.replay()
-        else:
-            out = pt2q.quantize_layer(W, X, bs, use_ssr, workspace=ws, check_spd=False, outputs=outs)
-        if world > 1:
-            packed, _ = pt2q.pack_ternary(out.T)
-            sharding.gather_to_root({"T2": packed, "alpha": out.alpha, "mu": out.mu,
-                                     "perm": out.perm}, dst=0)
-        return out
-
-    for _ in range(a.warmup):
-        out = step()
-    torch.cuda.synchronize()
-    if a.warmup and int(out.info.item()) != 0:
+    t_setup = time.perf_counter()
+    work = ModelStep(a, rank, world, dev, io) if a.workload == "model" else LayerStep(a, rank, world, dev, io)
+    log(rank, f"{a.workload} inputs resident ({time.perf_counter() - t_setup:.1f}s); warmup {a.warmup}")
+    for i in range(a.warmup):
+        work.step()
+        torch.cuda.synchronize()
+        log(rank, f"warmup step {i + 1}/{a.warmup} done")
+    if a.workload == "layer" and not work.graph.spd():
         raise RuntimeError("synthetic Hessian not SPD")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for i in range(a.steps):
+        work.step()
+        if a.steps > 3:
+            log(rank, f"step {i + 1}/{a.steps}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -144,77 +260,111 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / max(a.steps, 1)
+    cols = sharding.units_cols(work.units) if a.workload == "model" else world * a.m
+    log(rank, f"timed {a.steps} steps: {ms_per_step:.1f} ms/step")
 
-    # dominant kernel: the symmetric Gram XᵀX (16-bit MFMA for fp16/bf16 X, f32 MFMA for f32 X),
-    # timed alone with HIP events on the stream it is launched on (torch's current stream)
-    G = torch.empty((m, m), dtype=torch.float32, device=dev)
-    reps = 3
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    pt2q.gram(X, G)
-    ev0.record()
-    for _ in range(reps):
-        pt2q.gram(X, G)
-    ev1.record()
-    torch.cuda.synchronize()
-    gram_ms = ev0.elapsed_time(ev1) / reps
-    gram_flops = float(N) * m * (m + 1)  # unique entries of the symmetric product, 2 flop each
-    achieved = gram_flops / (gram_ms * 1e-3) / 1e12
-
-    # secondary: s/layer at N=2048 (the survey's other d=4096 CPU reference point)
-    s_layer_2048 = float("nan")
-    X2 = X[:2048].contiguous() if not a.no_n2048 else None
-    if X2 is not None:
-        g2 = pt2q.LayerGraph(W, X2, bs, use_ssr) if not a.eager else None
-        run2 = g2.replay if g2 is not None else (
-            lambda: pt2q.quantize_layer(W, X2, bs, use_ssr, workspace=ws, check_spd=False, outputs=outs))
-        run2()
+    extra = {}
+    roof = None
+    if rank == 0 and not a.no_extra:
+        # the d=4096 q_proj layer alone (s/layer at d=4096): one hipGraph replay per layer
+        if a.workload == "model":
+            Wl = pt2q.fill_synthetic((d, d), 1000, std=0.02, device=dev).to(io)
+            Xl = work.X.get(d)
+            if Xl is None:
+                Xl = pt2q.fill_synthetic((N, d), 2000 + d, std=1.0, outliers=True, device=dev).to(io)
+            g = pt2q.LayerGraph(Wl, Xl, bs, use_ssr)
+        else:
+            Wl, Xl, g = work.Wl, work.Xl, work.graph
+        g.replay()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(5):
+            g.replay()
+        torch.cuda.synchronize()
+        s_layer = (time.perf_counter() - t1) / 5
+        if not g.spd():
+            raise RuntimeError("synthetic Hessian not SPD")
+        X2 = Xl[:2048].contiguous()
+        g2 = pt2q.LayerGraph(Wl, X2, bs, use_ssr)
+        g2.replay()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         for _ in range(5):
-            run2()
+            g2.replay()
         torch.cuda.synchronize()
         s_layer_2048 = (time.perf_counter() - t2) / 5
+        g2.spd()
+        extra.update({"s_per_layer_d4096": s_layer, "cols_per_s_layer_d4096": d / s_layer,
+                      "s_per_layer_d4096_n2048": s_layer_2048, "cols_per_s_layer_d4096_n2048": d / s_layer_2048})
+        del g, g2
+        # dominant kernel: the symmetric Gram XᵀX (16-bit MFMA for fp16/bf16 X), timed alone with
+        # HIP events per input width, averaged over the step's mix of Gram launches
+        mix = {}
+        for _, lins, Nu in work.units:
+            mix[lins[0][2]] = mix.get(lins[0][2], 0) + 1
+        launches = sum(mix.values())
+        tot_ms = tot_fl = 0.0
+        per_m = {}
+        for m, cnt in sorted(mix.items()):
+            Xm = work.X.get(m) if a.workload == "model" else work.Xl
+            if Xm is None:
+                Xm = pt2q.fill_synthetic((N, m), 2000 + m, std=1.0, outliers=True, device=dev).to(io)
+            ms = gram_time_ms(Xm, m)
+            fl = float(N) * m * (m + 1)   # unique entries of the symmetric product, 2 flop each
+            per_m[str(m)] = {"launches_per_step": cnt, "avg_launch_ms": ms, "tflops": fl / ms / 1e9}
+            tot_ms += cnt * ms
+            tot_fl += cnt * fl
+        avg_ms, avg_fl = tot_ms / launches, tot_fl / launches
+        achieved = avg_fl / (avg_ms * 1e-3) / 1e12
+        peak = MI355X_F32_MFMA_PEAK_TFLOPS if a.io_dtype == "fp32" else MI355X_F16_MFMA_PEAK_TFLOPS
+        kname = ("gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)" if a.io_dtype == "fp32" else
+                 "gram16x_kernel (symmetric Gram XᵀX: LDS-DMA staging, ds_read_b64_tr_b16, 16-bit MFMA "
+                 "32x32x16, f32 accumulate)")
+        roof = {"bound": "mfma", "kernel": kname, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": None, "avg_launch_ms": avg_ms,
+                "flops_per_launch": avg_fl, "per_width": per_m,
+                "gram_share_of_step": tot_ms / (ms_per_step * max(world, 1)) if a.workload == "model" else
+                avg_ms / ms_per_step}
+        tr = load_traffic()
+        if tr:
+            roof["traffic"] = tr.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = tr.get("source")
 
-    if a.io_dtype == "fp32":
-        kname = "gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)"
-        peak = MI355X_F32_MFMA_PEAK_TFLOPS
-    else:
-        kname = ("gram16x_kernel (symmetric Gram XᵀX: LDS-DMA staging, ds_read_b64_tr_b16, "
-                 "16-bit MFMA 32x32x16, f32 accumulate)")
-        peak = MI355X_F16_MFMA_PEAK_TFLOPS
     if rank == 0:
+        model_desc = (f"llama-2-7b shapes: {a.layers} layers x (q,k,v,o {d}x{d}; gate,up {a.inter}x{d}; "
+                      f"down {d}x{a.inter}) = {sum(len(l) for _, l, _ in work.units)} linears in "
+                      f"{len(work.units)} shared-input units" if a.workload == "model" else
+                      f"one {a.n}x{a.m} linear per rank")
         res = {
-            "metric": "weight-columns quantized/sec (d=4096 linear, 262144 calibration rows)",
-            "value": world * a.steps * m / elapsed,
+            "metric": "weight-columns quantized/sec (and s/layer) at d=4096",
+            "value": cols / (ms_per_step * 1e-3),
             "unit": "cols/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms_per_step,
-            "s_per_layer": ms_per_step / 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.workload == "model" else "weak",
             "vs_baseline": None,
             "dtype": "fp16->f32" if a.io_dtype != "fp32" else "f32",
-            "data": "synthetic (counter-hash weights std 0.02; unit-variance activations, 1% x20 outlier channels)",
-            "config": {"workload": f"llama2-7b q_proj {n}x{m}, N={N} (CLI 128x2048), variant M, "
+            "data": ("synthetic (counter-hash fp16 weights std 0.02; fp16 activations, unit variance, "
+                     "1% x20 outlier channels; one resident activation tensor per input width per rank)"),
+            "config": {"workload": f"{model_desc}, N={N} calibration rows (CLI 128x2048), variant M, "
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
-                       "n": n, "m": m, "tokens": N, "io_dtype": a.io_dtype, "block_size": bs,
-                       "parallelism": f"layer-sharded x{world}" + (", rccl gather" if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": kname,
-                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": None,
-                         "avg_launch_ms": gram_ms, "flops_per_launch": gram_flops},
-            "extra": {"s_per_layer_n2048": None if a.no_n2048 else s_layer_2048,
-                      "cols_per_s_n2048": None if a.no_n2048 else m / s_layer_2048,
-                      "gram_share_of_step": gram_ms / ms_per_step},
+                       "weight_columns_per_step": cols, "tokens": N, "io_dtype": a.io_dtype,
+                       "block_size": bs,
+                       "parallelism": (f"LPT unit sharding x{world}" if a.workload == "model" else
+                                       f"layer per rank x{world}") + (", rccl gather" if world > 1 else "")},
         }
-        tr = load_traffic()
-        if tr:
-            res["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
-            res["roofline"]["traffic_source"] = tr.get("source")
+        if a.workload == "model":
+            res["s_model"] = ms_per_step / 1e3
+        if roof is not None:
+            res["roofline"] = roof
+        res["extra"] = extra
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(n, m, N, a.cpu_sample_rows, bs, use_ssr)
+            log(rank, "cpu baseline (oracle) ...")
+            units = work.units if a.workload == "model" else [("layer", [("proj", a.n, a.m)], N)]
+            res["cpu_baseline"] = cpu_baseline(units, N, bs, use_ssr, d if a.workload == "model" else a.m)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -5,8 +5,14 @@ independent work units.  Units are assigned longest-processing-tim
 that share an input (q/k/v, gate/up) form ONE unit so they share a Gram and a Cholesky.  The only
 collective is a gather of the quantised results to the root rank over RCCL/xGMI (backend "nccl"
 is RCCL on ROCm) — 2-bit packed codes (utils.py:189-219 layout) plus scales and permutation.
+
+Reference flow replaced: main.py:257-304 (every linear of every decoder layer, one after the
+other, on the devices HF/accelerate `device_map="auto"` placed the layers on, model.py:257).
+
+Units are (name, [(proj, n, m)], N) tuples.  This module imports no device code at load time, so
+the assignment and the gather are testable on CPU with gloo.
 """
-from typing import Dict, List, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -63,3 +69,131 @@ def gather_to_root(tensors: Dict[str, torch.Tensor], dst: int = 0, group=None):
         if rank == dst:
             out[name] = bucket
     return out
+
+
+# ----------------------------------------------------------------- heterogeneous result gather
+
+_ALIGN = 16  # every entry starts 16-byte aligned, so the receiver views the bytes in place
+
+
+def _flatten(results: Dict[str, Dict[str, torch.Tensor]]):
+    """(manifest, flat uint8 tensor) of {name: {key: tensor}}: every tensor's bytes back to back
+    (each padded to 16 bytes) in sorted (name, key) order; the manifest records
+    (name, key, dtype, shape, padded nbytes)."""
+    manifest, parts = [], []
+    for name in sorted(results):
+        for key in sorted(results[name]):
+            t = results[name][key].contiguous()
+            b = t.reshape(-1).view(torch.uint8) if t.numel() else torch.empty(0, dtype=torch.uint8,
+                                                                               device=t.device)
+            pad = (-b.numel()) % _ALIGN
+            if pad:
+                b = torch.cat([b, torch.zeros(pad, dtype=torch.uint8, device=b.device)])
+            manifest.append((name, key, str(t.dtype).replace("torch.", ""), tuple(t.shape), b.numel()))
+            parts.append(b)
+    if parts:
+        flat = torch.cat(parts)
+    else:
+        flat = torch.empty(0, dtype=torch.uint8)
+    return manifest, flat
+
+
+def _unflatten(manifest, flat: torch.Tensor) -> Dict[str, Dict[str, torch.Tensor]]:
+    out: Dict[str, Dict[str, torch.Tensor]] = {}
+    o = 0
+    for name, key, dt, shape, nb in manifest:
+        dtype = getattr(torch, dt)
+        cnt = 1
+        for d in shape:
+            cnt *= d
+        used = cnt * torch.empty(0, dtype=dtype).element_size()
+        t = flat[o:o + used].view(dtype).reshape(shape)
+        out.setdefault(name, {})[key] = t
+        o += nb
+    return out
+
+
+def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, group=None):
+    """Gather heterogeneous per-rank results ({unit.linear: {key: tensor}}, any shapes/dtypes) to
+    `dst`: one small object gather of the shape manifests, then ONE size-exact byte buffer per
+    rank point-to-point (send/recv; RCCL over xGMI on GPUs, gloo on CPU).  Returns the merged dict
+    on dst (tensors on dst's device), None elsewhere."""
+    manifest, flat = _flatten(results)
+    if not dist.is_initialized():
+        return _unflatten(manifest, flat)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world == 1:
+        return _unflatten(manifest, flat)
+    manifests = [None] * world if rank == dst else None
+    dist.gather_object(manifest, manifests, dst=dst, group=group)
+    if rank != dst:
+        if flat.numel():
+            dist.send(flat, dst=dst, group=group)
+        return None
+    merged = _unflatten(manifest, flat)
+    dev = flat.device
+    ops, bufs = [], {}
+    for r in range(world):
+        if r == dst:
+            continue
+        nbytes = sum(e[4] for e in manifests[r])
+        if nbytes:
+            bufs[r] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            ops.append(dist.P2POp(dist.irecv, bufs[r], r, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for r, buf in bufs.items():
+        merged.update(_unflatten(manifests[r], buf))
+    return merged
+
+
+# ----------------------------------------------------------------- sharded model quantisation
+
+def units_cols(units) -> int:
+    """Weight columns (the metric's unit) of a list of units: Σ m over their linears."""
+    return sum(m for _, lins, _ in units for _, _, m in lins)
+
+
+def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callable] = None,
+                           block_size: int = 128, use_ssr: bool = True, percdamp: float = 0.01,
+                           pack: bool = True, dst: int = 0, group=None, gather: bool = True):
+    """Quantise a list of independent work units across the ranks of `group` (LPT shards), then
+    gather every linear's result to `dst`.
+
+    provider(unit) -> (X, {proj: W}) gives a unit's activations and weights on this rank's device
+    (called only for this rank's units).  run_unit(Ws, X) -> [LayerOutput] defaults to
+    engine.quantize_unit (Gram -> damping -> Cholesky inverse -> block loops, shared per unit).
+    Results are {f"{unit}.{proj}": {"T2" (2-bit packed, utils.py:189-219) or "T", "alpha", "mu",
+    "perm", "shape"}}.  Returns (results on dst or None, this rank's unit indices)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    shards = assign_lpt([unit_cost(u) for u in units], world)
+    mine = shards[rank]
+    if run_unit is None:
+        from . import engine  # noqa: WPS433 (device code only when quantising for real)
+
+        def run_unit(Ws, X):
+            return engine.quantize_unit(Ws, X, block_size=block_size, use_ssr=use_ssr,
+                                        percdamp=percdamp, defer=True)
+    runs = []
+    for i in mine:
+        name, lins, _ = units[i]
+        X, Wd = provider(units[i])
+        runs.append((name, [p for p, _, _ in lins], run_unit([Wd[p] for p, _, _ in lins], X)))
+    results = {}
+    for name, projs, run in runs:
+        outs = run.finish() if hasattr(run, "finish") else run
+        for p, out in zip(projs, outs):
+            r = {"alpha": out.alpha, "mu": out.mu, "perm": out.perm,
+                 "shape": torch.tensor(list(out.T.shape), dtype=torch.int64, device=out.T.device)}
+            if pack:
+                from . import engine
+                r["T2"] = engine.pack_ternary(out.T)[0]
+            else:
+                r["T"] = out.T
+            results[f"{name}.{p}"] = r
+    if not gather:
+        return results, mine
+    return gather_results(results, dst=dst, group=group), mine

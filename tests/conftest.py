@@ -34,7 +34,26 @@ def layer_inputs(g):
     X = synth.activations(int(g["xseed"]), N, m, outliers=bool(g.get("outliers", True)))
     if "zero_col" in g:
         X[:, int(g["zero_col"])] = 0.0
+    if "dtype" in g:  # 16-bit fixture: the fp32 upcast of the 16-bit tensors (what the reference ran)
+        W, X = round16(W, str(g["dtype"])), round16(X, str(g["dtype"]))
     return W, X
+
+
+def round16(a, dtype):
+    if dtype == "fp16":
+        return a.astype(np.float16).astype(np.float32)
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).bfloat16().float().numpy()
+
+
+def layer_inputs16(g):
+    """16-bit fixture inputs as the engine takes them: W (fp32 upcast, exact) and X as fp16 numpy
+    or bf16 torch -- the oracle then applies the 16-bit MFMA Gram arithmetic (orc.gram16)."""
+    W, X = layer_inputs(g)
+    if str(g["dtype"]) == "fp16":
+        return W, X.astype(np.float16)
+    import torch
+    return W, torch.from_numpy(X).bfloat16()
 
 
 def gpu_available():

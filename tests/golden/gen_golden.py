@@ -293,9 +293,38 @@ def gen_ternary():
              bias=bias.numpy(), x=x.numpy(), out=out.numpy())
 
 
+def round16(a, dtype):
+    """fp16 / bf16 rounding of an fp32 array, back in fp32 (exact: 16-bit values are fp32)."""
+    if dtype == "fp16":
+        return a.astype(np.float16).astype(np.float32)
+    return torch.from_numpy(a).bfloat16().float().numpy()
+
+
+def gen_fp16():
+    """16-bit layers (configs C3/C4 fp16, C5 bf16).  The reference cannot run fp16/bf16 through
+    its error feedback (main.py:214 dtype mismatch), so its output for a 16-bit layer
+    is the fp32-upcast layer: W and X rounded to 16 bits, then run in fp32 (every 16-bit value is
+    exact in fp32).  The HIP path takes the 16-bit tensors themselves (16-bit MFMA Gram)."""
+    print("16-bit-input layer fixtures (variant M, fp32-upcast reference)")
+    cases = [
+        ("layer_m16_512x512_n2048", "fp16", 512, 512, 2048, 128),
+        ("layer_m16_1024x768_n2048", "fp16", 1024, 768, 2048, 128),
+        ("layer_m16_768x3072_n2048", "fp16", 768, 3072, 2048, 128),
+        ("layer_m16_bf16_640x1024_pc", "bf16", 640, 1024, 1024, 1024),
+    ]
+    for name, dt, n, m, N, bs in cases:
+        ws, xs = 5 + n, 6 + m
+        W = round16(synth.weights(ws, n, m), dt)
+        X = round16(synth.activations(xs, N, m), dt)
+        r = ref_layer_m(W, X, True, bs)
+        save(name, variant="M", dtype=dt, n=n, m=m, N=N, wseed=ws, xseed=xs, outliers=True,
+             use_ssr=True, block_size=bs, alpha=r["alpha"].numpy(), mu=r["mu"].numpy(),
+             T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
+
+
 GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
               "trace": gen_trace, "examples": gen_examples, "wide": gen_wide,
-              "ternary": gen_ternary}
+              "ternary": gen_ternary, "fp16": gen_fp16}
 
 if __name__ == "__main__":
     # `python gen_golden.py [group ...]` regenerates only the named groups (default: all)

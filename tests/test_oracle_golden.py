@@ -7,7 +7,7 @@ sizes where the reference is itself reproducible.
 import numpy as np
 import pytest
 
-from conftest import golden_names, layer_inputs, load_golden
+from conftest import golden_names, layer_inputs, layer_inputs16, load_golden
 from oracle import oracle as orc
 
 SCALE_TOL = 1e-5
@@ -63,6 +63,22 @@ def test_layer_variant_m(name):
     g = load_golden(name)
     W, X = layer_inputs(g)
     out = orc.quantize_layer_m(W, X, block_size=int(g["block_size"]), use_ssr=bool(g["use_ssr"]))
+    assert out["spd"]
+    if name in NEAR_TIE_LAYERS:
+        _check_layer_sets(g, out, int(g["block_size"]))
+    else:
+        _check_layer(g, out)
+
+
+@pytest.mark.parametrize("name", golden_names("layer_m16_"))
+def test_layer_variant_m_16bit(name):
+    """16-bit layers (configs C3/C4 fp16, C5 bf16 per-channel): the oracle with the 16-bit MFMA
+    Gram arithmetic (orc.gram16: what the HIP path computes) against the reference's
+    fp32-upcast run of the same 16-bit values (main.py:128-139 after X.float())."""
+    g = load_golden(name)
+    W, X16 = layer_inputs16(g)
+    orc.set_threads(8)
+    out = orc.quantize_layer_m(W, X16, block_size=int(g["block_size"]), use_ssr=True)
     assert out["spd"]
     if name in NEAR_TIE_LAYERS:
         _check_layer_sets(g, out, int(g["block_size"]))

@@ -3,6 +3,7 @@ and the gather of per-rank results to rank 0 (bench.py's N>1 step uses the same 
 RCCL)."""
 import os
 import socket
+import zlib
 
 import pytest
 import torch
@@ -83,3 +84,104 @@ def test_gather_to_root_world2():
         gen = torch.Generator().manual_seed(r)
         torch.randint(0, 3, (16, 40), generator=gen)
         assert torch.equal(got["perm"][r], torch.randperm(40, generator=gen))
+
+
+class _FakeOut:
+    """A LayerOutput stand-in (CPU): deterministic from (n, m, seed)."""
+
+    def __init__(self, n, m, seed, bs=128):
+        g = torch.Generator().manual_seed(seed)
+        B = -(-m // bs)
+        self.alpha = torch.rand((n, B), generator=g)
+        self.mu = torch.rand((n, B), generator=g)
+        self.T = (torch.randint(0, 3, (n, m), generator=g) - 1).to(torch.int8)
+        self.perm = torch.randperm(m, generator=g)
+
+
+def _mixed_units():
+    # qkv-like (3 x 64x48), o-like, gate/up-like (2 x 96x48) and down-like (48x96) units:
+    # heterogeneous shapes and linear counts per unit
+    return [("l0.qkv", [("q_proj", 64, 48), ("k_proj", 64, 48), ("v_proj", 64, 48)], 256),
+            ("l0.o", [("o_proj", 64, 48)], 256),
+            ("l0.gate_up", [("gate_proj", 96, 48), ("up_proj", 96, 48)], 256),
+            ("l0.down", [("down_proj", 48, 96)], 256),
+            ("l1.down", [("down_proj", 48, 96)], 256)]
+
+
+def _fake_run(units):
+
+    def provider(unit):
+        name, lins, _ = unit
+        return None, {p: (name, p, n, m) for p, n, m in lins}
+
+    def run_unit(Ws, X):
+        return [_FakeOut(n, m, zlib.crc32(f"{name}.{p}".encode()) % 10007) for (name, p, n, m) in Ws]
+    return provider, run_unit
+
+
+def _worker_mixed(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = _sharding()
+    units = _mixed_units()
+    provider, run_unit = _fake_run(units)
+    res, mine = sh.quantize_units_sharded(units, provider, run_unit=run_unit, pack=False, dst=0)
+    q.put(("mine", rank, mine))
+    if rank == 0:
+        # numpy copies: tensors shared through the queue would need this process alive
+        q.put(("res", 0, {k: {f: t.numpy().copy() for f, t in v.items()} for k, v in res.items()}))
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_sharded_units_heterogeneous_gather_world2():
+    """quantize_units_sharded over 2 gloo ranks with mixed unit shapes (qkv-like 3 x 64x48,
+    gate/up-like, down-like 48x96): every linear's result reaches rank 0 intact, each unit runs
+    on exactly one rank (the LPT shard), and the shapes ride along in the manifest."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mixed, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    mine = {}
+    for _ in range(3):
+        kind, r, v = q.get(timeout=90)
+        if kind == "res":
+            got = v
+        else:
+            mine[r] = v
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    units = _mixed_units()
+    sh = _sharding()
+    assert sorted(mine[0] + mine[1]) == list(range(len(units)))
+    assert mine == {r: s for r, s in enumerate(sh.assign_lpt([sh.unit_cost(u) for u in units], 2))}
+    want_names = {f"{name}.{p}" for name, lins, _ in units for p, _, _ in lins}
+    assert set(got) == want_names
+    for name, lins, _ in units:
+        for p, n, m in lins:
+            ref = _FakeOut(n, m, zlib.crc32(f"{name}.{p}".encode()) % 10007)
+            r = {f: torch.from_numpy(a) for f, a in got[f"{name}.{p}"].items()}
+            assert r["T"].dtype == torch.int8 and tuple(r["T"].shape) == (n, m)
+            assert torch.equal(r["T"], ref.T) and torch.equal(r["perm"], ref.perm)
+            assert torch.equal(r["alpha"], ref.alpha) and torch.equal(r["mu"], ref.mu)
+            assert r["shape"].tolist() == [n, m]
+    assert sh.units_cols(units) == 3 * 48 + 48 + 2 * 48 + 96 + 96
+
+
+def test_flatten_roundtrip_cpu():
+    sh = _sharding()
+    res = {"b": {"x": torch.arange(6, dtype=torch.int64).reshape(2, 3), "e": torch.empty(0)},
+           "a": {"y": torch.tensor([1.5, -2.0]), "z": torch.tensor([[1, -1]], dtype=torch.int8)}}
+    man, flat = sh._flatten(res)
+    back = sh._unflatten(man, flat)
+    for k, v in res.items():
+        for f, t in v.items():
+            assert back[k][f].dtype == t.dtype and torch.equal(back[k][f], t)
