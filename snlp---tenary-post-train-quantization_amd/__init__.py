@@ -5,7 +5,8 @@ Drop-in for the reference's hot-path surface:
     compute_column_similarity_to_mean, select_next_block_ssr                      (reorder.py)
     GPTQ, GPTQQuantizer                                                            (gptq.py)
     PT2LLMQuantizer.quantize_layer                                                 (main.py)
-    pack_ternary, unpack_ternary, save/load_quantized_model                        (utils.py)
+    pack_ternary, unpack_ternary, save/load_quantized_model,
+    compute_bits_per_weight                                                        (utils.py)
     TernaryLinear, replace_linear_with_ternary                                     (model.py)
 All compute runs in libpt2q.so (HIP, gfx950); importing fails loudly if it is not built.
 """
@@ -16,8 +17,8 @@ from .gptq import GPTQ, GPTQQuantizer
 from .pt2llm import PT2LLMQuantizer
 from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_llm_layers,
                           quantize_decoder_layer)
-from .ternary import (TernaryLinear, load_quantized_model, replace_linear_with_ternary,
-                      save_quantized_model)
+from .ternary import (TernaryLinear, compute_bits_per_weight, load_quantized_model,
+                      replace_linear_with_ternary, save_quantized_model)
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, UnitRun, UnitWorkspace, cholesky_inverse,
                      dequantize, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
                      quantize_blocks, quantize_layer, quantize_shared, quantize_unit, unpack_ternary)
@@ -31,5 +32,5 @@ __all__ = [
     "unpack_ternary", "fill_synthetic", "hessian_inverse", "quantize_shared", "GramAccumulator",
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
     "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
-    "UnitRun", "UnitWorkspace", "quantize_unit",
+    "UnitRun", "UnitWorkspace", "quantize_unit", "compute_bits_per_weight",
 ]

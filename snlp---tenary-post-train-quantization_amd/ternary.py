@@ -145,6 +145,25 @@ def replace_linear_with_ternary(model: nn.Module, quantized_params: Dict[str, Di
     return model
 
 
+def compute_bits_per_weight(model: nn.Module, include_scales: bool = True) -> float:
+    """utils.py:251-285: average bits per weight over the ternary layers of `model` -- log2(3)
+    rounded to 1.58 bits per code plus 16 bits per alpha / mu entry; 16.0 when the model has no
+    ternary layer (the reference finds none after its own CLI run).  Host
+    arithmetic on buffer sizes only."""
+    total_params = 0
+    total_bits = 0.0
+    for _, module in model.named_modules():
+        if hasattr(module, "T"):  # TernaryLinear (the reference's duck test)
+            nw = module.T.numel()
+            total_params += nw
+            total_bits += nw * 1.58
+            if include_scales:
+                total_bits += (module.alpha.numel() + module.mu.numel()) * 16
+    if total_params == 0:
+        return 16.0
+    return total_bits / total_params
+
+
 def save_quantized_model(model: nn.Module, save_path: str,
                          quantized_params: Dict[str, Dict[str, torch.Tensor]]):
     """utils.py:288-296 (same file layout)."""

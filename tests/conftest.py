@@ -46,6 +46,12 @@ def round16(a, dtype):
     return torch.from_numpy(np.ascontiguousarray(a)).bfloat16().float().numpy()
 
 
+def unpack2(T2, m):
+    """tests/golden/gen_golden.py pack2 inverse: n x ceil(2m/8) bytes -> int8 codes n x m."""
+    bits = np.unpackbits(T2, axis=1)[:, :2 * m].reshape(T2.shape[0], m, 2)
+    return (bits[..., 0].astype(np.int16) * 2 + bits[..., 1] - 1).astype(np.int8)
+
+
 def layer_inputs16(g):
     """16-bit fixture inputs as the engine takes them: W (fp32 upcast, exact) and X as fp16 numpy
     or bf16 torch -- the oracle then applies the 16-bit MFMA Gram arithmetic (orc.gram16)."""

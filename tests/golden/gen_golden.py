@@ -309,7 +309,8 @@ def gen_fp16():
     cases = [
         ("layer_m16_512x512_n2048", "fp16", 512, 512, 2048, 128),
         ("layer_m16_1024x768_n2048", "fp16", 1024, 768, 2048, 128),
-        ("layer_m16_768x3072_n2048", "fp16", 768, 3072, 2048, 128),
+        # (768 x 3072 and 1024 x 2048: see gen_loop16 -- whole-layer results there depend on
+        # H⁻¹ rounding, so the loop is pinned with the engine's H⁻¹)
         ("layer_m16_bf16_640x1024_pc", "bf16", 640, 1024, 1024, 1024),
     ]
     for name, dt, n, m, N, bs in cases:
@@ -322,9 +323,116 @@ def gen_fp16():
              T=r["T"].numpy().astype(np.int8), perm=r["perm"].numpy())
 
 
+def pack2(T):
+    """int8 codes {-1,0,1} (n x m) -> 2 bits each, row-wise, MSB first (conftest.unpack2)."""
+    c = (T.astype(np.int16) + 1).astype(np.uint8)
+    bits = (c[..., None] >> np.array([1, 0], np.uint8)) & 1
+    return np.packbits(bits.reshape(T.shape[0], -1), axis=1)
+
+
+def ref_loop_with_hinv(W, X, Hinv, bs=128):
+    """main.py:158-230 driven by the reference's own components (reorder.select_next_block_ssr,
+    quantizer.AsymmetricTernaryQuantizer.quantize, the error feedback of main.py:199-214) with a
+    GIVEN H⁻¹ in place of main.py:136-141.  gen_trace checks this restatement against
+    quantize_layer bit-for-bit when H⁻¹ is the reference's own."""
+    W = torch.from_numpy(W.copy())
+    X = torch.from_numpy(X.copy())
+    H_inv = torch.from_numpy(Hinv)
+    n, m = W.shape
+    atq = rq.AsymmetricTernaryQuantizer()
+    rem = torch.arange(m)
+    T_full = torch.zeros(n, m, dtype=torch.int8)
+    alphas, mus, perm = [], [], []
+    while len(rem) > 0:
+        blk, rem = rr.select_next_block_ssr(W, rem, bs)
+        Wb = W[:, blk]
+        a, mu, Tb = atq.quantize(Wb, X[:, blk])
+        T_full[:, blk] = Tb.to(torch.int8)
+        alphas.append(a); mus.append(mu); perm += blk.tolist()
+        E = Wb - (a * Tb + mu)
+        if len(rem) > 0:
+            C = H_inv[blk][:, rem] / H_inv[blk, blk].unsqueeze(1).clamp(min=1e-8)
+            W[:, rem] -= E @ C
+    return dict(alpha=torch.cat(alphas, 1).numpy(), mu=torch.cat(mus, 1).numpy(), T=T_full.numpy(),
+                perm=np.array(perm, np.int64))
+
+
+def gen_loop16():
+    """Full-size block-loop pins for 16-bit layers whose whole-layer result depends on H⁻¹
+    rounding (d >= 3k: a different but equally valid fp32 inverse -- MKL's vs the engine's
+    canonical chains, rel. diff ~1e-4 -- moves SSR picks from block ~4 on).  The reference's
+    own loop components run on the fp32 upcast of the 16-bit tensors with the ENGINE's H⁻¹ (the
+    CPU oracle's orc.gram16 -> prepare_hessian -> cholesky_inverse, which the HIP path matches
+    bit-for-bit); H⁻¹ itself is pinned to the reference separately (hess_* fixtures)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import oracle as orc
+    orc.set_threads(8)
+    print("16-bit block-loop fixtures (reference loop, engine H^-1)")
+    for name, dt, n, m, N in (("loop16_768x3072_n2048", "fp16", 768, 3072, 2048),
+                              ("loop16_1024x2048_n2048", "fp16", 1024, 2048, 2048)):
+        ws, xs = 7 + n, 8 + m
+        W = round16(synth.weights(ws, n, m), dt)
+        X = round16(synth.activations(xs, N, m), dt)
+        G = orc.gram16(X.astype(np.float16))
+        H, _ = orc.prepare_hessian(G, N)
+        Hinv, spd = orc.cholesky_inverse(H)
+        assert spd
+        r = ref_loop_with_hinv(W, X, Hinv)
+        save(name, variant="M", dtype=dt, n=n, m=m, N=N, wseed=ws, xseed=xs, outliers=True,
+             use_ssr=True, block_size=128, alpha=r["alpha"], mu=r["mu"],
+             T2=pack2(r["T"]),
+             perm=r["perm"])
+
+
+TINY_LLAMA = dict(vocab_size=512, hidden_size=256, intermediate_size=384, num_hidden_layers=2,
+                  num_attention_heads=4, num_key_value_heads=4, max_position_embeddings=256)
+
+
+def tiny_llama_and_samples():
+    """A 2-layer Llama built from config (no download) with torch.manual_seed(0), fp32, and three
+    64-token calibration samples (torch.manual_seed(1)).  tests/test_gpu_model.py rebuilds the
+    same model and samples and checks the state-dict checksum stored with the fixture."""
+    import transformers
+    cfg = transformers.LlamaConfig(**TINY_LLAMA)
+    torch.manual_seed(0)
+    model = transformers.LlamaForCausalLM(cfg).eval()
+    torch.manual_seed(1)
+    samples = [torch.randint(0, TINY_LLAMA["vocab_size"], (1, 64)) for _ in range(3)]
+    return model, samples
+
+
+def state_checksum(model):
+    return np.array([float(p.detach().double().sum()) for p in model.state_dict().values()])
+
+
+def gen_model():
+    """The reference's model-level loop PT2LLMQuantizer.quantize (main.py:232-311): hooks,
+    calibration forwards, quantize_layer per linear and the _dequantize_weight write-back
+    (main.py:313-335, wrong under SSR -- SURVEY §0.5), with get_calibration_data overridden on
+    the instance (the reference downloads wikitext; there is no network)."""
+    print("model-loop fixture (2-layer Llama, main.py:232-311)")
+    model, samples = tiny_llama_and_samples()
+    csum = state_checksum(model)
+    q = rm.PT2LLMQuantizer(model, None, model_type="llama", block_size=128, use_ssr=True,
+                           device="cpu")
+    q.get_calibration_data = lambda: samples
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        params = q.quantize()
+    kw = {"checksum": csum, "names": np.array(sorted(params))}
+    for i, name in enumerate(sorted(params)):
+        p = params[name]
+        kw[f"alpha{i}"] = p["alpha"].numpy()
+        kw[f"mu{i}"] = p["mu"].numpy()
+        kw[f"T2_{i}"] = pack2(p["T"].numpy())
+        kw[f"perm{i}"] = p["perm"].numpy()
+        kw[f"m{i}"] = p["T"].shape[1]
+    save("model_llama2l", **kw)
+
+
 GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
               "trace": gen_trace, "examples": gen_examples, "wide": gen_wide,
-              "ternary": gen_ternary, "fp16": gen_fp16}
+              "ternary": gen_ternary, "fp16": gen_fp16, "loop16": gen_loop16,
+              "model": gen_model}
 
 if __name__ == "__main__":
     # `python gen_golden.py [group ...]` regenerates only the named groups (default: all)

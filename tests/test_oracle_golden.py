@@ -7,7 +7,7 @@ sizes where the reference is itself reproducible.
 import numpy as np
 import pytest
 
-from conftest import golden_names, layer_inputs, layer_inputs16, load_golden
+from conftest import golden_names, layer_inputs, layer_inputs16, load_golden, unpack2
 from oracle import oracle as orc
 
 SCALE_TOL = 1e-5
@@ -84,6 +84,23 @@ def test_layer_variant_m_16bit(name):
         _check_layer_sets(g, out, int(g["block_size"]))
     else:
         _check_layer(g, out)
+
+
+@pytest.mark.parametrize("name", golden_names("loop16_"))
+def test_block_loop_16bit_full_size(name):
+    """The whole block loop (24 / 16 blocks, SSR + ATQ + error feedback) of a 16-bit layer vs the
+    reference's own loop components fed the same H⁻¹ (gen_golden.gen_loop16): codes and
+    permutation bit-exact, scales within 1e-5.  (Whole-layer parity at this size is limited by
+    the H⁻¹ rounding itself, MKL's vs the canonical chains -- DESIGN.md §6.)"""
+    g = load_golden(name)
+    W, X16 = layer_inputs16(g)
+    orc.set_threads(8)
+    out = orc.quantize_layer_m(W, X16, block_size=int(g["block_size"]), use_ssr=True)
+    assert out["spd"]
+    np.testing.assert_array_equal(out["perm"], g["perm"])
+    np.testing.assert_array_equal(out["T"].astype(np.int8), unpack2(g["T2"], W.shape[1]))
+    check_scales(out["alpha"], g["alpha"], "alpha")
+    check_scales(out["mu"], g["mu"], "mu")
 
 
 @pytest.mark.parametrize("name", golden_names("layer_g_"))
