@@ -142,6 +142,17 @@ int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const int64_t* re
                     int64_t* blk, int64_t* newrem, float* sim, void* workspace,
                     size_t workspace_bytes, void* stream);
 
+/* One block's GPTQ error feedback, in place (main.py:187-214, gptq.py:158-186):
+ *   C = Hinv[blk][:, rem] / clamp(diag(Hinv)[blk], 1e-8);  W[:, rem] -= E @ C
+ * W n x m fp32 row-major (updated), blk: bs int64, rem: r int64 (the columns still to quantise),
+ * E: n x bs fp32 (the block's quantisation error W_b - (alpha*T + mu)), Hinv m x m.  The product
+ * is rounded before the subtraction, as in the reference.  pt2q_quantize_blocks runs the same
+ * kernels inside its loop. */
+size_t pt2q_error_feedback_workspace_bytes(int n, int m, int bs);
+int pt2q_error_feedback(float* W, int64_t ldw, int n, int m, const int64_t* blk, int bs,
+                        const int64_t* rem, int r, const float* E, int64_t lde, const float* Hinv,
+                        int64_t ldhi, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Reconstruct W_q[:, perm[kb:(k+1)b]] = alpha[:,k] * T + mu[:,k] (gptq.py:201-230). T int8 or
  * fp32 (tdtype), out fp32 n x m. */
 int pt2q_dequantize(const float* alpha, const float* mu, const void* T, int tdtype,

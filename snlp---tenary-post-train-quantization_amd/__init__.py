@@ -20,7 +20,7 @@ from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_
 from .ternary import (TernaryLinear, compute_bits_per_weight, load_quantized_model,
                       replace_linear_with_ternary, save_quantized_model)
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, UnitRun, UnitWorkspace, cholesky_inverse,
-                     dequantize, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
+                     dequantize, error_feedback, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
                      quantize_blocks, quantize_layer, quantize_shared, quantize_unit, unpack_ternary)
 
 __version__ = "0.1.0"
@@ -32,5 +32,5 @@ __all__ = [
     "unpack_ternary", "fill_synthetic", "hessian_inverse", "quantize_shared", "GramAccumulator",
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
     "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
-    "UnitRun", "UnitWorkspace", "quantize_unit", "compute_bits_per_weight",
+    "UnitRun", "UnitWorkspace", "quantize_unit", "compute_bits_per_weight", "error_feedback",
 ]

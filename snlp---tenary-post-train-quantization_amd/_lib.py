@@ -58,6 +58,8 @@ _SIGS = {
     "pt2q_s1_from_gram": (I, [P, I64, I, P, P, P]),
     "pt2q_ssr_select": (I, [P, I64, I, I, P, I, I, P, P, P, P, SZ, P]),
     "pt2q_dequantize": (I, [P, P, P, I, P, I, I, I, P, P]),
+    "pt2q_error_feedback_workspace_bytes": (SZ, [I, I, I]),
+    "pt2q_error_feedback": (I, [P, I64, I, I, P, I, P, I, P, I64, P, I64, P, SZ, P]),
     "pt2q_pack_ternary": (I, [P, I64, P, P]),
     "pt2q_unpack_ternary": (I, [P, I64, P, P]),
     "pt2q_fill_synthetic": (I, [P, I64, ctypes.c_uint64, F, I64, I, F, P]),
@@ -125,6 +127,20 @@ def require_device(t):
         raise Pt2qError("pt2q kernels need tensors on a HIP device (MI355X); got "
                         f"{getattr(t, 'device', type(t))}")
     return t.device
+
+
+def compute_device(*tensors):
+    """The HIP device the kernels run on for the reference-surface classes: the inputs' own
+    device if any is on a GPU, else the current HIP device (a reference-style caller passing CPU
+    tensors gets its results back on the CPU -- the arithmetic still runs in libpt2q on the GPU).
+    With no HIP device present this raises: there is no CPU path."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return t.device
+    if not torch.cuda.is_available():
+        raise Pt2qError("pt2q kernels need an MI355X (HIP device); none is visible and there is "
+                        "no CPU path")
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def workspace(nbytes, device):

@@ -470,3 +470,64 @@ extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const 
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
+
+// ---- standalone error feedback (main.py:187-214 / gptq.py:158-186 for one block)
+extern "C" size_t pt2q_error_feedback_workspace_bytes(int n, int m, int bs) {
+  if (n <= 0 || m <= 0 || bs <= 0) return 0;
+  Carve c{nullptr, 0};
+  c.dry = true;
+  const long ldW = round_up(n, 64);
+  c.take<int>(PT2Q_STATUS_BYTES / sizeof(int));
+  c.take<float>((size_t)m * ldW);
+  c.take<float>((size_t)bs * ldW);
+  c.take<float>((size_t)bs * round_up(m, 4));
+  c.take<int>((size_t)bs);
+  c.take<int>((size_t)m);
+  return c.used;
+}
+
+extern "C" int pt2q_error_feedback(float* W, int64_t ldw, int n, int m, const int64_t* blk, int bs,
+                                   const int64_t* rem, int r, const float* E, int64_t lde,
+                                   const float* Hinv, int64_t ldhi, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!W || !blk || !E || !Hinv || n <= 0 || m <= 0 || bs <= 0 || r < 0 || bs + r > m ||
+      ldw < m || lde < bs || ldhi < m || (r > 0 && !rem))
+    return PT2Q_E_ARG;
+  if (r == 0) return PT2Q_OK;
+  Carve c{(char*)workspace, workspace_bytes};
+  int rc;
+  take_status(c, st, rc);  // reserved (nothing in this call waits on another workgroup)
+  if (rc != PT2Q_OK) return rc;
+  const long ldW = round_up(n, 64), ldc = round_up(m, 4);
+  float* Wt = c.take<float>((size_t)m * ldW);
+  float* Et = c.take<float>((size_t)bs * ldW);
+  float* Ck = c.take<float>((size_t)bs * ldc);
+  int* blk32 = c.take<int>((size_t)bs);
+  int* rem32 = c.take<int>((size_t)m);
+  if (!c.ok) return PT2Q_E_WORKSPACE;
+  // feature-major working copies: column gathers W[:, rem] become row gathers of Wt
+  if ((rc = pt2q_launch_transpose_to_f32(W, PT2Q_F32, ldw, n, m, Wt, ldW, st)) != PT2Q_OK) return rc;
+  if ((rc = pt2q_launch_transpose_to_f32(E, PT2Q_F32, lde, n, bs, Et, ldW, st)) != PT2Q_OK) return rc;
+  hipLaunchKernelGGL(i64_to_i32_kernel, dim3(ceil_div(bs, 256)), dim3(256), 0, st, blk, bs, blk32);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(i64_to_i32_kernel, dim3(ceil_div(r, 256)), dim3(256), 0, st, rem, r, rem32);
+  PT2Q_LAUNCH_CHECK();
+  // C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k], 1e-8)   (main.py:201-209)
+  if ((rc = pt2q_launch_ef_coeffs(Hinv, ldhi, blk32, bs, rem32, r, Ck, ldc, st)) != PT2Q_OK) return rc;
+  // W[:, rem] -= E @ C   (main.py:214: product rounded, then one subtraction)
+  rc = pt2q_tuning().ef_kernel ? pt2q_launch_ef(Ck, ldc, Et, Wt, ldW, m, rem32, r, bs, st)
+                               : PT2Q_E_UNSUPPORTED;
+  if (rc == PT2Q_E_UNSUPPORTED) {
+    GemmDesc g{};
+    g.M = r; g.N = n; g.K = bs;
+    g.A = Ck; g.lda = ldc; g.a_layout = LAY_KMAJOR;
+    g.B = Et; g.ldb = ldW; g.b_layout = LAY_KMAJOR;
+    g.in_dtype = PT2Q_F32;
+    g.C = Wt; g.ldc = ldW; g.crow = rem32;
+    g.mode = GEMM_SUB;
+    rc = pt2q_launch_gemm(g, st);
+  }
+  if (rc != PT2Q_OK) return rc;
+  return pt2q_launch_transpose_f32(Wt, ldW, m, n, W, ldw, st);
+}

@@ -365,6 +365,29 @@ class LayerGraph:
         return check_layer_status(self.out, "LayerGraph")
 
 
+def error_feedback(W: torch.Tensor, blk: torch.Tensor, rem: torch.Tensor, E: torch.Tensor,
+                   Hinv: torch.Tensor) -> torch.Tensor:
+    """main.py:187-214 for one block, in place on fp32 W (n x m):
+    W[:, rem] -= E @ (Hinv[blk][:, rem] / clamp(Hinv[blk, blk], 1e-8))."""
+    _lib.require_device(W)
+    if W.dtype != torch.float32 or not W.is_contiguous():
+        raise _lib.Pt2qError("error_feedback updates a contiguous fp32 W in place")
+    n, m = W.shape
+    blk = blk.to(device=W.device, dtype=torch.int64).contiguous()
+    rem = rem.to(device=W.device, dtype=torch.int64).contiguous()
+    E = E.to(device=W.device, dtype=torch.float32).contiguous()
+    Hinv = Hinv.to(device=W.device, dtype=torch.float32).contiguous()
+    bs, r = blk.numel(), rem.numel()
+    if E.shape != (n, bs) or Hinv.shape != (m, m):
+        raise ValueError("error_feedback: E must be n x len(blk) and Hinv m x m")
+    ws = _lib.workspace(_lib.lib().pt2q_error_feedback_workspace_bytes(n, m, max(bs, 1)), W.device)
+    _lib.check(_lib.lib().pt2q_error_feedback(_lib.ptr(W), m, n, m, _lib.ptr(blk), bs, _lib.ptr(rem), r,
+                                              _lib.ptr(E), bs, _lib.ptr(Hinv), m, _lib.ptr(ws),
+                                              ws.numel(), _lib.stream_of(W.device)),
+               "pt2q_error_feedback")
+    return W
+
+
 def dequantize(alpha, mu, T, perm, block_size):
     """Correct reconstruction W_q[:, perm[k*b:(k+1)*b]] = alpha[:,k]*T + mu[:,k] (gptq.py:201-230)."""
     n, m = T.shape

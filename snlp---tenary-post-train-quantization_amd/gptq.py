@@ -28,8 +28,10 @@ class GPTQ:
         self.dtype = layer.weight.dtype
         W = layer.weight.data
         self.rows, self.columns = W.shape
-        _lib.require_device(W)
-        self.H = torch.zeros((self.columns, self.columns), device=self.device, dtype=torch.float32)
+        # the kernels' device: the layer's own, or the current HIP device for a CPU layer (the
+        # reference's CPU call shape; results are returned on the layer's device)
+        self._dev = _lib.compute_device(W)
+        self.H = torch.zeros((self.columns, self.columns), device=self._dev, dtype=torch.float32)
         self.nsamples = 0
         self.alpha = None
         self.mu = None
@@ -41,7 +43,7 @@ class GPTQ:
         """gptq.py:59-76: H += inpᵀ inp; nsamples += rows."""
         if inp.dim() == 3:
             inp = inp.reshape(-1, inp.shape[-1])
-        engine.gram(inp.to(self.device), self.H, accumulate=True)
+        engine.gram(inp.to(self._dev), self.H, accumulate=True)
         self.nsamples += inp.shape[0]
 
     def quantize(self, use_ssr: bool = True) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -50,14 +52,14 @@ class GPTQ:
             raise RuntimeError("GPTQ.quantize: no calibration data (call add_batch first)")
         H, _ = engine.prepare_hessian(self.H, self.nsamples, self.percdamp)
         Hinv, spd = engine.cholesky_inverse(H)
-        out = engine.quantize_blocks(self.layer.weight.data, H, Hinv, self.block_size, use_ssr,
-                                     _lib.AGA_HESS, 100, torch.float32)
+        out = engine.quantize_blocks(self.layer.weight.data.to(self._dev), H, Hinv, self.block_size,
+                                     use_ssr, _lib.AGA_HESS, 100, torch.float32)
         out.spd = spd
         self.last_output = out
-        self.alpha = out.alpha.to(self.dtype)
-        self.mu = out.mu.to(self.dtype)
-        self.T = out.T.to(self.dtype)
-        self.perm = out.perm
+        self.alpha = out.alpha.to(self.device, self.dtype)
+        self.mu = out.mu.to(self.device, self.dtype)
+        self.T = out.T.to(self.device, self.dtype)
+        self.perm = out.perm.to(self.device)
         return self.alpha, self.mu, self.T, self.perm
 
     def get_quantized_weight(self) -> torch.Tensor:
@@ -65,7 +67,9 @@ class GPTQ:
         if self.T is None:
             raise RuntimeError("Must call quantize() first")
         bs = self.block_size if self.block_size < self.columns else self.columns
-        return engine.dequantize(self.alpha, self.mu, self.T, self.perm, bs).to(self.dtype)
+        d = self._dev
+        return engine.dequantize(self.alpha.to(d), self.mu.to(d), self.T.to(d), self.perm.to(d),
+                                 bs).to(self.device, self.dtype)
 
 
 class GPTQQuantizer:

@@ -76,10 +76,13 @@ class PT2LLMQuantizer:
             calibration_samples = self.get_calibration_data()
         layers = calibration.get_llm_layers(self.model, self.model_type)
         self.model.eval()
+        # the calibration forwards run wherever the model lives (main.py:281 moves samples to the
+        # model's device); captured inputs stream to the GPU Grams either way
+        model_dev = next(self.model.parameters()).device
         for idx, layer in enumerate(layers):
             def run(cap):
                 for sample in calibration_samples:
-                    self.model(sample.to(self.device))
+                    self.model(sample.to(model_dev))
                     cap.next_pass()
             res = calibration.quantize_decoder_layer(layer, run, self.block_size, self.use_ssr,
                                                      self.percdamp, idx, writeback, self.device)

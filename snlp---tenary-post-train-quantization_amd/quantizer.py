@@ -4,6 +4,8 @@ Every method runs one HIP kernel of libpt2q (pt2q_atq_stage, atq.hip); results a
 to the CPU oracle and match the reference's codes exactly (tests/test_gpu_parity.py).
 Inputs are computed in fp32: fp16/bf16 weights are upcast (exact) and outputs cast back to the
 weight dtype (the reference itself overflows fp16 in `d = 1ᵀS1`, quantizer.py:218 — SURVEY §0.2).
+CPU tensors (the reference's own call shape) are computed on the current HIP device and the
+results returned on the CPU; with no HIP device the call raises (_lib.compute_device).
 """
 from typing import Optional, Tuple
 
@@ -12,8 +14,8 @@ import torch
 from . import _lib
 
 
-def _dev_f32(t):
-    _lib.require_device(t)
+def _dev_f32(t, dev):
+    t = t.to(dev)
     return t.contiguous().float() if t.dtype != torch.float32 else t.contiguous()
 
 
@@ -30,12 +32,13 @@ class AsymmetricTernaryQuantizer:
 
     # --------------------------------------------------------------- helpers
     def _stage(self, mode, W, alpha=None, mu=None, T=None, S1=None, d=None):
-        Wf = _dev_f32(W)
+        dev = _lib.compute_device(W)
+        Wf = _dev_f32(W, dev)
         n, b = Wf.shape
-        dev = Wf.device
         a = torch.empty(n, dtype=torch.float32, device=dev) if alpha is None else _col(alpha, n, dev).clone()
         m = torch.empty(n, dtype=torch.float32, device=dev) if mu is None else _col(mu, n, dev).clone()
-        Tt = torch.empty((n, b), dtype=torch.float32, device=dev) if T is None else T.float().contiguous().clone()
+        Tt = (torch.empty((n, b), dtype=torch.float32, device=dev) if T is None
+              else T.to(dev).float().contiguous().clone())
         iters = torch.zeros(1, dtype=torch.int32, device=dev)
         ws = _lib.workspace(256, dev)
         rc = _lib.lib().pt2q_atq_stage(
@@ -46,10 +49,11 @@ class AsymmetricTernaryQuantizer:
         return a, m, Tt, iters
 
     def _out(self, W, a, m, T=None):
+        """Results in W's dtype, on W's device (CPU in -> CPU out)."""
         n = a.shape[0]
-        res = (a.view(n, 1).to(W.dtype), m.view(n, 1).to(W.dtype))
+        res = (a.view(n, 1).to(W.device, W.dtype), m.view(n, 1).to(W.device, W.dtype))
         if T is not None:
-            res = res + (T.to(W.dtype),)
+            res = res + (T.to(W.device, W.dtype),)
         return res
 
     @staticmethod
@@ -57,8 +61,7 @@ class AsymmetricTernaryQuantizer:
         """S = XᵀX (quantizer.py:207), S1 = S·1 (:216), d = 1ᵀS1 (:218) on the device."""
         if X.dim() == 3:
             X = X.reshape(-1, b)
-        _lib.require_device(X)
-        X = X.contiguous()
+        X = X.to(_lib.compute_device(X)).contiguous()
         if X.dtype not in (torch.float32, torch.float16, torch.bfloat16):
             X = X.float()
         dev = X.device
@@ -89,7 +92,8 @@ class AsymmetricTernaryQuantizer:
         return T.to(W.dtype)
 
     def iterative_ternary_fitting(self, W, alpha, mu, T):
-        """quantizer.py:136-175 (whole-block convergence semantics)."""
+        """quantizer.py:136-175 (whole-block convergence semantics).  `last_itf_iters` holds the
+        iteration count (device int32)."""
         a, m, Tn, it = self._stage(_lib.STAGE_ITF, W, alpha=alpha, mu=mu, T=T)
         self.last_itf_iters = it
         return self._out(W, a, m, Tn)
@@ -105,6 +109,7 @@ class AsymmetricTernaryQuantizer:
         """quantizer.py:250-277: init -> ITF -> AGA (if X) in one fused kernel."""
         S1 = d = None
         if X is not None:
+            X = X.to(_lib.compute_device(W, X))
             S1, d = self.s1_from_activations(X, W.shape[1])
         a, m, T, it = self._stage(_lib.STAGE_FULL, W, S1=S1, d=d)
         self.last_itf_iters = it

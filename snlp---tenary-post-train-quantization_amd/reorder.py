@@ -2,7 +2,8 @@
 
 One call = the similarity of every remaining column to the remaining-column mean plus the
 ordered top-k (ssr.hip).  Ties (equal similarity) resolve to the lower position in
-`remaining_indices`; torch.topk leaves that order unspecified.
+`remaining_indices`; torch.topk leaves that order unspecified.  CPU inputs (the reference's call
+shape) are computed on the current HIP device and returned on the CPU.
 """
 from typing import Tuple
 
@@ -12,10 +13,9 @@ from . import _lib
 
 
 def _ssr_call(W, remaining_indices, block_size, want_sim):
-    _lib.require_device(W)
-    Wf = W.contiguous().float()
+    dev = _lib.compute_device(W, remaining_indices)  # CPU callers: computed on the GPU
+    Wf = W.to(dev).contiguous().float()
     n, m = Wf.shape
-    dev = Wf.device
     rem = remaining_indices.to(device=dev, dtype=torch.int64).contiguous()
     r = rem.numel()
     bs = min(block_size, r)
@@ -33,7 +33,7 @@ def _ssr_call(W, remaining_indices, block_size, want_sim):
 def compute_column_similarity_to_mean(W: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
     """reorder.py:36-61: cosine similarity of each W[:, indices] column to their mean."""
     _, _, sim = _ssr_call(W, indices, 1, True)
-    return sim.to(W.dtype)
+    return sim.to(W.device, W.dtype)
 
 
 def select_next_block_ssr(W: torch.Tensor, remaining_indices: torch.Tensor,
@@ -43,5 +43,5 @@ def select_next_block_ssr(W: torch.Tensor, remaining_indices: torch.Tensor,
         return remaining_indices, torch.tensor([], dtype=remaining_indices.dtype,
                                                device=remaining_indices.device)
     blk, newrem, _ = _ssr_call(W, remaining_indices, block_size, False)
-    dt = remaining_indices.dtype
-    return blk.to(dt), newrem.to(dt)
+    dt, dv = remaining_indices.dtype, remaining_indices.device
+    return blk.to(dv, dt), newrem.to(dv, dt)

@@ -105,3 +105,15 @@ def test_ops_refuse_cpu_tensors(pt2q):
     import torch
     with pytest.raises(pt2q._lib.Pt2qError):
         pt2q.gram(torch.zeros(4, 4))
+
+
+def test_reference_surface_fails_loudly_without_gpu(pt2q):
+    """The class surface takes CPU tensors (the reference's call shape) but computes on the GPU;
+    on a machine without one it raises instead of falling back to a CPU path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    with pytest.raises(pt2q._lib.Pt2qError):
+        pt2q.AsymmetricTernaryQuantizer().quantize(torch.zeros(4, 128))
+    with pytest.raises(pt2q._lib.Pt2qError):
+        pt2q.select_next_block_ssr(torch.zeros(4, 300), torch.arange(300), 128)

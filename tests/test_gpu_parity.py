@@ -438,3 +438,52 @@ def test_gptq_wide_blocks_vs_oracle(pt2q, n, m, N, bs, ssr):
     np.testing.assert_array_equal(host(perm), ref["perm"])
     np.testing.assert_array_equal(host(T), ref["T"])
     assert bits_equal(host(alpha), ref["alpha"]) and bits_equal(host(mu), ref["mu"])
+
+
+@pytest.mark.parametrize("n,m,bs", [(300, 700, 128), (256, 1024, 256), (64, 200, 37)])
+def test_error_feedback_entry_vs_oracle(pt2q, n, m, bs):
+    """pt2q_error_feedback (main.py:187-214 for one block, standalone C entry) vs the oracle's
+    orc_error_feedback: bit-exact W after the update; rem in arbitrary (non-sorted) order."""
+    rng = np.random.default_rng(n + m)
+    W = synth.weights(700 + n, n, m)
+    cols = rng.permutation(m)
+    blk, rem = cols[:bs].astype(np.int64), cols[bs:].astype(np.int64)
+    E = synth.weights(701 + n, n, bs) * np.float32(0.1)
+    X = synth.activations(702 + m, 2 * m, m)
+    H, _ = orc.prepare_hessian(orc.gram(X), 2 * m)
+    Hinv, spd = orc.cholesky_inverse(H)
+    assert spd
+    Wd = cuda(W)
+    pt2q.error_feedback(Wd, cuda(blk), cuda(rem), cuda(E), cuda(Hinv))
+    ref = orc.error_feedback(W, blk, rem, E, Hinv)
+    assert bits_equal(host(Wd), ref)
+    assert bits_equal(host(Wd)[:, blk], W[:, blk])  # the block's own columns are untouched
+
+
+def test_reference_call_shapes_with_cpu_tensors(pt2q):
+    """The reference runs these on CPU tensors; here they compute on the GPU and hand results
+    back on the caller's device, identical to the GPU-tensor call."""
+    W = synth.weights(810, 256, 384)
+    X = synth.activations(811, 300, 384)
+    q = pt2q.AsymmetricTernaryQuantizer()
+    a_c, m_c, T_c = q.quantize(torch.from_numpy(W[:, :128].copy()), torch.from_numpy(X[:, :128].copy()))
+    a_g, m_g, T_g = q.quantize(cuda(W[:, :128]), cuda(X[:, :128]))
+    assert a_c.device.type == "cpu" and T_c.device.type == "cpu"
+    assert bits_equal(a_c.numpy(), host(a_g)) and np.array_equal(T_c.numpy(), host(T_g))
+    rem = torch.arange(384)
+    blk, new = pt2q.select_next_block_ssr(torch.from_numpy(W), rem, 128)
+    assert blk.device.type == "cpu" and new.device.type == "cpu"
+    rblk, rnew = orc.select_next_block_ssr(W, rem.numpy(), 128)
+    np.testing.assert_array_equal(blk.numpy(), rblk)
+    np.testing.assert_array_equal(new.numpy(), rnew)
+    lin = torch.nn.Linear(384, 256, bias=False)
+    lin.weight.data = torch.from_numpy(W.copy())
+    gq = pt2q.GPTQ(lin, 128, 0.01)
+    gq.add_batch(torch.from_numpy(X.copy()))
+    alpha, mu, T, perm = gq.quantize()
+    assert alpha.device.type == "cpu" and perm.device.type == "cpu"
+    Hs = orc.gram(X)
+    ref = orc.quantize_layer_g(W, Hs, X.shape[0])
+    np.testing.assert_array_equal(perm.numpy(), ref["perm"])
+    np.testing.assert_array_equal(T.numpy(), ref["T"])
+    assert gq.get_quantized_weight().device.type == "cpu"
