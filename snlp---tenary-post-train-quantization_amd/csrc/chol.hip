@@ -7,9 +7,10 @@
 //                        j in [k,i) of Uinv[k][j]*U[j][i]) / U[i][i]
 //   Hinv = Uinv·Uinvᵀ:   Hinv[i][k] = j-ascending chain over j >= max(i,k) of Uinv[i][j]*Uinv[k][j]
 //
-// Blocked right-looking with NB = 64 panels; the trailing updates and the triangular products
-// run on the f32-MFMA GEMM (gemm.hip) whose k-ordered chains keep every element bit-identical
-// to the unblocked definition above (oracle/pt2q_oracle.c).
+// Blocked right-looking with NB = 64 blocks inside panels of CP = 512 / 1024 rows; the strip updates
+// inside a panel run on the rank-<=128 kernel (gemm.hip), the panel-wide updates and lauum on
+// the LDS-DMA f32 GEMM (gemmx.hip).  Their k-ordered chains keep every element bit-identical to
+// the unblocked definition above (oracle/pt2q_oracle.c).
 #include <cstdlib>
 
 #include "common.hpp"
@@ -119,10 +120,12 @@ PT2Q_DEV void chol_panel(float* A, long lda, int p0, int nb, int m, int bid,
 }
 
 // In-block part of the triangular inverse for column block [c0, c0+nb): rows k < c0+nb.
-// Ui[k][c0..] holds the running chains for k < c0 (zero otherwise).  Four lanes share a row.
+// The inverse is kept TRANSPOSED, UiT[i][k] = Uinv[k][i] (lower triangular), so that every
+// product that reads it has K-major operands (gemmx.hip).  UiT[c0..][k] holds the running chains
+// for k < c0 (zero otherwise).  Four lanes share a row k of Uinv.
 // For rows inside the block, columns left of the diagonal start at zero and only ever receive
 // zero terms, so they need no mask until the final store.
-PT2Q_DEV void trtri_load(const float* Ui, long ldi, int c0, int nb, int bid, float (&acc)[SEG]) {
+PT2Q_DEV void trtri_load(const float* UiT, long ldi, int c0, int nb, int bid, float (&acc)[SEG]) {
   const int k = (bid * (int)blockDim.x + (int)threadIdx.x) / LPR;
   const int sub = threadIdx.x & (LPR - 1);
   const bool valid = k < c0 + nb;
@@ -130,7 +133,7 @@ PT2Q_DEV void trtri_load(const float* Ui, long ldi, int c0, int nb, int bid, flo
   for (int s = 0; s < SEG; ++s) {
     int q = sub * SEG + s;
     const bool in = valid && k < c0 && q < nb;
-    acc[s] = Ui[in ? (long)k * ldi + c0 + q : 0];  // branch-free loads
+    acc[s] = UiT[in ? (long)(c0 + q) * ldi + k : 0];  // branch-free loads; Uinv[k][c0+q]
     acc[s] = in ? acc[s] : 0.0f;
   }
 }
@@ -166,7 +169,7 @@ PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float 
 #pragma unroll
   for (int s = 0; s < SEG; ++s) {
     int q = sub * SEG + s;
-    if (q < nb) Ui[(long)k * ldi + c0 + q] = (q >= jb) ? acc[s] : 0.0f;
+    if (q < nb) Ui[(long)(c0 + q) * ldi + k] = (q >= jb) ? acc[s] : 0.0f;  // UiT[c0+q][k]
   }
 }
 
@@ -217,24 +220,36 @@ GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int 
   return g;
 }
 
-// Ui[0 .. c0+nb, c0+nb ..] chains += Ui[:, block J] · U[block J, c0+nb ..] (terms j in J).
-GemmDesc trtri_desc(const float* U, float* Ui, long ld, int c0, int nb, int rest) {
+// Inverse chains of columns [c1, c1 + cols) (rows of UiT), over rows k < nk of Uinv, get the terms
+// j in [j0, j0 + K) (ascending):  UiT[c][k] += sum_j U[j][c] * UiT[j][k].
+GemmDesc trtri_desc(const float* U, float* UiT, long ld, int j0, int K, int c1, int cols, int nk) {
   GemmDesc g{};
-  g.M = c0 + nb; g.N = rest; g.K = nb;
-  g.A = Ui + c0; g.lda = ld; g.a_layout = LAY_ROWMAJOR;                    // (k, j) = Ui[k][c0+j]
-  g.B = U + (long)c0 * ld + c0 + nb; g.ldb = ld; g.b_layout = LAY_KMAJOR;  // (j, i) = U[c0+j][c0+nb+i]
+  g.M = cols; g.N = nk; g.K = K;
+  g.A = U + (long)j0 * ld + c1; g.lda = ld; g.a_layout = LAY_KMAJOR;   // (c, j) = U[j0+j][c1+c]
+  g.B = UiT + (long)j0 * ld; g.ldb = ld; g.b_layout = LAY_KMAJOR;      // (j, k) = UiT[j0+j][k]
   g.in_dtype = PT2Q_F32;
-  g.C = Ui + c0 + nb; g.ldc = ld;
+  g.C = UiT + (long)c1 * ld; g.ldc = ld;
   g.mode = GEMM_CHAIN_POS;
   return g;
 }
 
+// Large chain GEMMs (panel-wide updates, lauum): the LDS-DMA kernel where it applies and pays.
+int launch_big(const GemmDesc& g, hipStream_t st) {
+  const long tiles = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128) / (g.upper ? 2 : 1);
+  if (tiles >= 64 && g.K >= 128) {
+    const int rc = pt2q_launch_gemmx(g, st);
+    if (rc != PT2Q_E_UNSUPPORTED) return rc;
+  }
+  return pt2q_launch_gemm(g, st);
+}
+
 }  // namespace
 
-// One stream, three launches per 64-wide block J: diagonal factor; panel solve + in-block
-// triangular inverse; trailing update + triangular-inverse update (grouped GEMM).  The inverse
-// Uinv = U^-1 is built right-looking by column blocks as soon as rows of block J are final, so
-// no second stream (and no cross-queue dependency in a captured graph) is needed.
+// One stream: per 64-wide block J a panel solve + in-block triangular inverse launch and a strip
+// update launch (which also factors the next diagonal block); per 512- or 1024-row panel two rank-512 or -1024
+// updates.  The inverse (kept transposed, UiT) is built right-looking by column blocks as soon
+// as rows of block J are final, so no second stream (and no cross-queue dependency in a
+// captured graph) is needed.
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
                                  float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form) {
   const long ld = m;  // U and Ui are packed m x m
@@ -260,46 +275,43 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };
-  // Blocks go in pairs (J, J+1): after J only block row J+1 gets J's terms (it is all the next
-  // factor needs); after J+1 the rest of the trailing triangle gets the terms of both blocks in
-  // one rank-128 pass (k ascending, so every chain is the one-block-at-a-time chain), which
-  // halves the passes over the trailing matrix.  Each update launch also factors the diagonal
-  // block it produces (the workgroup of that tile, from its registers: chol_diag.hpp), so no
-  // launch of its own sits between an update and the next panel.
+  // Panels of CP rows: inside a panel, 64-blocks right-looking restricted to the panel (the
+  // block's rows of U solved across the full width; the panel's later rows of U and later
+  // columns of the inverse get the block's terms by rank-64 strip updates, whose first tile is
+  // the next diagonal block, factored in the same launch); after the panel, ONE rank-CP update of
+  // the trailing U triangle and one of the inverse columns to the right (gemmx).  Every chain
+  // still takes its terms in ascending k: earlier panels' bulk terms, then this panel's blocks.
+  const int tp = pt2q_tuning().chol_panel;
+  const int CP = tp >= NB ? tp / NB * NB : (m > 6144 ? 1024 : 512);  // panel rows (multiple of NB)
   bool factored = false;
-  for (int p0 = 0; p0 < m;) {
-    const int nb = (m - p0 < NB) ? m - p0 : NB;
-    if ((rc = factor(p0, nb, factored)) != PT2Q_OK) return rc;
-    const int rest = m - p0 - nb;
-    if (rest <= 0) break;
-    const int p1 = p0 + nb, nb1 = (rest < NB) ? rest : NB, rest1 = rest - nb1;
-    if (rest1 <= 0 || !pt2q_tuning().chol_pair) {  // one plain update
-      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, rest, p1, rest),
-                                  trtri_desc(U, Ui, ld, p0, nb, rest), st, U, ld, p1, nb1, info,
-                                  &factored)) != PT2Q_OK)
+  for (int P0 = 0; P0 < m; P0 += CP) {
+    const int Pend = (m - P0 < CP) ? m : P0 + CP;
+    for (int p0 = P0; p0 < Pend; p0 += NB) {
+      const int nb = (Pend - p0 < NB) ? Pend - p0 : NB;
+      if ((rc = factor(p0, nb, factored)) != PT2Q_OK) return rc;
+      factored = false;
+      const int p1 = p0 + nb;
+      if (p1 >= Pend) break;
+      const int nb1 = (Pend - p1 < NB) ? Pend - p1 : NB;
+      // U rows [p1, Pend) x columns [p1, m) and inverse columns [p1, Pend) x rows [0, p1)
+      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, Pend - p1, p1, m - p1, false),
+                                  trtri_desc(U, Ui, ld, p0, nb, p1, Pend - p1, p1), st, U, ld, p1,
+                                  nb1, info, &factored)) != PT2Q_OK)
         return rc;
-      p0 = p1;
-      continue;
     }
-    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, nb1, p1, rest, false),
-                                trtri_desc(U, Ui, ld, p0, nb, rest), st, U, ld, p1, nb1, info,
-                                &factored)) != PT2Q_OK)
-      return rc;
-    if ((rc = factor(p1, nb1, factored)) != PT2Q_OK) return rc;
-    const int p2 = p1 + nb1, nb2 = (rest1 < NB) ? rest1 : NB;
-    if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb + nb1, p2, rest1, p2, rest1),
-                                trtri_desc(U, Ui, ld, p1, nb1, rest1), st, U, ld, p2, nb2, info,
-                                &factored)) != PT2Q_OK)
-      return rc;
-    p0 = p2;
+    if (Pend >= m) break;
+    const int K = Pend - P0, rest = m - Pend;
+    if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend, rest, Pend, rest), st)) != PT2Q_OK) return rc;
+    if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend, rest, Pend), st)) != PT2Q_OK) return rc;
   }
-  // Hinv = Uinv Uinvᵀ (upper tiles, mirrored)
+  // Hinv = Uinv Uinvᵀ (upper tiles, mirrored): Hinv[i][k] = chain over j >= max(i, k) of
+  // UiT[j][i] * UiT[j][k]
   GemmDesc g{};
   g.M = m; g.N = m; g.K = m;
-  g.A = Ui; g.lda = ld; g.a_layout = LAY_ROWMAJOR;   // (i, j) = Ui[i][j]
-  g.B = Ui; g.ldb = ld; g.b_layout = LAY_ROWMAJOR;   // (j, k) = Ui[k][j]
+  g.A = Ui; g.lda = ld; g.a_layout = LAY_KMAJOR;   // (i, j) = UiT[j][i]
+  g.B = Ui; g.ldb = ld; g.b_layout = LAY_KMAJOR;   // (j, k) = UiT[j][k]
   g.in_dtype = PT2Q_F32;
   g.C = Hinv; g.ldc = ldhi;
   g.mode = GEMM_STORE; g.upper = 1; g.mirror = 1; g.kstart_diag = 2;
-  return pt2q_launch_gemm(g, st);
+  return launch_big(g, st);
 }

@@ -62,6 +62,9 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
 int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, float* dA = nullptr,
                       long dld = 0, int dp0 = 0, int dnb = 0, int* info = nullptr,
                       bool* fused = nullptr);
+// f32 chain GEMM with K-major operands, LDS-DMA staged (gemmx.hip); E_UNSUPPORTED if the desc
+// does not fit it (then use pt2q_launch_gemm)
+int pt2q_launch_gemmx(const GemmDesc& g, hipStream_t st);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
 // status (nullable): the caller's status word for stall reports (else a word of the flag area)
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);
