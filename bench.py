@@ -326,8 +326,10 @@ def main():
                 "gram_share_of_step": tot_ms / (ms_per_step * max(world, 1)) if a.workload == "model" else
                 avg_ms / ms_per_step}
         tr = load_traffic()
-        if tr:
-            roof["traffic"] = tr.get("hbm_bytes_per_launch")
+        if tr and "per_width" in tr and all(str(m) in tr["per_width"] for m in mix):
+            # PMC fabric bytes per launch of each width, averaged over the step's launch mix
+            pw = tr["per_width"]
+            roof["traffic"] = sum(cnt * pw[str(m)]["fabric_bytes_per_launch"] for m, cnt in mix.items()) / launches
             roof["traffic_source"] = tr.get("source")
 
     if rank == 0:
