@@ -116,7 +116,9 @@ def main():
           "fabric bytes = FETCH_SIZE x 2 + WRITE_SIZE (KB x 1024; L2 <-> fabric, Infinity-Cache hits "
           "included); MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
           "clock = GRBM_GUI_ACTIVE / 8 / duration.  Durations are those of the PMC runs (serialised "
-          "dispatches).", ""]
+          "dispatches).  For short kernels (tens of µs) GRBM_GUI_ACTIVE also counts the dispatch's "
+          "ramp-up and drain, so their GHz column reads above the real clock and their MFMA-busy "
+          "fraction is a lower bound; the long kernels (Gram, gemmx) give the true figures.", ""]
     for wl, desc in WORKLOADS.items():
         L += [f"### {wl}: {desc}", "", "| kernel | dispatches | avg µs | fabric MB | GB/s | MFMA busy | GHz |",
               "|---|---|---|---|---|---|---|"]
