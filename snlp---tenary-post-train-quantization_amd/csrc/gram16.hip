@@ -38,28 +38,30 @@ constexpr int GX_DMA_PER_STAGE = 12;        // LDS-DMA wave-instructions per wav
 
 __device__ uint4 gx_zero16;  // the source of out-of-range chunks (zero-initialised)
 
-// Upper tiles of the 128 x 256 grid (tile (ti, tj) exists iff ti <= 2tj + 1), ordered by
-// super-blocks of (2SJ) x SJ tiles (column-block major over super-blocks, column major inside
-// one), so that a contiguous run of the order -- one XCD's share -- covers a compact square of
-// G and its workgroups read few distinct panels of X through their common L2.
+// Upper tiles of the BM x BN grid (BN = RATIO * BM; tile (ti, tj) exists iff ti < RATIO (tj + 1))
+// ordered by super-blocks of (RATIO SJ) x SJ tiles (column-block major over super-blocks, column
+// major inside one), so that a contiguous run of the order -- one XCD's share -- covers a
+// compact square of G and its workgroups read few distinct panels of X through their common L2.
+template <int RATIO>
 PT2Q_DEV int gx_col_count(int tj, int lo, int hi) {  // tiles ti in [lo, hi) of column tj
-  return max(0, min(hi, 2 * tj + 2) - lo);
+  return max(0, min(hi, RATIO * (tj + 1)) - lo);
 }
 
+template <int RATIO>
 PT2Q_DEV void gx_tile(int a, int TI, int TJ, int SJ, int& ti, int& tj) {
-  const int SI = 2 * SJ;
+  const int SI = RATIO * SJ;
   for (int J = 0; J * SJ < TJ; ++J) {
     const int tj1 = min(TJ, (J + 1) * SJ);
     for (int I = 0; I * SI < TI; ++I) {
       const int lo = I * SI, hi = min(TI, lo + SI);
       int c = 0;
-      for (int t = J * SJ; t < tj1; ++t) c += gx_col_count(t, lo, hi);
+      for (int t = J * SJ; t < tj1; ++t) c += gx_col_count<RATIO>(t, lo, hi);
       if (a >= c) {
         a -= c;
         continue;
       }
       for (int t = J * SJ; t < tj1; ++t) {
-        const int ct = gx_col_count(t, lo, hi);
+        const int ct = gx_col_count<RATIO>(t, lo, hi);
         if (a < ct) {
           ti = lo + a;
           tj = t;
@@ -72,12 +74,76 @@ PT2Q_DEV void gx_tile(int a, int TI, int TJ, int SJ, int& ti, int& tj) {
   ti = tj = 0;  // unreachable for a < gx_ntile
 }
 
-long gx_ntile(int m) {
-  const int TI = ceil_div(m, GX_BM), TJ = ceil_div(m, GX_BN);
+long gx_ntile(int TI, int TJ, int ratio) {
   long s = 0;
-  for (int t = 0; t < TJ; ++t) s += std::min(2 * t + 2, TI);
+  for (int t = 0; t < TJ; ++t) s += std::min(ratio * (t + 1), TI);
   return s;
 }
+long gx_ntile(int m) { return gx_ntile(ceil_div(m, GX_BM), ceil_div(m, GX_BN), GX_BN / GX_BM); }
+
+// The work split of both 16-bit Gram kernels over one workgroup per CU.
+// D data-parallel waves first: in wave v workgroup w = x + NG*r takes whole tile
+// v*grid + x*R + r, so the R workgroups of one XCD run 32 neighbouring tiles of the order at the
+// same k and share their X panels through that XCD's L2.  The rest of the tile line (stream-K)
+// is cut into NG contiguous groups; group x is worked by workgroups w = x, x + NG, x + 2NG, ...
+// (R of them), which on the round-robin dispatch share an XCD and so its L2 (speed only).
+// Inside a group, team r/P takes rows [team*L, (team+1)*L) of the group's line of cnt * Kp rows
+// (units of P tiles): tail piece first (chains from the start of its last unit), full units,
+// then the head piece of its first unit, continuing the partial that the same member of the
+// previous team (w - P*NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
+// P = 2: the line is cut into tile pairs (2j, 2j+1), which share their column block tj, and
+// workgroups r = 2i, 2i+1 (a team) walk the same stretch of pairs in step, one tile of each
+// pair apiece, so the X panel of tj is fetched into L2 once for both.
+struct GxSched {
+  long base, t0;
+  int D, R, P, x, r, mem, Kp, a0, a1, k0, k1, f0, npieces;
+  bool head, tail;
+
+  PT2Q_DEV GxSched(long ntile, int Kp_, int NG, int R_, int P_, int D_) : D(D_), R(R_), P(P_), Kp(Kp_) {
+    const int w = blockIdx.x;
+    x = w % NG;
+    r = w / NG;
+    base = (long)D * gridDim.x;  // first stream-K tile
+    mem = r % P;
+    const int team = r / P, nteam = R / P;
+    const long npair = max(0l, (ntile - base) / P);
+    t0 = P * (npair * x / NG);
+    const long cnt = npair * (x + 1) / NG - npair * x / NG;
+    const long W = cnt * Kp;
+    const long L = (R == 0) ? Kp : ((W + nteam - 1) / nteam + GX_BK - 1) / GX_BK * GX_BK;
+    const long s = (long)team * L, e = min(s + L, W);
+    a0 = (int)(s / Kp);
+    k0 = (int)(s % Kp);
+    a1 = (int)((e - 1) / Kp);
+    k1 = (int)(e - (long)a1 * Kp);
+    head = k0 > 0;
+    tail = k1 < Kp && !(head && a1 == a0);
+    f0 = head ? a0 + 1 : a0;
+    const int f1 = tail ? a1 - 1 : a1;
+    const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
+    npieces = (s >= e || npair == 0) ? 0 : (tail ? 1 : 0) + nfull + (head ? 1 : 0);
+  }
+
+  // piece pc in [-D, npieces): global tile a (flags are per tile), rows [kb, ke), and whether it
+  // continues a partial that another workgroup publishes
+  PT2Q_DEV void piece(int pc, int& a, int& kb, int& ke, bool& from_partial) const {
+    from_partial = false;
+    if (pc < 0) {
+      a = (pc + D) * (int)gridDim.x + x * R + r;
+      kb = 0;
+      ke = Kp;
+      return;
+    }
+    if (tail && pc == 0) {
+      a = a1; kb = 0; ke = k1;
+    } else if (head && pc == npieces - 1) {
+      a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
+    } else {
+      a = f0 + pc - (tail ? 1 : 0); kb = 0; ke = Kp;
+    }
+    a = (int)(base + t0) + P * a + mem;
+  }
+};
 
 template <bool DMA>
 PT2Q_DEV void gx_copy16(const uint16_t* X, long ld, int gk, int kend, int gd, int M, uint8_t* blk,
@@ -298,59 +364,22 @@ struct GxTile {
   }
 };
 
-// g: M = N = m, K = rows, A = X (ld lda), C = G (ldc), mode STORE / ADD / CHAIN_POS.
-// D data-parallel waves first: in wave v workgroup w = x + NG*r takes whole tile
-// v*grid + x*R + r, so the R workgroups of one XCD run 32 neighbouring tiles of the order at the
-// same k and share their X panels through that XCD's L2.  The rest of the tile line (stream-K)
-// is cut into NG contiguous groups; group x is worked by workgroups w = x, x + NG, x + 2NG, ...
-// (R of them), which on the round-robin dispatch share an XCD and so its L2 (speed only).
-// Inside a group, team r/P takes rows [team*L, (team+1)*L) of the group's line of cnt * Kp rows
-// (units of P tiles): tail piece first (chains from the start of its last unit), full units,
-// then the head piece of its first unit, continuing the partial that the same member of the
-// previous team (w - P*NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
+// g: M = N = m, K = rows, A = X (ld lda), C = G (ldc), mode STORE / ADD / CHAIN_POS; the split:
+// GxSched.
 template <bool BF16, bool DMA>
 __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ, int SJ, int Kp, long ntile, int NG,
                                                       int R, int P, int D, int* flags, int* status,
                                                       long cap) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[GX_LDS];
   const uint16_t* X = (const uint16_t*)g.A;
-  const int w = blockIdx.x;
-  const int x = w % NG, r = w / NG;
-  const long base = (long)D * gridDim.x;  // first stream-K tile
-  // P = 2: the line is cut into tile pairs (2j, 2j+1), which share their column block tj, and
-  // workgroups r = 2i, 2i+1 (a team) walk the same stretch of pairs in step, one tile of each
-  // pair apiece, so the X panel of tj is fetched into L2 once for both.
-  const int mem = r % P, team = r / P, nteam = R / P;
-  const long npair = (ntile - base) / P;
-  const long t0 = P * (npair * x / NG), cnt = npair * (x + 1) / NG - npair * x / NG;
-  const long W = cnt * Kp;
-  const long L = (R == 0) ? Kp : ((W + nteam - 1) / nteam + GX_BK - 1) / GX_BK * GX_BK;
-  const long s = (long)team * L, e = min(s + L, W);
-  const int a0 = (int)(s / Kp), k0 = (int)(s % Kp);
-  const int a1 = (int)((e - 1) / Kp), k1 = (int)(e - (long)a1 * Kp);
-  const bool head = k0 > 0;
-  const bool tail = k1 < Kp && !(head && a1 == a0);
-  const int f0 = head ? a0 + 1 : a0, f1 = tail ? a1 - 1 : a1;
-  const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
-  const int npieces = s >= e ? 0 : (tail ? 1 : 0) + nfull + (head ? 1 : 0);
+  const GxSched S(ntile, Kp, NG, R, P, D);
   const bool vec4 = ((uintptr_t)g.C % 16 == 0) && (g.ldc % 4 == 0);
-  for (int pc = -D; pc < npieces; ++pc) {
+  for (int pc = -D; pc < S.npieces; ++pc) {
     int a, kb, ke;
-    bool from_partial = false;
-    if (pc < 0) {
-      a = (pc + D) * (int)gridDim.x + x * R + r; kb = 0; ke = Kp;
-    } else {
-      if (tail && pc == 0) {
-        a = a1; kb = 0; ke = k1;
-      } else if (head && pc == npieces - 1) {
-        a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
-      } else {
-        a = f0 + pc - (tail ? 1 : 0); kb = 0; ke = Kp;
-      }
-      a = (int)(base + t0) + P * a + mem;  // global tile index (flags are per tile)
-    }
+    bool from_partial;
+    S.piece(pc, a, kb, ke, from_partial);
     int ti, tj;
-    gx_tile(a, TI, TJ, SJ, ti, tj);
+    gx_tile<GX_BN / GX_BM>(a, TI, TJ, SJ, ti, tj);
     const int i0 = ti * GX_BM, j0 = tj * GX_BN;
     GxTile F;
     if (from_partial && threadIdx.x == 0) {
@@ -414,6 +443,349 @@ __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ
   }
 }
 
+// ---- 256 x 256 tiles (m % 256 == 0, at least two tile waves) ---------------------------------
+// Per k-row a 128 x 256 tile reads 768 B of X for 65 536 MACs, a 256 x 256 tile 1 KiB for
+// 131 072: a third fewer L2 -> LDS bytes per MFMA, which is what the 128 x 256 kernel runs out
+// of at large m (profiles/r02a_summary.md).  4 waves, 2 x 2, each 128 x 128 = 4 x 4 MFMA tiles
+// (256 accumulator registers: one wave per SIMD).  Stages of 32 k-rows in a 5-slot ring (the
+// whole 160 KiB LDS: 128 KiB in flight per CU, which L2-miss latency needs -- with 4 slots the
+// MFMA pipe idled half the time even when every workgroup of an XCD read the same panels),
+// both panels 512 B per k-row with the same swizzle as above; stage t+4 is issued during stage
+// t, and the barrier that publishes stage t+1 sits before the last MFMA group of stage t so the
+// first fragment reads of t+1 hide under those MFMAs.
+constexpr int GW_B = 256, GW_BK = 32, GW_NS = 5;
+constexpr int GW_ROW = 2 * GW_B;          // 512 B per k-row of a 256-feature panel
+constexpr int GW_PNL = GW_BK * GW_ROW;    // 16 KiB: one panel of one stage
+constexpr int GW_STG = 2 * GW_PNL;        // 32 KiB per stage (A panel, B panel)
+constexpr int GW_LDS = GW_NS * GW_STG;    // 160 KiB: the whole LDS
+constexpr int GW_DMA = 8;                 // LDS-DMA wave-instructions per wave per stage
+
+// lane's DMA chunk of wave-instruction q (rows 2q, 2q+1 of a panel): k-row and logical column
+PT2Q_DEV void gw_chunk(int q, int& row, int& c) {
+  const int lane = threadIdx.x & 63;
+  row = 2 * q + (lane >> 5);
+  c = (lane & 31) ^ ((row & 3) << 2);
+}
+
+// whole stage with per-lane sources (rows past kend read the zero chunk)
+PT2Q_DEV void gw_stage(const uint16_t* X, long ld, int i0, int j0, int k0, int kend, uint8_t* stg) {
+#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
+  return;
+#endif
+  const int wave = threadIdx.x >> 6;
+  typedef __attribute__((address_space(3))) void* lptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave * 4 + j;
+    int row, c;
+    gw_chunk(q, row, c);
+    const bool in = k0 + row < kend;
+    const uint16_t* xr = X + (long)(k0 + row) * ld;
+    __builtin_amdgcn_global_load_lds(in ? (const void*)(xr + i0 + 8 * c) : (const void*)&gx_zero16,
+                                     (lptr)(stg + q * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(in ? (const void*)(xr + j0 + 8 * c) : (const void*)&gx_zero16,
+                                     (lptr)(stg + GW_PNL + q * 1024), 16, 0, 0);
+  }
+}
+
+// byte offsets of this lane's 8 chunk sources from the stage's first k-row (A: 0..3, B: 4..7)
+PT2Q_DEV void gw_voff(long ld, int i0, int j0, uint32_t (&vo)[8]) {
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int row, c;
+    gw_chunk(wave * 4 + j, row, c);
+    vo[j] = (uint32_t)(((long)row * ld + i0 + 8 * c) * 2);
+    vo[4 + j] = (uint32_t)(((long)row * ld + j0 + 8 * c) * 2);
+  }
+}
+
+// half hf of a whole in-range stage: A and B chunks j = 2hf, 2hf + 1
+PT2Q_DEV void gw_stage_half(const uint16_t* Xk0, const uint32_t (&vo)[8], uint8_t* stg, int hf) {
+#ifdef GX_PROBE_NO_DMA
+  return;
+#endif
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* sb = (const char*)Xk0;
+  typedef __attribute__((address_space(3))) void* lptr;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int j = 2 * hf + e;
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vo[j]), (lptr)(stg + (wave * 4 + j) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(sb + vo[4 + j]), (lptr)(stg + GW_PNL + (wave * 4 + j) * 1024),
+                                     16, 0, 0);
+  }
+}
+
+struct GwFrags {
+  s16x4 lo[8], hi[8];  // 0..3: A tiles mt; 4..7: B tiles nt
+};
+
+// the 16 transposed reads of k16 step S of a stage (rows 16S .. 16S+15)
+template <int S>
+PT2Q_DEV void gw_read(GwFrags& f, const uint32_t (&addr)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    f.lo[q] = gx_tr<S * 16 * GW_ROW>(addr[q]);
+    f.hi[q] = gx_tr<S * 16 * GW_ROW + 4 * GW_ROW>(addr[q]);
+  }
+}
+
+// wait until at most N LDS reads are outstanding (N <= 15: the counter's range), tying f
+template <int N>
+PT2Q_DEV void gw_wait(GwFrags& f) {
+  asm volatile("s_waitcnt lgkmcnt(%16)"
+               : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]), "+v"(f.lo[5]),
+                 "+v"(f.lo[6]), "+v"(f.lo[7]), "+v"(f.hi[0]), "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3]),
+                 "+v"(f.hi[4]), "+v"(f.hi[5]), "+v"(f.hi[6]), "+v"(f.hi[7])
+               : "n"(N));
+}
+
+template <int N>
+PT2Q_DEV void gw_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait for a stage while the y younger stages (0 <= y <= GW_NS - 2) stay in flight
+PT2Q_DEV void gw_vmwait_y(int y) {
+  static_assert(GW_NS == 5, "one case per younger stage");
+  switch (y) {
+    case 0: gw_vmwait<0>(); break;
+    case 1: gw_vmwait<GW_DMA>(); break;
+    case 2: gw_vmwait<2 * GW_DMA>(); break;
+    default: gw_vmwait<3 * GW_DMA>(); break;
+  }
+}
+
+// ---- the hand-scheduled k16 step --------------------------------------------------------------
+// Fragment reads and LDS-DMA issues are inline asm and every MFMA is followed by a full
+// scheduling barrier, so the step keeps exactly this interleaving: the 16 MFMAs are spaced by
+// the reads of the next step's 16 fragment halves (two per MFMA gap, which the LDS absorbs in
+// the MFMA's shadow) and by the four DMAs of half a future stage.  The barrier that publishes
+// the next stage sits after the step's first MFMA, so the MFMA pipe is busy while the waves
+// meet.
+template <bool BF16>
+PT2Q_DEV void gw_mfma1(f32x16& acc, const s16x4& alo, const s16x4& ahi, const s16x4& blo, const s16x4& bhi) {
+#ifndef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
+  acc = gx_mfma<BF16>(gx_cat(alo, ahi), gx_cat(blo, bhi), acc);
+#endif
+  __builtin_amdgcn_sched_barrier(0);  // nothing moves across: the step's interleaving stays
+}
+
+// one 16-B LDS-DMA: global (sbase + voff) -> LDS m0 + 16 lane
+PT2Q_DEV void gw_dma_asm(const char* sbase, uint32_t voff, uint32_t m0) {
+#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
+  return;
+#endif
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0)
+               : "memory");  // (m0 is reserved: the compiler sets it afresh before its own DMAs)
+}
+
+struct GwDma {          // half a future stage's LDS-DMAs
+  const char* src;      // the stage's first k-row
+  uint32_t m0;          // the LDS slot + this wave's first chunk
+};
+
+// one k16 step: MFMAs on cur, the 16 reads of nxt (byte offset ROFF from ra) in the gaps.
+// SYNC: after the first MFMA wait for the stage the reads need (Y younger stages stay in flight;
+// Y < 0: y at run time) and meet the other waves.  HALF >= 0: issue that half of a stage's
+// DMAs.  No run-time branch between the MFMAs of a steady step (Y >= 0): a branch there makes
+// the register allocator shuffle the 256 accumulator registers.
+template <bool BF16, int ROFF, bool SYNC, int Y, int HALF>
+PT2Q_DEV void gw_step(f32x16 (&acc)[4][4], const GwFrags& cur, GwFrags& nxt, const uint32_t (&ra)[8], int y,
+                      const GwDma& d, const uint32_t (&vo)[8]) {
+  gw_mfma1<BF16>(acc[0][0], cur.lo[0], cur.hi[0], cur.lo[4], cur.hi[4]);
+  if constexpr (SYNC) {
+    if constexpr (Y >= 0)
+      gw_vmwait<Y * GW_DMA>();
+    else
+      gw_vmwait_y(y);
+    asm volatile("s_barrier" ::: "memory");
+  }
+#pragma unroll
+  for (int i = 1; i < 16; ++i) {
+    const int mt = i >> 2, nt = i & 3;
+    gw_mfma1<BF16>(acc[mt][nt], cur.lo[mt], cur.hi[mt], cur.lo[4 + nt], cur.hi[4 + nt]);
+    if (i <= 8) {
+      const int q = i - 1;
+      nxt.lo[q] = gx_tr<ROFF>(ra[q]);
+      nxt.hi[q] = gx_tr<ROFF + 4 * GW_ROW>(ra[q]);
+    }
+    if constexpr (HALF >= 0) {
+      if (i >= 10 && i <= 13) {
+        const int e = i - 10, j = 2 * HALF + (e >> 1);
+        // A chunk j then B chunk j
+        gw_dma_asm(d.src, vo[(e & 1) * 4 + j], d.m0 + (e & 1) * GW_PNL + j * 1024);
+      }
+    }
+  }
+  gw_wait<0>(nxt);
+}
+
+// continue the chains of tile (i0, j0) over X rows [kbeg, kend) (kbeg a multiple of 32)
+template <bool BF16>
+PT2Q_DEV void gw_chain(f32x16 (&acc)[4][4], const uint16_t* X, long ld, int i0, int j0, int kbeg, int kend,
+                       uint8_t* smem) {
+  const int nk = (kend - kbeg + GW_BK - 1) / GW_BK;
+  if (nk <= 0) return;
+  const int nkf = (kend - kbeg) / GW_BK;  // whole stages
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, gh = (lane >> 4) & 1, h = lane >> 5;
+  uint32_t off[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ca = wr * 16 + t * 4 + 2 * gh + (p >> 1), cb = wc * 16 + t * 4 + 2 * gh + (p >> 1);
+    off[t] = (8 * h + q) * GW_ROW + ((ca ^ (q << 2)) << 4) + 8 * (p & 1);
+    off[4 + t] = GW_PNL + (8 * h + q) * GW_ROW + ((cb ^ (q << 2)) << 4) + 8 * (p & 1);
+  }
+  uint32_t vo[8];
+  gw_voff(ld, i0, j0, vo);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+#pragma unroll
+  for (int s = 0; s < GW_NS - 1; ++s)
+    if (s < nk) gw_stage(X, ld, i0, j0, kbeg + s * GW_BK, kend, smem + s * GW_STG);
+  gw_vmwait_y(min(GW_NS - 2, nk - 1));
+  asm volatile("s_barrier" ::: "memory");
+  uint32_t ra[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) ra[u] = lds0 + off[u];
+  GwFrags P, Q;
+  gw_read<0>(P, ra);
+  gw_wait<0>(P);
+  const uint32_t mw = lds0 + (uint32_t)(wave * 4 * 1024);
+  // steady state: stage t+NS-1 is a whole stage, issued by the fast DMAs of both steps
+  const int t1 = max(0, nkf - (GW_NS - 1));
+  int t = 0;
+  for (; t < t1; ++t) {
+    GwDma d;
+    d.src = (const char*)(X + (long)(kbeg + (t + GW_NS - 1) * GW_BK) * ld);
+    d.m0 = mw + (uint32_t)(((t + GW_NS - 1) % GW_NS) * GW_STG);
+    gw_step<BF16, 16 * GW_ROW, false, 0, 0>(acc, P, Q, ra, 0, d, vo);  // reads of Q: rows 16..31 of stage t
+    const uint32_t base = lds0 + (uint32_t)(((t + 1) % GW_NS) * GW_STG);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ra[u] = base + off[u];
+    gw_step<BF16, 0, true, GW_NS - 2, 1>(acc, Q, P, ra, 0, d, vo);  // stage t+1 published; reads of P
+  }
+  // the last stages: a ragged stage (per-lane sources) and a draining ring
+  for (; t < nk; ++t) {
+    if (t + GW_NS - 1 < nk)
+      gw_stage(X, ld, i0, j0, kbeg + (t + GW_NS - 1) * GW_BK, kend, smem + ((t + GW_NS - 1) % GW_NS) * GW_STG);
+    GwDma d{};
+    gw_step<BF16, 16 * GW_ROW, false, 0, -1>(acc, P, Q, ra, 0, d, vo);
+    const uint32_t base = lds0 + (uint32_t)(((t + 1) % GW_NS) * GW_STG);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) ra[u] = base + off[u];
+    // (past the last stage: vmcnt(0), a barrier and reads of a stale slot, never used)
+    gw_step<BF16, 0, true, -1, -1>(acc, Q, P, ra, max(0, min(t + GW_NS - 1, nk - 1) - (t + 1)), d, vo);
+  }
+  asm volatile("s_barrier" ::: "memory");  // the ring is reused by the next piece
+}
+
+// Same split and output contract as gram16x_kernel (STORE / CHAIN_POS, upper + mirror), on
+// 256 x 256 tiles of the T x T grid.  A published partial is the whole tile, unpredicated.
+template <bool BF16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram16w_kernel(
+    GemmDesc g, int T, int SJ, int Kp, long ntile, int NG, int R, int D, int* flags, int* status, long cap) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[GW_LDS];
+  const uint16_t* X = (const uint16_t*)g.A;
+  const GxSched S(ntile, Kp, NG, R, 1, D);
+  const int lane = threadIdx.x & 63;
+  const long ldc = g.ldc;
+  for (int pc = -D; pc < S.npieces; ++pc) {
+    int a, kb, ke;
+    bool from_partial;
+    S.piece(pc, a, kb, ke, from_partial);
+    int ti, tj;
+    gx_tile<1>(a, T, T, SJ, ti, tj);
+    const int i0 = ti * GW_B, j0 = tj * GW_B;
+    if (from_partial && threadIdx.x == 0) {
+      wait_flag_ge<2>(&flags[a], 1, cap, status, STALL_GRAM);  // gives up loudly (status word)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (from_partial) __syncthreads();
+    // this lane's element (mt, nt, r) sits at row R(mt, r) + 4(lane>>5), column C(nt) + (lane&31)
+    // with R, C wave-uniform: addresses are a uniform row pointer plus a 32-bit lane offset
+    const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wu >> 1, wc = wu & 1;
+    const int iw = i0 + wr * 128, jw = j0 + wc * 128;  // the wave's 128 x 128 block
+    const uint32_t lo = (uint32_t)(4 * (lane >> 5)) * (uint32_t)ldc + (lane & 31);
+    f32x16 acc[4][4];
+    if (from_partial || g.mode == GEMM_CHAIN_POS) {
+      // (a diagonal tile's lower half continues whatever is there; it is never stored as final)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float* rp = g.C + (long)(iw + mt * 32 + (r & 3) + 8 * (r >> 2)) * ldc + jw;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[mt][nt][r] = rp[lo + nt * 32];
+        }
+        // into the accumulator registers per row group, so the loads do not all stay live
+        asm volatile("" : "+a"(acc[mt][0]), "+a"(acc[mt][1]), "+a"(acc[mt][2]), "+a"(acc[mt][3]));
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counts its own DMAs
+    gw_chain<BF16>(acc, X, g.lda, i0, j0, kb, min(ke, g.K), smem);
+    if (ke < Kp) {  // publish the partial (whole tile) for the workgroup that continues it
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float* rp = g.C + (long)(iw + mt * 32 + (r & 3) + 8 * (r >> 2)) * ldc + jw;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) rp[lo + nt * 32] = acc[mt][nt][r];
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&flags[a], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    const bool diag = ti == tj;
+    // column minus row of this lane's element (mt, nt, 4 g4 + u), minus (tile-local) u
+    const int dl = (wc * 128 + (lane & 31)) - (wr * 128 + 4 * (lane >> 5));
+    // mirror: column c of the tile is row c of G; the 4 rows (r&3) of a register group are 4
+    // consecutive elements of it
+    const uint32_t lm = (uint32_t)(lane & 31) * (uint32_t)ldc + 4 * (lane >> 5);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int rl = mt * 32 + 8 * g4;
+          const f32x16& A = acc[mt][nt];
+          const int dc = dl + nt * 32 - rl;  // element (u) exists iff dc >= u (diagonal tiles)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float* rp = g.C + (long)(iw + rl + u) * ldc + jw;
+            if (!diag || dc >= u) rp[lo + nt * 32] = A[4 * g4 + u];
+          }
+          float* mp = g.C + (long)(jw + nt * 32) * ldc + iw + rl;
+          if (!diag || dc > 3) {
+            *(float4*)(mp + lm) = make_float4(A[4 * g4], A[4 * g4 + 1], A[4 * g4 + 2], A[4 * g4 + 3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (dc > u) mp[lm + u] = A[4 * g4 + u];
+          }
+        }
+  }
+}
+
 }  // namespace
 
 size_t pt2q_gram16_flags_ints(int m) { return (size_t)gx_ntile(m) + 2; }
@@ -456,6 +828,19 @@ int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st, int* statu
   // (fast staging keeps a stage's byte offsets in 32 bits: 64 rows * lda * 2 < 2^32)
   const bool dma = ((uintptr_t)g.A % 16 == 0) && (g.lda % 8 == 0) && (m % 8 == 0) && g.lda < (1l << 25);
   const bool bf = g.in_dtype == PT2Q_BF16;
+  // 256 x 256 tiles when m is a multiple of 256 and they make at least two waves (so the
+  // data-parallel part keeps every CU busy); mirror stores are float4
+  const int TW = m / GW_B;
+  const long ntw = (long)TW * (TW + 1) / 2;
+  if (split && dma && tu.gram_wide && m % GW_B == 0 && ntw >= 2l * NG * R && (uintptr_t)g.C % 16 == 0 &&
+      g.ldc % 4 == 0) {
+    const int SW = tu.gram_super > 0 ? tu.gram_super : 8;
+    const int Dw = tu.gram_dp ? (int)std::max(0l, ntw / (NG * R) - 1) : 0;
+    hipLaunchKernelGGL(bf ? gram16w_kernel<true> : gram16w_kernel<false>, dim3(grid), dim3(256), 0, st, g, TW, SW,
+                       Kp, ntw, NG, R, Dw, flags, status, tu.spin_cap_long);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   void (*k)(GemmDesc, int, int, int, int, long, int, int, int, int, int*, int*, long) =
       bf ? (dma ? gram16x_kernel<true, true> : gram16x_kernel<true, false>)
          : (dma ? gram16x_kernel<false, true> : gram16x_kernel<false, false>);

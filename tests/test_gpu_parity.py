@@ -80,6 +80,28 @@ def test_gram_streamk_bitexact(pt2q, N, m, dt):
     assert bits_equal(host(G), oracle_gram(Xd))
 
 
+@pytest.mark.parametrize("N,m,dt,cut", [(1500, 8192, torch.float16, 1024), (2000, 11008, torch.bfloat16, 640),
+                                        (4133, 13824, torch.float16, 4096)])
+def test_gram_wide_tiles_continue(pt2q, N, m, dt, cut):
+    """256 x 256 tiles (m % 256 == 0, >= 2 tile waves): data-parallel waves + stream-K pieces,
+    a ragged last stage (N % 32 != 0), and a second launch continuing the chains
+    (accumulate="continue") at a row cut: bit-identical to the one-launch Gram and, on sampled
+    column blocks, to the oracle's 16-bit arithmetic."""
+    from test_gpu_configs import sample_cols
+    X = synth.activations(17 + m, N, m)
+    Xd = cuda(X).to(dt)
+    G = pt2q.gram(Xd)
+    G2 = pt2q.gram(Xd[:cut], torch.empty_like(G))
+    G2 = pt2q.gram(Xd[cut:], G2, accumulate="continue")
+    Gh = host(G)
+    assert bits_equal(host(G2), Gh)
+    assert np.array_equal(Gh, Gh.T)
+    orc.set_threads(16)
+    S = sample_cols(m)
+    Xs = Xd[:, torch.from_numpy(S).to(Xd.device)].contiguous()
+    assert bits_equal(Gh[np.ix_(S, S)], orc.gram16(oracle_x(Xs)))
+
+
 @pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500)])
 def test_hessian_cholesky_inverse_bitexact(pt2q, m, N):
     X = synth.activations(11 + m, N, m)

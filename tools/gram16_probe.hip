@@ -6,16 +6,29 @@
 #include "../snlp---tenary-post-train-quantization_amd/csrc/gram16.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
+
+// the library's tuning (api.hip), reduced to the Gram knobs this probe varies
+const Pt2qTuning& pt2q_tuning() {
+  static Pt2qTuning t = [] {
+    Pt2qTuning u;
+    auto gi = [](const char* k, int d) { const char* v = getenv(k); return v ? atoi(v) : d; };
+    u.gram_wide = gi("PT2Q_GRAM_WIDE", 1);
+    u.gram_super = gi("PT2Q_GRAM_SUPER", 0);
+    return u;
+  }();
+  return t;
+}
 
 static float time_launch(GemmDesc g, int* F, int reps) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  pt2q_launch_gram16(g, F, 0);
+  pt2q_launch_gram16(g, F, 0, nullptr);
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(e0, 0);
-  for (int i = 0; i < reps; ++i) pt2q_launch_gram16(g, F, 0);
+  for (int i = 0; i < reps; ++i) pt2q_launch_gram16(g, F, 0, nullptr);
   (void)hipEventRecord(e1, 0);
   (void)hipDeviceSynchronize();
   float ms = 0;
@@ -48,6 +61,6 @@ int main(int argc, char** argv) {
   printf("resident X N=%ld m=%d: %.3f ms  %.1f TFLOP/s\n", N, m, ms, fl / ms / 1e9);
   int info = 0;
   (void)hipMemcpy(&info, (int*)F + gx_ntile(m), 4, hipMemcpyDeviceToHost);
-  printf("timeout flag %d\n", info);
+  printf("status word %d\n", info);
   return 0;
 }

@@ -1,34 +1,50 @@
-"""Per-dispatch PMC table for gpurun_out/pmcp (tools/pmc_probe16.sh): python tools/pmc_table.py [dir]"""
-import csv, glob, os, sys
-from collections import defaultdict
-d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcp"
-vals = defaultdict(dict)
-dur = {}
-for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
-    for r in csv.DictReader(open(f)):
-        if "gram16" not in r["Kernel_Name"]:
+"""Per-kernel PMC table of a tools/pmc_gram.sh run (dev tool): python tools/pmc_table.py <dir>
+
+One counter per run (<dir>/<CTR>/); FETCH_SIZE x 2 (gfx950) and KB x 1024 as in
+tools/summarize_r02.py; L2 hit = TCC_HIT / (TCC_HIT + TCC_MISS); LDS conflict share =
+SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from summarize_r02 import find, pass_values  # noqa: E402
+
+
+def main():
+    d = sys.argv[1]
+    per = {}
+    for ctr in sorted(os.listdir(d)):
+        p = os.path.join(d, ctr)
+        if not os.path.isdir(p):
             continue
-        k = int(r["Dispatch_Id"])
-        vals[k][r["Counter_Name"]] = vals[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-for f in sorted(glob.glob(os.path.join(d, "p*", "run_kernel_trace.csv"))):
-    for r in csv.DictReader(open(f)):
-        if "gram16" in r["Kernel_Name"]:
-            dur.setdefault(os.path.dirname(f), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-# dispatches are numbered per pass; group by order within the pass
-bypass = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
-    ids = sorted({int(r["Dispatch_Id"]) for r in csv.DictReader(open(f)) if "gram16" in r["Kernel_Name"]})
-    rows = defaultdict(dict)
-    for r in csv.DictReader(open(f)):
-        if "gram16" in r["Kernel_Name"]:
-            k = int(r["Dispatch_Id"])
-            rows[k][r["Counter_Name"]] = rows[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    for pos, k in enumerate(ids):
-        bypass[pos].append(rows[k])
-for pos in sorted(bypass):
-    merged = {}
-    for x in bypass[pos]:
-        merged.update(x)
-    print(pos, {k: f"{v:.4g}" for k, v in sorted(merged.items())})
-for k, v in dur.items():
-    print(k, [f"{x/1e6:.2f}" for x in v])
+        vals, dur = pass_values(find(p))
+        for k, v in vals.items():
+            e = per.setdefault(k, {})
+            e[ctr] = sum(v) / len(v)
+            e["ns"] = sum(dur[k]) / len(dur[k])
+            e["n"] = len(v)
+    for k, e in per.items():
+        if "gram" not in k:
+            continue
+        ns = e["ns"]
+        cyc = e.get("GRBM_GUI_ACTIVE", 0) / 8
+        out = [f"{k}: {e['n']} dispatches, {ns / 1e6:.2f} ms"]
+        if "FETCH_SIZE" in e:
+            fb = 2 * e["FETCH_SIZE"] * 1024
+            out.append(f"fetch {fb / 1e9:.1f} GB ({fb / ns:.0f} GB/s)")
+        if "WRITE_SIZE" in e:
+            out.append(f"write {e['WRITE_SIZE'] * 1024 / 1e9:.2f} GB")
+        if cyc:
+            out.append(f"clock {cyc / ns:.2f} GHz")
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in e:
+                out.append(f"MFMA busy {e['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * 1024):.3f}")
+        if "TCC_HIT_sum" in e and "TCC_MISS_sum" in e:
+            h, mi = e["TCC_HIT_sum"], e["TCC_MISS_sum"]
+            out.append(f"L2 hit {h / max(1, h + mi):.3f} ({(h + mi) * 128 / 1e9:.0f} GB of 128-B requests)")
+        if "SQ_LDS_BANK_CONFLICT" in e and "SQ_LDS_IDX_ACTIVE" in e:
+            out.append(f"LDS conflict {e['SQ_LDS_BANK_CONFLICT'] / max(1, e['SQ_LDS_IDX_ACTIVE']):.3f}")
+        print("; ".join(out))
+
+
+if __name__ == "__main__":
+    main()
