@@ -364,12 +364,287 @@ struct GxTile {
   }
 };
 
+// ---- the hand-scheduled chain (LDS-DMA path of both tile shapes) -----------------------------
+// BM x 256 output tiles, BM = 128 (gram16x_kernel) or 256 (gram16w_kernel: m % 256 == 0, at
+// least two tile waves).  Per k-row a 128 x 256 tile reads 768 B of X for 65 536 MACs, a
+// 256 x 256 tile 1 KiB for 131 072: a third fewer L2 -> LDS bytes per MFMA.  4 waves, 2 x 2,
+// each (BM/2) x 128 = MT x 4 MFMA tiles (BM = 256: 256 accumulator registers, one wave per
+// SIMD).  Stages of 32 k-rows in an NS-slot ring that fills the LDS (5 x 32 KiB / 6 x 24 KiB:
+// 128 / 120 KiB in flight per CU, which L2-miss latency needs); panel rows carry the swizzle of
+// gx_stage.  Stage t+NS-1 is issued during stage t.  Fragment reads and LDS-DMA issues are
+// inline asm and every MFMA is followed by a full scheduling barrier, so each k16 step keeps
+// exactly this interleaving: its MFMAs are spaced by the reads of the next step's fragment
+// halves (two per MFMA gap, absorbed in the MFMA's shadow) and by the DMAs of half a future
+// stage; the barrier that publishes the next stage sits after the step's first MFMA, so the
+// MFMA pipe is busy while the waves meet.  (Compiler-scheduled, the same loop left the MFMA
+// pipe idle half the time at m = 11008: 34.7 vs 30.0 ms.)
+constexpr int GW_B = 256, GW_BK = 32;
+constexpr int GW_ROW = 2 * GW_B;          // 512 B per k-row of a 256-feature panel (B, wide A)
+constexpr int GW_PNL = GW_BK * GW_ROW;    // 16 KiB: a 256-feature panel of one stage
+
+template <int BM>
+struct GwGeo {
+  static constexpr int MT = BM / 64;              // MFMA row tiles per wave
+  static constexpr int AROW = 2 * BM;             // bytes per k-row of the A panel
+  static constexpr int APNL = GW_BK * AROW;       // the A panel of one stage
+  static constexpr int STG = APNL + GW_PNL;       // A panel, then B panel
+  static constexpr int NS = BM == 256 ? 5 : 6;    // ring slots
+  static constexpr int LDS = NS * STG;            // 160 / 144 KiB
+  static constexpr int ADMA = APNL / 1024 / 4;    // A wave-instructions per wave per stage
+  static constexpr int DMA = ADMA + 4;            // + B: LDS-DMA wave-instructions per wave per stage
+  static constexpr int NF = MT + 4;               // fragments per k16 step
+};
+
+// lane's DMA chunk of wave-instruction q of a panel with `row` bytes per k-row: k-row, column
+template <int ROWB>
+PT2Q_DEV void gw_chunk(int q, int& row, int& c) {
+  constexpr int LPR = ROWB / 16;  // lanes per k-row
+  const int lane = threadIdx.x & 63;
+  row = (64 / LPR) * q + lane / LPR;
+  c = (lane % LPR) ^ ((row & 3) << 2);
+}
+
+// whole stage with per-lane sources: rows past kend and columns past M read the zero chunk
+template <int BM>
+PT2Q_DEV void gw_stage(const uint16_t* X, long ld, int M, int i0, int j0, int k0, int kend, uint8_t* stg) {
+#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
+  return;
+#endif
+  using G = GwGeo<BM>;
+  const int wave = threadIdx.x >> 6;
+  typedef __attribute__((address_space(3))) void* lptr;
+#pragma unroll
+  for (int j = 0; j < G::ADMA; ++j) {
+    const int q = wave * G::ADMA + j;
+    int row, c;
+    gw_chunk<G::AROW>(q, row, c);
+    const bool in = k0 + row < kend && i0 + 8 * c < M;
+    __builtin_amdgcn_global_load_lds(in ? (const void*)(X + (long)(k0 + row) * ld + i0 + 8 * c) : (const void*)&gx_zero16,
+                                     (lptr)(stg + q * 1024), 16, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave * 4 + j;
+    int row, c;
+    gw_chunk<GW_ROW>(q, row, c);
+    const bool in = k0 + row < kend && j0 + 8 * c < M;
+    __builtin_amdgcn_global_load_lds(in ? (const void*)(X + (long)(k0 + row) * ld + j0 + 8 * c) : (const void*)&gx_zero16,
+                                     (lptr)(stg + G::APNL + q * 1024), 16, 0, 0);
+  }
+}
+
+// byte offsets of this lane's chunk sources from a stage's first k-row: A chunks, then B chunks
+template <int BM>
+PT2Q_DEV void gw_voff(long ld, int i0, int j0, uint32_t (&vo)[GwGeo<BM>::DMA]) {
+  using G = GwGeo<BM>;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < G::ADMA; ++j) {
+    int row, c;
+    gw_chunk<G::AROW>(wave * G::ADMA + j, row, c);
+    vo[j] = (uint32_t)(((long)row * ld + i0 + 8 * c) * 2);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int row, c;
+    gw_chunk<GW_ROW>(wave * 4 + j, row, c);
+    vo[G::ADMA + j] = (uint32_t)(((long)row * ld + j0 + 8 * c) * 2);
+  }
+}
+
+template <int NF>
+struct GwFrags {
+  s16x4 lo[NF], hi[NF];  // 0 .. NF-5: A tiles mt; NF-4 .. NF-1: B tiles nt
+};
+
+// wait until at most N LDS reads are outstanding (N <= 15: the counter's range), tying f
+template <int N, int NF>
+PT2Q_DEV void gw_wait(GwFrags<NF>& f) {
+  if constexpr (NF == 8)
+    asm volatile("s_waitcnt lgkmcnt(%16)"
+                 : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]), "+v"(f.lo[5]),
+                   "+v"(f.lo[6]), "+v"(f.lo[7]), "+v"(f.hi[0]), "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3]),
+                   "+v"(f.hi[4]), "+v"(f.hi[5]), "+v"(f.hi[6]), "+v"(f.hi[7])
+                 : "n"(N));
+  else
+    asm volatile("s_waitcnt lgkmcnt(%12)"
+                 : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]), "+v"(f.lo[5]),
+                   "+v"(f.hi[0]), "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3]), "+v"(f.hi[4]), "+v"(f.hi[5])
+                 : "n"(N));
+}
+
+template <int N>
+PT2Q_DEV void gw_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait for a stage while the y younger stages (0 <= y <= NS - 2) stay in flight
+template <int D>
+PT2Q_DEV void gw_vmwait_y(int y) {
+  switch (y) {
+    case 0: gw_vmwait<0>(); break;
+    case 1: gw_vmwait<D>(); break;
+    case 2: gw_vmwait<2 * D>(); break;
+    case 3: gw_vmwait<3 * D>(); break;
+    default: gw_vmwait<4 * D>(); break;
+  }
+}
+
+template <bool BF16>
+PT2Q_DEV void gw_mfma1(f32x16& acc, const s16x4& alo, const s16x4& ahi, const s16x4& blo, const s16x4& bhi) {
+#ifndef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
+  acc = gx_mfma<BF16>(gx_cat(alo, ahi), gx_cat(blo, bhi), acc);
+#endif
+  __builtin_amdgcn_sched_barrier(0);  // nothing moves across: the step's interleaving stays
+}
+
+// one 16-B LDS-DMA: global (sbase + voff) -> LDS m0 + 16 lane
+PT2Q_DEV void gw_dma_asm(const char* sbase, uint32_t voff, uint32_t m0) {
+#ifdef GX_PROBE_NO_DMA
+  return;
+#endif
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0)
+               : "memory");  // (m0 is reserved: the compiler sets it afresh before its own DMAs)
+}
+
+struct GwDma {          // a future stage's LDS-DMAs
+  const char* src;      // the stage's first k-row
+  uint32_t mA, mB;      // LDS: this wave's first A chunk, first B chunk
+};
+
+// one k16 step: MFMAs on cur, the reads of nxt (byte offsets ROFFA / ROFFB from ra) in the gaps.
+// SYNC: after the first MFMA wait for the stage the reads need (Y younger stages stay in flight;
+// Y < 0: y at run time) and meet the other waves.  HALF >= 0: issue that half of a stage's
+// DMAs.  No run-time branch between the MFMAs of a steady step (Y >= 0): a branch there makes
+// the register allocator shuffle the accumulator registers.
+template <int BM, bool BF16, int ROFFA, int ROFFB, bool SYNC, int Y, int HALF>
+PT2Q_DEV void gw_step(f32x16 (&acc)[GwGeo<BM>::MT][4], const GwFrags<GwGeo<BM>::NF>& cur,
+                      GwFrags<GwGeo<BM>::NF>& nxt, const uint32_t (&ra)[GwGeo<BM>::NF], int y, const GwDma& d,
+                      const uint32_t (&vo)[GwGeo<BM>::DMA]) {
+  using G = GwGeo<BM>;
+  constexpr int NM = G::MT * 4, HD = G::DMA / 2;
+  gw_mfma1<BF16>(acc[0][0], cur.lo[0], cur.hi[0], cur.lo[G::MT], cur.hi[G::MT]);
+  if constexpr (SYNC) {
+    if constexpr (Y >= 0)
+      gw_vmwait<Y * G::DMA>();
+    else
+      gw_vmwait_y<G::DMA>(y);
+    asm volatile("s_barrier" ::: "memory");
+  }
+#pragma unroll
+  for (int i = 1; i < NM; ++i) {
+    const int mt = i >> 2, nt = i & 3;
+    gw_mfma1<BF16>(acc[mt][nt], cur.lo[mt], cur.hi[mt], cur.lo[G::MT + nt], cur.hi[G::MT + nt]);
+    if (i <= G::NF) {
+      const int q = i - 1;
+      if (q < G::MT) {
+        nxt.lo[q] = gx_tr<ROFFA>(ra[q]);
+        nxt.hi[q] = gx_tr<ROFFA + 4 * G::AROW>(ra[q]);
+      } else {
+        nxt.lo[q] = gx_tr<ROFFB>(ra[q]);
+        nxt.hi[q] = gx_tr<ROFFB + 4 * GW_ROW>(ra[q]);
+      }
+    }
+    if constexpr (HALF >= 0) {
+      if (i >= NM - HD) {
+        const int e = HALF * HD + i - (NM - HD);  // chunk e of the stage: A chunks, then B
+        if (e < G::ADMA)
+          gw_dma_asm(d.src, vo[e], d.mA + e * 1024);
+        else
+          gw_dma_asm(d.src, vo[e], d.mB + (e - G::ADMA) * 1024);
+      }
+    }
+  }
+  gw_wait<0>(nxt);
+}
+
+// continue the chains of tile (i0, j0) over X rows [kbeg, kend) (kbeg a multiple of 32); a tile
+// that crosses the matrix edge (full = false) takes every stage with per-lane sources
+template <int BM, bool BF16>
+PT2Q_DEV void gw_chain(f32x16 (&acc)[GwGeo<BM>::MT][4], const uint16_t* X, long ld, int M, int i0, int j0,
+                       int kbeg, int kend, bool full, uint8_t* smem) {
+  using G = GwGeo<BM>;
+  constexpr int NS = G::NS;
+  const int nk = (kend - kbeg + GW_BK - 1) / GW_BK;
+  if (nk <= 0) return;
+  const int nkf = (kend - kbeg) / GW_BK;  // whole stages
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, gh = (lane >> 4) & 1, h = lane >> 5;
+  uint32_t off[G::NF];
+#pragma unroll
+  for (int t = 0; t < G::MT; ++t) {
+    const int ca = wr * 4 * G::MT + t * 4 + 2 * gh + (p >> 1);  // 16-B chunk of the A panel row
+    off[t] = (8 * h + q) * G::AROW + ((ca ^ (q << 2)) << 4) + 8 * (p & 1);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int cb = wc * 16 + t * 4 + 2 * gh + (p >> 1);
+    off[G::MT + t] = G::APNL + (8 * h + q) * GW_ROW + ((cb ^ (q << 2)) << 4) + 8 * (p & 1);
+  }
+  uint32_t vo[G::DMA];
+  gw_voff<BM>(ld, i0, j0, vo);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) gw_stage<BM>(X, ld, M, i0, j0, kbeg + s * GW_BK, kend, smem + s * G::STG);
+  gw_vmwait_y<G::DMA>(min(NS - 2, nk - 1));
+  asm volatile("s_barrier" ::: "memory");
+  uint32_t ra[G::NF];
+#pragma unroll
+  for (int u = 0; u < G::NF; ++u) ra[u] = lds0 + off[u];
+  GwFrags<G::NF> P, Q;
+#pragma unroll
+  for (int u = 0; u < G::MT; ++u) {
+    P.lo[u] = gx_tr<0>(ra[u]);
+    P.hi[u] = gx_tr<4 * G::AROW>(ra[u]);
+  }
+#pragma unroll
+  for (int u = G::MT; u < G::NF; ++u) {
+    P.lo[u] = gx_tr<0>(ra[u]);
+    P.hi[u] = gx_tr<4 * GW_ROW>(ra[u]);
+  }
+  gw_wait<0>(P);
+  const uint32_t mwA = lds0 + (uint32_t)(wave * G::ADMA * 1024), mwB = lds0 + (uint32_t)(G::APNL + wave * 4 * 1024);
+  constexpr int RA1 = 16 * G::AROW, RB1 = 16 * GW_ROW;  // rows 16..31 of a stage
+  // steady state: stage t+NS-1 is a whole in-range stage, issued by the fast DMAs of both steps
+  const int t1 = full ? max(0, nkf - (NS - 1)) : 0;
+  int t = 0;
+  for (; t < t1; ++t) {
+    GwDma d;
+    d.src = (const char*)(X + (long)(kbeg + (t + NS - 1) * GW_BK) * ld);
+    const uint32_t so = (uint32_t)(((t + NS - 1) % NS) * G::STG);
+    d.mA = mwA + so;
+    d.mB = mwB + so;
+    gw_step<BM, BF16, RA1, RB1, false, 0, 0>(acc, P, Q, ra, 0, d, vo);
+    const uint32_t base = lds0 + (uint32_t)(((t + 1) % NS) * G::STG);
+#pragma unroll
+    for (int u = 0; u < G::NF; ++u) ra[u] = base + off[u];
+    gw_step<BM, BF16, 0, 0, true, NS - 2, 1>(acc, Q, P, ra, 0, d, vo);  // stage t+1 published
+  }
+  // the rest: per-lane sources (a ragged last stage, an edge tile) and a draining ring
+  for (; t < nk; ++t) {
+    if (t + NS - 1 < nk)
+      gw_stage<BM>(X, ld, M, i0, j0, kbeg + (t + NS - 1) * GW_BK, kend, smem + ((t + NS - 1) % NS) * G::STG);
+    GwDma d{};
+    gw_step<BM, BF16, RA1, RB1, false, 0, -1>(acc, P, Q, ra, 0, d, vo);
+    const uint32_t base = lds0 + (uint32_t)(((t + 1) % NS) * G::STG);
+#pragma unroll
+    for (int u = 0; u < G::NF; ++u) ra[u] = base + off[u];
+    // (past the last stage: vmcnt(0), a barrier and reads of a stale slot, never used)
+    gw_step<BM, BF16, 0, 0, true, -1, -1>(acc, Q, P, ra, max(0, min(t + NS - 1, nk - 1) - (t + 1)), d, vo);
+  }
+  asm volatile("s_barrier" ::: "memory");  // the ring is reused by the next piece
+}
+
 // g: M = N = m, K = rows, A = X (ld lda), C = G (ldc), mode STORE / ADD / CHAIN_POS; the split:
-// GxSched.
+// GxSched.  DMA: the hand-scheduled chain (gw_chain); else register-staged operands (GxTile).
 template <bool BF16, bool DMA>
 __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ, int SJ, int Kp, long ntile, int NG,
                                                       int R, int P, int D, int* flags, int* status,
                                                       long cap) {
+  static_assert(GwGeo<GX_BM>::LDS == GX_LDS, "one LDS image for both chains");
   __shared__ __attribute__((aligned(1024))) uint8_t smem[GX_LDS];
   const uint16_t* X = (const uint16_t*)g.A;
   const GxSched S(ntile, Kp, NG, R, P, D);
@@ -400,7 +675,11 @@ __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ
           F.acc[mt][nt][r] = (load && rw < g.M && c < g.N && c >= rw) ? g.C[(long)rw * g.ldc + c] : 0.0f;
         }
       }
-    F.chain<BF16, DMA>(X, g.lda, g.M, i0, j0, kb, min(ke, g.K), smem);
+    if constexpr (DMA)
+      gw_chain<GX_BM, BF16>(F.acc, X, g.lda, g.M, i0, j0, kb, min(ke, g.K), i0 + GX_BM <= g.M && j0 + GX_BN <= g.M,
+                            smem);
+    else
+      F.chain<BF16, DMA>(X, g.lda, g.M, i0, j0, kb, min(ke, g.K), smem);
     const bool final = (ke >= Kp);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -443,252 +722,12 @@ __global__ __launch_bounds__(256) void gram16x_kernel(GemmDesc g, int TI, int TJ
   }
 }
 
-// ---- 256 x 256 tiles (m % 256 == 0, at least two tile waves) ---------------------------------
-// Per k-row a 128 x 256 tile reads 768 B of X for 65 536 MACs, a 256 x 256 tile 1 KiB for
-// 131 072: a third fewer L2 -> LDS bytes per MFMA, which is what the 128 x 256 kernel runs out
-// of at large m (profiles/r02a_summary.md).  4 waves, 2 x 2, each 128 x 128 = 4 x 4 MFMA tiles
-// (256 accumulator registers: one wave per SIMD).  Stages of 32 k-rows in a 5-slot ring (the
-// whole 160 KiB LDS: 128 KiB in flight per CU, which L2-miss latency needs -- with 4 slots the
-// MFMA pipe idled half the time even when every workgroup of an XCD read the same panels),
-// both panels 512 B per k-row with the same swizzle as above; stage t+4 is issued during stage
-// t, and the barrier that publishes stage t+1 sits before the last MFMA group of stage t so the
-// first fragment reads of t+1 hide under those MFMAs.
-constexpr int GW_B = 256, GW_BK = 32, GW_NS = 5;
-constexpr int GW_ROW = 2 * GW_B;          // 512 B per k-row of a 256-feature panel
-constexpr int GW_PNL = GW_BK * GW_ROW;    // 16 KiB: one panel of one stage
-constexpr int GW_STG = 2 * GW_PNL;        // 32 KiB per stage (A panel, B panel)
-constexpr int GW_LDS = GW_NS * GW_STG;    // 160 KiB: the whole LDS
-constexpr int GW_DMA = 8;                 // LDS-DMA wave-instructions per wave per stage
-
-// lane's DMA chunk of wave-instruction q (rows 2q, 2q+1 of a panel): k-row and logical column
-PT2Q_DEV void gw_chunk(int q, int& row, int& c) {
-  const int lane = threadIdx.x & 63;
-  row = 2 * q + (lane >> 5);
-  c = (lane & 31) ^ ((row & 3) << 2);
-}
-
-// whole stage with per-lane sources (rows past kend read the zero chunk)
-PT2Q_DEV void gw_stage(const uint16_t* X, long ld, int i0, int j0, int k0, int kend, uint8_t* stg) {
-#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
-  return;
-#endif
-  const int wave = threadIdx.x >> 6;
-  typedef __attribute__((address_space(3))) void* lptr;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = wave * 4 + j;
-    int row, c;
-    gw_chunk(q, row, c);
-    const bool in = k0 + row < kend;
-    const uint16_t* xr = X + (long)(k0 + row) * ld;
-    __builtin_amdgcn_global_load_lds(in ? (const void*)(xr + i0 + 8 * c) : (const void*)&gx_zero16,
-                                     (lptr)(stg + q * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(in ? (const void*)(xr + j0 + 8 * c) : (const void*)&gx_zero16,
-                                     (lptr)(stg + GW_PNL + q * 1024), 16, 0, 0);
-  }
-}
-
-// byte offsets of this lane's 8 chunk sources from the stage's first k-row (A: 0..3, B: 4..7)
-PT2Q_DEV void gw_voff(long ld, int i0, int j0, uint32_t (&vo)[8]) {
-  const int wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int row, c;
-    gw_chunk(wave * 4 + j, row, c);
-    vo[j] = (uint32_t)(((long)row * ld + i0 + 8 * c) * 2);
-    vo[4 + j] = (uint32_t)(((long)row * ld + j0 + 8 * c) * 2);
-  }
-}
-
-// half hf of a whole in-range stage: A and B chunks j = 2hf, 2hf + 1
-PT2Q_DEV void gw_stage_half(const uint16_t* Xk0, const uint32_t (&vo)[8], uint8_t* stg, int hf) {
-#ifdef GX_PROBE_NO_DMA
-  return;
-#endif
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const char* sb = (const char*)Xk0;
-  typedef __attribute__((address_space(3))) void* lptr;
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int j = 2 * hf + e;
-    __builtin_amdgcn_global_load_lds((const void*)(sb + vo[j]), (lptr)(stg + (wave * 4 + j) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(sb + vo[4 + j]), (lptr)(stg + GW_PNL + (wave * 4 + j) * 1024),
-                                     16, 0, 0);
-  }
-}
-
-struct GwFrags {
-  s16x4 lo[8], hi[8];  // 0..3: A tiles mt; 4..7: B tiles nt
-};
-
-// the 16 transposed reads of k16 step S of a stage (rows 16S .. 16S+15)
-template <int S>
-PT2Q_DEV void gw_read(GwFrags& f, const uint32_t (&addr)[8]) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    f.lo[q] = gx_tr<S * 16 * GW_ROW>(addr[q]);
-    f.hi[q] = gx_tr<S * 16 * GW_ROW + 4 * GW_ROW>(addr[q]);
-  }
-}
-
-// wait until at most N LDS reads are outstanding (N <= 15: the counter's range), tying f
-template <int N>
-PT2Q_DEV void gw_wait(GwFrags& f) {
-  asm volatile("s_waitcnt lgkmcnt(%16)"
-               : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]), "+v"(f.lo[5]),
-                 "+v"(f.lo[6]), "+v"(f.lo[7]), "+v"(f.hi[0]), "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3]),
-                 "+v"(f.hi[4]), "+v"(f.hi[5]), "+v"(f.hi[6]), "+v"(f.hi[7])
-               : "n"(N));
-}
-
-template <int N>
-PT2Q_DEV void gw_vmwait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// wait for a stage while the y younger stages (0 <= y <= GW_NS - 2) stay in flight
-PT2Q_DEV void gw_vmwait_y(int y) {
-  static_assert(GW_NS == 5, "one case per younger stage");
-  switch (y) {
-    case 0: gw_vmwait<0>(); break;
-    case 1: gw_vmwait<GW_DMA>(); break;
-    case 2: gw_vmwait<2 * GW_DMA>(); break;
-    default: gw_vmwait<3 * GW_DMA>(); break;
-  }
-}
-
-// ---- the hand-scheduled k16 step --------------------------------------------------------------
-// Fragment reads and LDS-DMA issues are inline asm and every MFMA is followed by a full
-// scheduling barrier, so the step keeps exactly this interleaving: the 16 MFMAs are spaced by
-// the reads of the next step's 16 fragment halves (two per MFMA gap, which the LDS absorbs in
-// the MFMA's shadow) and by the four DMAs of half a future stage.  The barrier that publishes
-// the next stage sits after the step's first MFMA, so the MFMA pipe is busy while the waves
-// meet.
-template <bool BF16>
-PT2Q_DEV void gw_mfma1(f32x16& acc, const s16x4& alo, const s16x4& ahi, const s16x4& blo, const s16x4& bhi) {
-#ifndef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
-  acc = gx_mfma<BF16>(gx_cat(alo, ahi), gx_cat(blo, bhi), acc);
-#endif
-  __builtin_amdgcn_sched_barrier(0);  // nothing moves across: the step's interleaving stays
-}
-
-// one 16-B LDS-DMA: global (sbase + voff) -> LDS m0 + 16 lane
-PT2Q_DEV void gw_dma_asm(const char* sbase, uint32_t voff, uint32_t m0) {
-#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
-  return;
-#endif
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0)
-               : "memory");  // (m0 is reserved: the compiler sets it afresh before its own DMAs)
-}
-
-struct GwDma {          // half a future stage's LDS-DMAs
-  const char* src;      // the stage's first k-row
-  uint32_t m0;          // the LDS slot + this wave's first chunk
-};
-
-// one k16 step: MFMAs on cur, the 16 reads of nxt (byte offset ROFF from ra) in the gaps.
-// SYNC: after the first MFMA wait for the stage the reads need (Y younger stages stay in flight;
-// Y < 0: y at run time) and meet the other waves.  HALF >= 0: issue that half of a stage's
-// DMAs.  No run-time branch between the MFMAs of a steady step (Y >= 0): a branch there makes
-// the register allocator shuffle the 256 accumulator registers.
-template <bool BF16, int ROFF, bool SYNC, int Y, int HALF>
-PT2Q_DEV void gw_step(f32x16 (&acc)[4][4], const GwFrags& cur, GwFrags& nxt, const uint32_t (&ra)[8], int y,
-                      const GwDma& d, const uint32_t (&vo)[8]) {
-  gw_mfma1<BF16>(acc[0][0], cur.lo[0], cur.hi[0], cur.lo[4], cur.hi[4]);
-  if constexpr (SYNC) {
-    if constexpr (Y >= 0)
-      gw_vmwait<Y * GW_DMA>();
-    else
-      gw_vmwait_y(y);
-    asm volatile("s_barrier" ::: "memory");
-  }
-#pragma unroll
-  for (int i = 1; i < 16; ++i) {
-    const int mt = i >> 2, nt = i & 3;
-    gw_mfma1<BF16>(acc[mt][nt], cur.lo[mt], cur.hi[mt], cur.lo[4 + nt], cur.hi[4 + nt]);
-    if (i <= 8) {
-      const int q = i - 1;
-      nxt.lo[q] = gx_tr<ROFF>(ra[q]);
-      nxt.hi[q] = gx_tr<ROFF + 4 * GW_ROW>(ra[q]);
-    }
-    if constexpr (HALF >= 0) {
-      if (i >= 10 && i <= 13) {
-        const int e = i - 10, j = 2 * HALF + (e >> 1);
-        // A chunk j then B chunk j
-        gw_dma_asm(d.src, vo[(e & 1) * 4 + j], d.m0 + (e & 1) * GW_PNL + j * 1024);
-      }
-    }
-  }
-  gw_wait<0>(nxt);
-}
-
-// continue the chains of tile (i0, j0) over X rows [kbeg, kend) (kbeg a multiple of 32)
-template <bool BF16>
-PT2Q_DEV void gw_chain(f32x16 (&acc)[4][4], const uint16_t* X, long ld, int i0, int j0, int kbeg, int kend,
-                       uint8_t* smem) {
-  const int nk = (kend - kbeg + GW_BK - 1) / GW_BK;
-  if (nk <= 0) return;
-  const int nkf = (kend - kbeg) / GW_BK;  // whole stages
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int i16 = lane & 15, q = i16 >> 2, p = i16 & 3, gh = (lane >> 4) & 1, h = lane >> 5;
-  uint32_t off[8];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int ca = wr * 16 + t * 4 + 2 * gh + (p >> 1), cb = wc * 16 + t * 4 + 2 * gh + (p >> 1);
-    off[t] = (8 * h + q) * GW_ROW + ((ca ^ (q << 2)) << 4) + 8 * (p & 1);
-    off[4 + t] = GW_PNL + (8 * h + q) * GW_ROW + ((cb ^ (q << 2)) << 4) + 8 * (p & 1);
-  }
-  uint32_t vo[8];
-  gw_voff(ld, i0, j0, vo);
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
-#pragma unroll
-  for (int s = 0; s < GW_NS - 1; ++s)
-    if (s < nk) gw_stage(X, ld, i0, j0, kbeg + s * GW_BK, kend, smem + s * GW_STG);
-  gw_vmwait_y(min(GW_NS - 2, nk - 1));
-  asm volatile("s_barrier" ::: "memory");
-  uint32_t ra[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) ra[u] = lds0 + off[u];
-  GwFrags P, Q;
-  gw_read<0>(P, ra);
-  gw_wait<0>(P);
-  const uint32_t mw = lds0 + (uint32_t)(wave * 4 * 1024);
-  // steady state: stage t+NS-1 is a whole stage, issued by the fast DMAs of both steps
-  const int t1 = max(0, nkf - (GW_NS - 1));
-  int t = 0;
-  for (; t < t1; ++t) {
-    GwDma d;
-    d.src = (const char*)(X + (long)(kbeg + (t + GW_NS - 1) * GW_BK) * ld);
-    d.m0 = mw + (uint32_t)(((t + GW_NS - 1) % GW_NS) * GW_STG);
-    gw_step<BF16, 16 * GW_ROW, false, 0, 0>(acc, P, Q, ra, 0, d, vo);  // reads of Q: rows 16..31 of stage t
-    const uint32_t base = lds0 + (uint32_t)(((t + 1) % GW_NS) * GW_STG);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) ra[u] = base + off[u];
-    gw_step<BF16, 0, true, GW_NS - 2, 1>(acc, Q, P, ra, 0, d, vo);  // stage t+1 published; reads of P
-  }
-  // the last stages: a ragged stage (per-lane sources) and a draining ring
-  for (; t < nk; ++t) {
-    if (t + GW_NS - 1 < nk)
-      gw_stage(X, ld, i0, j0, kbeg + (t + GW_NS - 1) * GW_BK, kend, smem + ((t + GW_NS - 1) % GW_NS) * GW_STG);
-    GwDma d{};
-    gw_step<BF16, 16 * GW_ROW, false, 0, -1>(acc, P, Q, ra, 0, d, vo);
-    const uint32_t base = lds0 + (uint32_t)(((t + 1) % GW_NS) * GW_STG);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) ra[u] = base + off[u];
-    // (past the last stage: vmcnt(0), a barrier and reads of a stale slot, never used)
-    gw_step<BF16, 0, true, -1, -1>(acc, Q, P, ra, max(0, min(t + GW_NS - 1, nk - 1) - (t + 1)), d, vo);
-  }
-  asm volatile("s_barrier" ::: "memory");  // the ring is reused by the next piece
-}
-
 // Same split and output contract as gram16x_kernel (STORE / CHAIN_POS, upper + mirror), on
 // 256 x 256 tiles of the T x T grid.  A published partial is the whole tile, unpredicated.
 template <bool BF16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram16w_kernel(
     GemmDesc g, int T, int SJ, int Kp, long ntile, int NG, int R, int D, int* flags, int* status, long cap) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[GW_LDS];
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[GwGeo<GW_B>::LDS];
   const uint16_t* X = (const uint16_t*)g.A;
   const GxSched S(ntile, Kp, NG, R, 1, D);
   const int lane = threadIdx.x & 63;
@@ -735,7 +774,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counts its own DMAs
-    gw_chain<BF16>(acc, X, g.lda, i0, j0, kb, min(ke, g.K), smem);
+    gw_chain<GW_B, BF16>(acc, X, g.lda, g.M, i0, j0, kb, min(ke, g.K), true, smem);
     if (ke < Kp) {  // publish the partial (whole tile) for the workgroup that continues it
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
