@@ -12,6 +12,7 @@
 // the LDS-DMA f32 GEMM (gemmx.hip).  Their k-ordered chains keep every element bit-identical to
 // the unblocked definition above (oracle/pt2q_oracle.c).
 #include <cstdlib>
+#include <mutex>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -245,11 +246,42 @@ int launch_big(const GemmDesc& g, hipStream_t st) {
 
 }  // namespace
 
-// One stream: per 64-wide block J a panel solve + in-block triangular inverse launch and a strip
-// update launch (which also factors the next diagonal block); per 512- or 1024-row panel two rank-512 or -1024
-// updates.  The inverse (kept transposed, UiT) is built right-looking by column blocks as soon
-// as rows of block J are final, so no second stream (and no cross-queue dependency in a
-// captured graph) is needed.
+// The side stream of the look-ahead below (one per device, created on first use) and its two
+// events: `fork` (main -> side) and `join` (side -> main).  Under hipGraph capture the event
+// wait pulls the side stream into the capture and the final join brings it back.
+struct CholSide {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+int chol_side(CholSide*& out) {
+  static CholSide sides[64];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PT2Q_E_HIP;
+  std::lock_guard<std::mutex> lock(mu);
+  CholSide& c = sides[dev];
+  if (!c.st) {
+    int lo = 0, hi = 0;  // the side stream yields to the critical path: the lowest priority
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c.st, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess)
+      return PT2Q_E_HIP;
+  }
+  out = &c;
+  return PT2Q_OK;
+}
+
+// Main stream: per 64-wide block J a panel solve + in-block triangular inverse launch and a strip
+// update launch (which also factors the next diagonal block); per 512- or 1024-row panel P the
+// rank-CP terms of P go first to the NEXT panel's rows (main stream, on the critical path), and
+// to every row beyond it on a side stream, where they overlap the factorisation of panel P+1
+// (which touches only its own rows of U and of the inverse).  Before panel P+1's terms reach
+// those rows, the main stream joins the side stream, so every chain still takes panel P's terms
+// before panel P+1's: the order, and every bit, are those of the one-stream schedule.  The
+// inverse (kept transposed, UiT) is built right-looking by column blocks as soon as rows of
+// block J are final.
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
                                  float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form) {
   const long ld = m;  // U and Ui are packed m x m
@@ -278,12 +310,22 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   // Panels of CP rows: inside a panel, 64-blocks right-looking restricted to the panel (the
   // block's rows of U solved across the full width; the panel's later rows of U and later
   // columns of the inverse get the block's terms by rank-64 strip updates, whose first tile is
-  // the next diagonal block, factored in the same launch); after the panel, ONE rank-CP update of
-  // the trailing U triangle and one of the inverse columns to the right (gemmx).  Every chain
-  // still takes its terms in ascending k: earlier panels' bulk terms, then this panel's blocks.
-  const int tp = pt2q_tuning().chol_panel;
-  const int CP = tp >= NB ? tp / NB * NB : (m > 6144 ? 1024 : 512);  // panel rows (multiple of NB)
-  bool factored = false;
+  // the next diagonal block, factored in the same launch); after the panel, its rank-CP terms
+  // (gemmx) as described above.  Every chain takes its terms in ascending k.
+  const Pt2qTuning& tu = pt2q_tuning();
+  const int tp = tu.chol_panel;
+  // look-ahead from m > 6144 (measured: 4096 3.07 -> 3.24 ms with it, 11008 19.7 -> 18.6 ms with
+  // it and 512-row panels); panel rows (a multiple of NB): 512, or 1024 for a large m alone
+  const bool ahead = tu.chol_lookahead && m > 6144;
+  const int CP = tp >= NB ? tp / NB * NB : (m > 6144 && !ahead ? 1024 : 512);
+  CholSide* side = nullptr;
+  if (ahead && m > CP + CP && (rc = chol_side(side)) != PT2Q_OK) return rc;
+  bool factored = false, pending = false;  // pending: side-stream terms not yet joined
+  auto join = [&]() -> int {
+    if (pending && hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return PT2Q_E_HIP;
+    pending = false;
+    return PT2Q_OK;
+  };
   for (int P0 = 0; P0 < m; P0 += CP) {
     const int Pend = (m - P0 < CP) ? m : P0 + CP;
     for (int p0 = P0; p0 < Pend; p0 += NB) {
@@ -301,9 +343,25 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     }
     if (Pend >= m) break;
     const int K = Pend - P0, rest = m - Pend;
-    if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend, rest, Pend, rest), st)) != PT2Q_OK) return rc;
-    if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend, rest, Pend), st)) != PT2Q_OK) return rc;
+    // rows the side stream still owes earlier panels' terms must have them first
+    if ((rc = join()) != PT2Q_OK) return rc;
+    // the next panel's rows [Pend, Pend2) -- or all remaining rows without a side stream
+    const int Pend2 = side ? std::min(m, Pend + CP) : m;
+    if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend, Pend2 - Pend, Pend, rest, Pend2 < m ? false : true),
+                         st)) != PT2Q_OK)
+      return rc;
+    if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend, Pend2 - Pend, Pend), st)) != PT2Q_OK) return rc;
+    if (Pend2 < m) {  // every row beyond, on the side stream
+      if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->st, side->fork, 0) != hipSuccess)
+        return PT2Q_E_HIP;
+      if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend2, m - Pend2, Pend2, m - Pend2), side->st)) != PT2Q_OK)
+        return rc;
+      if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend2, m - Pend2, Pend), side->st)) != PT2Q_OK) return rc;
+      if (hipEventRecord(side->join, side->st) != hipSuccess) return PT2Q_E_HIP;
+      pending = true;
+    }
   }
+  if ((rc = join()) != PT2Q_OK) return rc;
   // Hinv = Uinv Uinvᵀ (upper tiles, mirrored): Hinv[i][k] = chain over j >= max(i, k) of
   // UiT[j][i] * UiT[j][k]
   GemmDesc g{};

@@ -106,6 +106,7 @@ struct Pt2qTuning {
   int gram_seglen = 0;         // PT2Q_GRAM_SEGLEN: f32 stream-K segment override
   int gemm_tile = 0;           // PT2Q_GEMM_TILE: 1 = 128x128, 6 = 64x64
   bool rank_update = true;     // PT2Q_RANK_UPDATE=0: generic grouped GEMM for Cholesky updates
+  bool chol_lookahead = true;  // PT2Q_CHOL_LOOKAHEAD=0: the trailing updates on the main stream only
   int chol_panel = 0;          // PT2Q_CHOL_PANEL: rows per rank-P Cholesky update (0: by m)
   bool wbar_fused = true;      // PT2Q_WBAR_FUSED=0: three SSR-mean launches
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch

@@ -102,8 +102,12 @@ def test_gram_wide_tiles_continue(pt2q, N, m, dt, cut):
     assert bits_equal(Gh[np.ix_(S, S)], orc.gram16(oracle_x(Xs)))
 
 
-@pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500)])
+@pytest.mark.parametrize("m,N", [(64, 256), (100, 80), (256, 512), (384, 200), (700, 1500), (2200, 2400),
+                                 (6400, 6500)])
 def test_hessian_cholesky_inverse_bitexact(pt2q, m, N):
+    """m = 2200: 512-row panels on one stream; m = 6400: the look-ahead (trailing terms of each
+    panel on the side stream, joined before the next panel's terms)."""
+    orc.set_threads(16)
     X = synth.activations(11 + m, N, m)
     G = orc.gram(X)
     H, damp = pt2q.prepare_hessian(cuda(G), N, 0.01)
