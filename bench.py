@@ -318,8 +318,9 @@ def main():
         achieved = avg_fl / (avg_ms * 1e-3) / 1e12
         peak = MI355X_F32_MFMA_PEAK_TFLOPS if a.io_dtype == "fp32" else MI355X_F16_MFMA_PEAK_TFLOPS
         kname = ("gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)" if a.io_dtype == "fp32" else
-                 "gram16x_kernel (symmetric Gram XᵀX: LDS-DMA staging, ds_read_b64_tr_b16, 16-bit MFMA "
-                 "32x32x16, f32 accumulate)")
+                 "gram16x_kernel (m=4096: 128x256 tiles) / gram16w_kernel (m=11008: 256x256 tiles): "
+                 "symmetric Gram XᵀX, LDS-DMA ring, ds_read_b64_tr_b16, hand-interleaved 16-bit MFMA "
+                 "32x32x16, f32 accumulate")
         roof = {"bound": "mfma", "kernel": kname, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": achieved / peak, "traffic": None, "avg_launch_ms": avg_ms,
                 "flops_per_launch": avg_fl, "per_width": per_m,

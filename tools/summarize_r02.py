@@ -91,12 +91,12 @@ def main():
     gram = {}
     for m in ("4096", "11008"):
         g = pmc[f"gram{m}"]
-        k = [x for x in g if "gram16x_kernel" in x][0]
-        gram[m] = {"fabric_bytes_per_launch": g[k]["fabric_bytes"], "avg_ms_pmc_run": g[k]["avg_us"] / 1e3,
+        k = [x for x in g if "gram16" in x][0]
+        gram[m] = {"kernel": k, "fabric_bytes_per_launch": g[k]["fabric_bytes"], "avg_ms_pmc_run": g[k]["avg_us"] / 1e3,
                    "mfma_busy_frac": g[k]["mfma_busy_frac"], "clock_GHz": g[k]["clock_GHz"],
                    "algorithmic_bytes_per_launch": 262144 * int(m) * 2 + int(m) * int(m) * 4}
     with open(os.path.join(out, "gram_pmc.json"), "w") as f:
-        json.dump({"kernel": "gram16x_kernel", "per_width": gram,
+        json.dump({"kernel": "gram16x_kernel (m=4096) / gram16w_kernel (m=11008)", "per_width": gram,
                    "source": f"profiles/{tag}_summary.md: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
                              "SQ_VALU_MFMA_BUSY_CYCLES | GRBM_GUI_ACTIVE, separate passes; FETCH_SIZE "
                              "x2 (gfx950), KB x1024; includes Infinity-Cache hits"}, f, indent=1)
