@@ -57,6 +57,10 @@ def parse():
     p.add_argument("--block-size", type=int, default=128)
     p.add_argument("--io-dtype", choices=["fp16", "fp32", "bf16"], default="fp16")
     p.add_argument("--no-ssr", action="store_true")
+    p.add_argument("--lanes", type=int, default=3, help="model workload: UnitPipeline lanes")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="model workload: run the units strictly one after another on one stream "
+                        "(default: engine.UnitPipeline overlaps unit i+1's Gram with unit i's tail)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the single-layer / Gram extras (profiling: keeps only the step's launches)")
@@ -173,6 +177,7 @@ class ModelStep:
         self.shards = sharding.assign_lpt([sharding.unit_cost(u) for u in self.units], world)
         self.mine = self.shards[rank]
         self.bs, self.ssr = a.block_size, not a.no_ssr
+        self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.X, self.W, self.ws = {}, {}, {}
         self.index = {u[0]: i for i, u in enumerate(self.units)}
         for i in self.mine:
@@ -181,7 +186,7 @@ class ModelStep:
             if m not in self.X:
                 self.X[m] = pt2q.fill_synthetic((N, m), 2000 + 97 * rank + m, std=1.0, outliers=True,
                                                 device=dev).to(io)
-                self.ws[m] = pt2q.UnitWorkspace(m, dev, self.bs)
+                self.ws[m] = self.pipe.workspace(m) if self.pipe else pt2q.UnitWorkspace(m, dev, self.bs)
             for k, (p, n, _) in enumerate(lins):
                 self.W[(i, p)] = pt2q.fill_synthetic((n, m), 100_000 + 16 * i + k, std=0.02,
                                                      device=dev).to(io)
@@ -193,6 +198,8 @@ class ModelStep:
         return self.X[lins[0][2]], {p: self.W[(i, p)] for p, _, _ in lins}
 
     def run_unit(self, Ws, X):
+        if self.pipe is not None:
+            return self.pipe.run(Ws, X)
         return pt2q.quantize_unit(Ws, X, block_size=self.bs, use_ssr=self.ssr,
                                   workspace=self.ws[X.shape[1]], defer=True)
 
@@ -357,7 +364,9 @@ def main():
                        "weight_columns_per_step": cols, "tokens": N, "io_dtype": a.io_dtype,
                        "block_size": bs,
                        "parallelism": (f"LPT unit sharding x{world}" if a.workload == "model" else
-                                       f"layer per rank x{world}") + (", rccl gather" if world > 1 else "")},
+                                       f"layer per rank x{world}") + (", rccl gather" if world > 1 else "")
+                                  + (f", {a.lanes} unit lanes (Grams chained, tails overlapped)"
+                                     if a.workload == "model" and not a.no_overlap else "")},
         }
         if a.workload == "model":
             res["s_model"] = ms_per_step / 1e3

@@ -173,12 +173,15 @@ class UnitRun:
     def __init__(self, outs, info, statuses, redo):
         self.outs, self.info, self.statuses, self._redo = outs, info, statuses, redo
         self.spd = None
+        self.join = None  # set by UnitPipeline: the caller's stream must wait for its streams
 
     def finish(self):
         """One host read of the Cholesky status and every stall word; raises Pt2qError on a
         stall, and re-runs the unit with pinv (main.py:140-141) if the Hessian was not SPD."""
         if self.spd is not None:
             return self.outs
+        if self.join is not None:
+            self.join()
         vals = torch.cat([self.info.reshape(1)] + [s.reshape(1) for s in self.statuses]).cpu().tolist()
         for v in vals[1:]:
             _lib.raise_stall(int(v), "quantize_unit")
@@ -205,13 +208,12 @@ def quantize_unit(Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor
     m = Ws[0].shape[1]
     dev = Ws[0].device
     ws = workspace if workspace is not None and workspace.m == m else UnitWorkspace(m, dev, block_size)
-    L = _lib.lib()
     statuses = []
     if X is not None:
         X = _float_input(X.reshape(-1, X.shape[-1]))
         nsamples = X.shape[0]
-        _lib.check(L.pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), nsamples, m, m, _lib.ptr(ws.G), m, 0,
-                               _lib.ptr(ws.gram_ws), ws.gram_ws.numel(), _lib.stream_of(dev)),
+        _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), nsamples, m, m, _lib.ptr(ws.G), m, 0,
+                                        _lib.ptr(ws.gram_ws), ws.gram_ws.numel(), _lib.stream_of(dev)),
                    "pt2q_gram")
         statuses.append(_lib.status_view(ws.gram_ws).clone())
         Gm = ws.G
@@ -219,6 +221,17 @@ def quantize_unit(Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor
         if G is None or nsamples is None:
             raise ValueError("quantize_unit needs X, or G and nsamples")
         Gm = G.contiguous().float()
+    run = _unit_tail(Ws, Gm, int(nsamples), ws, statuses, X, G, block_size, use_ssr, percdamp, max_iter,
+                     t_dtype)
+    return run if defer else run.finish()
+
+
+def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percdamp, max_iter, t_dtype):
+    """Damping, Cholesky inverse and every weight's block loop of a unit whose raw Gram is Gm,
+    on the current stream; returns the deferred UnitRun.  The pinv redo rebuilds the Gram from
+    the caller's X (or G): Gm may be a reused buffer by the time the status is read."""
+    m, dev = Ws[0].shape[1], Ws[0].device
+    L = _lib.lib()
     st = _lib.stream_of(dev)
     _lib.check(L.pt2q_prepare_hessian(_lib.ptr(Gm), m, m, int(nsamples), float(percdamp),
                                       _lib.ptr(ws.H), m, _lib.ptr(ws.damp), st), "pt2q_prepare_hessian")
@@ -243,15 +256,89 @@ def quantize_unit(Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor
         _lib.check(rc, "pt2q_quantize_blocks")
         statuses.append(_lib.status_view(bws).clone())
         outs.append(out)
+
     def redo():  # main.py:140-141: pinv of the damped Hessian, then the block loops again
-        # (the shared workspace may hold a later unit by now: rebuild G from the caller's tensors)
         Gr = gram(X) if X is not None else G.contiguous().float()
         Hinv = torch.linalg.pinv(prepare_hessian(Gr, nsamples, percdamp)[0])
         return [quantize_blocks(W, Gr, Hinv, block_size, use_ssr, _lib.AGA_ACT, max_iter, t_dtype)
                 for W in Ws]
 
-    run = UnitRun(outs, info, statuses, redo)
-    return run if defer else run.finish()
+    return UnitRun(outs, info, statuses, redo)
+
+
+class _Lane:
+    """One stream of a UnitPipeline with its own raw-Gram slot and unit workspaces per width."""
+
+    def __init__(self, dev, block_size):
+        self.dev, self.bs = dev, block_size
+        self.stream = torch.cuda.Stream(dev)
+        self.ws = {}
+
+    def workspace(self, m) -> UnitWorkspace:
+        if m not in self.ws:
+            self.ws[m] = UnitWorkspace(m, self.dev, self.bs)
+        return self.ws[m]
+
+
+class UnitPipeline:
+    """Cross-unit overlap for a model loop of independent units (main.py:289-299 per unit).
+
+    A unit is its Gram (MFMA-bound; every CU holds one long-lived workgroup that takes all of
+    its LDS and registers) and its tail: damping, Cholesky inverse and block loops, a long chain
+    of small latency-bound launches that leave most of the chip idle.  Units alternate between
+    `lanes` streams, each with its own Gram slot and workspaces; the Grams are chained by events
+    (one Gram at a time: a stream-K Gram needs every CU for its co-resident hand-offs).  The
+    next Gram takes the chip as soon as the previous one ends, so the tail of unit i is held
+    back until Gram i+1 is done and then runs beside the tail of unit i+1 -- two latency-bound
+    chains filling each other's gaps.  Every kernel sees exactly the operands of the sequential
+    order (per-lane buffers, stream order within a lane), so the results are bit-identical to
+    quantize_unit one unit after another.
+
+    run(Ws, X) returns a deferred UnitRun; its finish() joins the lanes into the caller's
+    stream (or call join())."""
+
+    def __init__(self, device, block_size: int = 128, use_ssr: bool = True, percdamp: float = 0.01,
+                 max_iter: int = 100, lanes: int = 3):
+        self.dev = torch.device(device)
+        self.bs, self.use_ssr, self.percdamp, self.max_iter = block_size, use_ssr, percdamp, max_iter
+        self.lanes = [_Lane(self.dev, block_size) for _ in range(lanes)]
+        self.turn = 0
+        self.gram_done = None  # event: the last Gram issued
+
+    def workspace(self, m) -> UnitWorkspace:
+        """Allocate every lane's buffers for width m now (outside any timed region)."""
+        for ln in self.lanes:
+            ln.workspace(m)
+        return self.lanes[0].workspace(m)
+
+    def run(self, Ws, X):
+        Ws = [_float_input(W) for W in Ws]
+        X = _float_input(X.reshape(-1, X.shape[-1]))
+        m, N = Ws[0].shape[1], X.shape[0]
+        ln = self.lanes[self.turn]
+        self.turn = (self.turn + 1) % len(self.lanes)
+        ws = ln.workspace(m)
+        st = ln.stream
+        st.wait_stream(torch.cuda.current_stream(self.dev))  # inputs written on the caller's stream
+        with torch.cuda.stream(st):
+            if self.gram_done is not None:
+                st.wait_event(self.gram_done)
+            _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), N, m, m, _lib.ptr(ws.G), m, 0,
+                                            _lib.ptr(ws.gram_ws), ws.gram_ws.numel(), _lib.stream_of(self.dev)),
+                       "pt2q_gram")
+            self.gram_done = torch.cuda.Event()
+            self.gram_done.record(st)
+            statuses = [_lib.status_view(ws.gram_ws).clone()]
+            run = _unit_tail(Ws, ws.G, N, ws, statuses, X, None, self.bs, self.use_ssr, self.percdamp,
+                             self.max_iter, torch.int8)
+        run.join = self.join
+        return run
+
+    def join(self):
+        """The caller's current stream waits for every unit issued so far."""
+        caller = torch.cuda.current_stream(self.dev)
+        for ln in self.lanes:
+            caller.wait_stream(ln.stream)
 
 
 class LayerWorkspace:

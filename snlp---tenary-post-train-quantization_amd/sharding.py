@@ -164,7 +164,8 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
 
     provider(unit) -> (X, {proj: W}) gives a unit's activations and weights on this rank's device
     (called only for this rank's units).  run_unit(Ws, X) -> [LayerOutput] defaults to
-    engine.quantize_unit (Gram -> damping -> Cholesky inverse -> block loops, shared per unit).
+    engine.UnitPipeline.run (Gram -> damping -> Cholesky inverse -> block loops, shared per unit,
+    the next unit's Gram overlapping this unit's tail on a second stream).
     Results are {f"{unit}.{proj}": {"T2" (2-bit packed, utils.py:189-219) or "T", "alpha", "mu",
     "perm", "shape"}}.  Returns (results on dst or None, this rank's unit indices)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -174,9 +175,13 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
     if run_unit is None:
         from . import engine  # noqa: WPS433 (device code only when quantising for real)
 
-        def run_unit(Ws, X):
-            return engine.quantize_unit(Ws, X, block_size=block_size, use_ssr=use_ssr,
-                                        percdamp=percdamp, defer=True)
+        pipes = {}
+
+        def run_unit(Ws, X):  # unit i+1's Gram overlaps unit i's tail (engine.UnitPipeline)
+            dev = Ws[0].device
+            if dev not in pipes:
+                pipes[dev] = engine.UnitPipeline(dev, block_size, use_ssr, percdamp)
+            return pipes[dev].run(Ws, X)
     runs = []
     for i in mine:
         name, lins, _ = units[i]

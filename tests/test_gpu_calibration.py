@@ -92,3 +92,30 @@ def test_model_loop_matches_reference_loop(pt2q):
     # the model was written back identically
     for pa, pb in zip(model_a.parameters(), model_b.parameters()):
         assert torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_unit_pipeline_equals_sequential(pt2q, lanes):
+    """engine.UnitPipeline (unit i+1's Gram on a low-priority stream while unit i's tail runs)
+    must give exactly the results of quantize_unit one unit after another: mixed input widths,
+    shared-input units with several linears, fp16 and fp32 activations, and more units per width
+    than Gram slots so every slot is rewritten while later units are in flight."""
+    units = []
+    for i, (m, ns, N, dt) in enumerate([(512, (384, 256), 1024, torch.float16),
+                                        (768, (512,), 2048, torch.float16),
+                                        (512, (640,), 1024, torch.float32),
+                                        (512, (256, 256, 128), 1536, torch.float16),
+                                        (768, (256,), 2048, torch.float16),
+                                        (512, (384,), 1024, torch.float16)]):
+        X = cuda(synth.activations(600 + i, N, m)).to(dt)
+        Ws = [cuda(synth.weights(700 + 10 * i + k, n, m)).to(dt) for k, n in enumerate(ns)]
+        units.append((Ws, X))
+    pipe = pt2q.UnitPipeline("cuda", 128, True, lanes=lanes)
+    runs = [pipe.run(Ws, X) for Ws, X in units]
+    got = [r.finish() for r in runs]
+    for (Ws, X), outs in zip(units, got):
+        want = pt2q.quantize_unit(Ws, X, block_size=128, use_ssr=True)
+        assert len(outs) == len(want)
+        for o, r in zip(outs, want):
+            for a, b in ((o.alpha, r.alpha), (o.mu, r.mu), (o.T, r.T), (o.perm, r.perm), (o.iters, r.iters)):
+                assert bits_equal(host(a), host(b))
