@@ -39,7 +39,8 @@ __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, 
   part[(long)c * n + i] = p;
 }
 
-// The three wbar steps in one launch (n <= 4096, n % 4 == 0): every workgroup forms its partial
+// The three wbar steps in one launch (n <= 16384, n % 4 == 0): every workgroup (one wave: 256
+// rows i, four per lane, so the reads spread over every CU) forms its partial
 // part[c][i] as ssr_wbar_partial_kernel; the last workgroup to finish a 256-row slice sums that
 // slice's partials in chunk order (wbar = sum / r); the last slice to finish forms
 // nw = clamp(sqrt(SUMN fma wbar^2)) and wn = wbar / nw.  Hand-offs: write-through (sc1) stores,
@@ -59,16 +60,16 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   typedef float f4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(part, 0, nchunks * n * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(wn, 0, n * 4, 0x00020000);
-  const int i = (blockIdx.y * 256 + threadIdx.x) * 4;
+  const int i = (blockIdx.y * blockDim.x + threadIdx.x) * 4;
   if (i < n) {
     f4 p = {0.0f, 0.0f, 0.0f, 0.0f};
     int e = 0;
-    for (; e + 8 <= ce; e += 8) {
-      f4 v[8];
+    for (; e + 16 <= ce; e += 16) {  // 16 loads in flight per lane
+      f4 v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(Wt + rows[e + u] + i);
+      for (int u = 0; u < 16; ++u) v[u] = *(const f4*)(Wt + rows[e + u] + i);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) p = p + v[u];
+      for (int u = 0; u < 16; ++u) p = p + v[u];
     }
     for (; e < ce; ++e) p = p + *(const f4*)(Wt + rows[e] + i);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, p), rp, (c * n + i) * 4, 0, 16);  // sc1
@@ -101,26 +102,36 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   __syncthreads();
   if (!last) return;
   if (threadIdx.x >= 64) return;
-  // wave 0: lane t holds elements {256u + 4t + q} (sumn_lane's order) in registers
+  // wave 0: lane t takes elements {256u + 4t + q} (sumn_lane's order), 16 float4 in flight;
+  // a second pass writes wn = wbar / nw (loads past n return zero, stores past n are dropped)
   const __amdgpu_buffer_rsrc_t rs = rw;
   const int t = threadIdx.x;
-  f4 v[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u)
-    v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (4 * t + 256 * u) * 4, 0, 16));
   float q = 0.0f;
+  for (int u0 = 0; u0 < n; u0 += 4096) {
+    f4 v[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u)
-    if (4 * t + 256 * u < n) {
-      q = fmaf(v[u][0], v[u][0], q);
-      q = fmaf(v[u][1], v[u][1], q);
-      q = fmaf(v[u][2], v[u][2], q);
-      q = fmaf(v[u][3], v[u][3], q);
-    }
+    for (int u = 0; u < 16; ++u)
+      v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + 4 * t + 256 * u) * 4, 0, 16));
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (u0 + 4 * t + 256 * u < n) {
+        q = fmaf(v[u][0], v[u][0], q);
+        q = fmaf(v[u][1], v[u][1], q);
+        q = fmaf(v[u][2], v[u][2], q);
+        q = fmaf(v[u][3], v[u][3], q);
+      }
+  }
   const float nw = clampmin(sqrtf(bfly64(q)));
+  for (int u0 = 0; u0 < n; u0 += 4096) {
+    f4 v[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u)
-    if (4 * t + 256 * u < n) *(f4*)(wn + 4 * t + 256 * u) = v[u] / nw;
+    for (int u = 0; u < 16; ++u)
+      v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (u0 + 4 * t + 256 * u) * 4, 0, 16));
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v[u] / nw), rs,
+                                             (u0 + 4 * t + 256 * u) * 4, 0, 0);
+  }
   if (t == 0) __hip_atomic_store(cnt + nsl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -183,6 +194,9 @@ __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) 
 }
 
 // One wave per remaining column: nj = clamp(sqrt(SUMN fma x^2)); s = SUMN fma (x/nj) * wn.
+// NV > 0 (n % 4 == 0, n <= 256 NV): one pass over the column, its NV float4 per lane kept in
+// registers for both chains; NV == 0: the generic two-pass paths.
+template <int NV>
 __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw, int n,
                                                       const int* rem, int r, const float* wn,
                                                       float* sim) {
@@ -192,17 +206,16 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
   const float* x = Wt + (long)rem[e] * ldw;
   float p = 0.0f;
   typedef float f4 __attribute__((ext_vector_type(4)));
-  if ((n & 3) == 0 && (ldw & 3) == 0 && n <= 4096) {
-    // one pass over the column: its 16 float4 per lane stay in registers for both chains
-    f4 v[16];
+  if constexpr (NV > 0) {
+    f4 v[NV];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < NV; ++u) {
       const long base = 4 * t + 256 * u;
       if (base < n) v[u] = *(const f4*)(x + base);
     }
     float ss = 0.0f;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < NV; ++u) {
       if (4 * t + 256 * u < n) {
         ss = fmaf(v[u][0], v[u][0], ss);
         ss = fmaf(v[u][1], v[u][1], ss);
@@ -212,7 +225,7 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
     }
     const float nj = clampmin(sqrtf(bfly64(ss)));
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < NV; ++u) {
       const long base = 4 * t + 256 * u;
       if (base < n) {
         const f4 w = *(const f4*)(wn + base);
@@ -749,8 +762,8 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   if (r <= 0 || n <= 0) return PT2Q_E_ARG;
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
-  if (cnt && n <= 4096 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && pt2q_tuning().wbar_fused) {
-    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 1024)), dim3(256), 0, st, Wt, ldw,
+  if (cnt && n <= 16384 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && pt2q_tuning().wbar_fused) {
+    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(64), 0, st, Wt, ldw,
                        n, rem, r, part, wn, cnt);
     PT2Q_LAUNCH_CHECK();
   } else {
@@ -768,8 +781,10 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
       PT2Q_LAUNCH_CHECK();
     }
   }
-  hipLaunchKernelGGL(ssr_sim_kernel, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r,
-                     wn, sim);
+  const bool v4 = (n & 3) == 0 && (ldw & 3) == 0;
+  auto sim_k = !v4 ? ssr_sim_kernel<0> : n <= 4096 ? ssr_sim_kernel<16> : n <= 12288 ? ssr_sim_kernel<48>
+                                                                                   : ssr_sim_kernel<0>;
+  hipLaunchKernelGGL(sim_k, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r, wn, sim);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

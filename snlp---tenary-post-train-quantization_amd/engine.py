@@ -311,7 +311,9 @@ class UnitPipeline:
             ln.workspace(m)
         return self.lanes[0].workspace(m)
 
-    def run(self, Ws, X):
+    def run(self, Ws, X, G: Optional[torch.Tensor] = None):
+        """Issue one unit.  G (optional, diagnostics): a raw Gram of X already computed, read in
+        place of the unit's own Gram launch (the tail alone is issued)."""
         Ws = [_float_input(W) for W in Ws]
         X = _float_input(X.reshape(-1, X.shape[-1]))
         m, N = Ws[0].shape[1], X.shape[0]
@@ -321,6 +323,11 @@ class UnitPipeline:
         st = ln.stream
         st.wait_stream(torch.cuda.current_stream(self.dev))  # inputs written on the caller's stream
         with torch.cuda.stream(st):
+            if G is not None:
+                run = _unit_tail(Ws, G, N, ws, [], X, None, self.bs, self.use_ssr, self.percdamp,
+                                 self.max_iter, torch.int8)
+                run.join = self.join
+                return run
             if self.gram_done is not None:
                 st.wait_event(self.gram_done)
             _lib.check(_lib.lib().pt2q_gram(_lib.ptr(X), _lib.dtype_code(X), N, m, m, _lib.ptr(ws.G), m, 0,

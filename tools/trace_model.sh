@@ -11,3 +11,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o run --output-forma
   python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extra > $OUT/bench.json 2> $OUT/bench.err || exit 1
 python3 $R/tools/kstats.py $(find $OUT -name "run_kernel_trace.csv" | head -1) --top 40 > $OUT/kstats.txt || exit 1
 echo "trace done"
+python3 $R/tools/overlap.py $(find $OUT -name "run_kernel_trace.csv" | head -1) > $OUT/overlap.txt || exit 1
