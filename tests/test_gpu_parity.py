@@ -281,6 +281,25 @@ def test_ssr_topk_ties_vs_oracle(pt2q, n, m, b, dup):
     np.testing.assert_array_equal(host(newrem), rnew)
 
 
+@pytest.mark.parametrize("n,m", [(4096, 700), (11008, 600), (320, 500)])
+def test_ssr_similarity_quotient_paths(pt2q, n, m):
+    """The similarity kernel divides by the column norm through an exact reciprocal quotient
+    when every element and the norm are in range, else by the division itself (wave-uniform):
+    columns with tiny (< 2^-60) or huge (> 2^60) elements and tiny-norm columns take the
+    fallback; every similarity must stay bit-identical to the oracle's plain division."""
+    W = synth.weights(70 + n, n, m)
+    W[:, 3] *= 1e-25          # every element below 2^-60 (and a tiny norm)
+    W[7, 10] = 3e18           # one element above 2^60
+    W[:5, 20] = 1e-20         # a few tiny elements in an otherwise normal column
+    W[:, 30] = 0.0            # an all-zero column (norm clamped to 1e-8)
+    W[:, 40] *= 1e-12         # small norm, elements still in range
+    rem = np.arange(m, dtype=np.int64)[(np.arange(m) % 7) != 2]
+    rem = np.concatenate([rem, np.array([2, 9], dtype=np.int64)])
+    rem.sort()
+    sim = pt2q.compute_column_similarity_to_mean(cuda(W), cuda(rem))
+    assert bits_equal(host(sim), orc.ssr_similarity(W, rem))
+
+
 def test_fill_synthetic_matches_numpy(pt2q):
     a = pt2q.fill_synthetic((300, 257), 1234, std=0.02)
     np.testing.assert_array_equal(host(a), synth.weights(1234, 300, 257))
