@@ -211,21 +211,33 @@ def dequantize_weight_reference(params, block_size: int) -> torch.Tensor:
 @torch.no_grad()
 def quantize_decoder_layer(layer: nn.Module, run_forward, block_size: int = 128,
                            use_ssr: bool = True, percdamp: float = 0.01, layer_idx: int = 0,
-                           writeback: str = "reference", device=None):
+                           writeback: str = "reference", device=None,
+                           pipeline: Optional["engine.UnitPipeline"] = None):
     """One iteration of main.py:258-303 for decoder layer `layer`.
 
     run_forward(capture) must run the calibration forwards (calling capture.next_pass() between
     samples).  Returns {"layer_<i>.<name>": {alpha, mu, T int8, perm}} (device tensors) and
     writes the quantised weights back into the linears ("reference": main.py:297-299 semantics,
-    "correct": gptq.py:201-230 reconstruction, "none": leave weights untouched)."""
+    "correct": gptq.py:201-230 reconstruction, "none": leave weights untouched).  With a
+    UnitPipeline the input groups' tails (their Grams are already captured) run concurrently on
+    its lanes -- they are independent: every input was captured before any write-back -- with
+    results identical to the one-after-another order."""
     linears = find_linear_layers(layer)
     cap = GramCapture(linears, device)
     with cap:
         run_forward(cap)
     results = {}
+    issued = []
     for acc, names in cap.groups():
         Ws = [linears[nm].weight.data.to(acc.device) for nm in names]
-        outs = engine.quantize_shared(Ws, acc.G, acc.nsamples, block_size, use_ssr, percdamp)
+        if pipeline is not None:
+            issued.append((names, pipeline.run(Ws, G=acc.G, nsamples=acc.nsamples)))
+        else:
+            issued.append((names, engine.quantize_shared(Ws, acc.G, acc.nsamples, block_size, use_ssr,
+                                                         percdamp)))
+    for names, outs in issued:
+        if pipeline is not None:
+            outs = outs.finish()
         for nm, out in zip(names, outs):
             lin = linears[nm]
             dt = lin.weight.dtype

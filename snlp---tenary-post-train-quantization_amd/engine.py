@@ -311,12 +311,17 @@ class UnitPipeline:
             ln.workspace(m)
         return self.lanes[0].workspace(m)
 
-    def run(self, Ws, X, G: Optional[torch.Tensor] = None):
-        """Issue one unit.  G (optional, diagnostics): a raw Gram of X already computed, read in
-        place of the unit's own Gram launch (the tail alone is issued)."""
+    def run(self, Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor] = None,
+            nsamples: Optional[int] = None):
+        """Issue one unit: its Gram from X, or -- with G (a raw Gram over nsamples rows, e.g. a
+        GramAccumulator's, read in place and not modified) -- its tail alone."""
         Ws = [_float_input(W) for W in Ws]
-        X = _float_input(X.reshape(-1, X.shape[-1]))
-        m, N = Ws[0].shape[1], X.shape[0]
+        if X is not None:
+            X = _float_input(X.reshape(-1, X.shape[-1]))
+            nsamples = X.shape[0]
+        elif G is None or nsamples is None:
+            raise ValueError("UnitPipeline.run needs X, or G and nsamples")
+        m, N = Ws[0].shape[1], int(nsamples)
         ln = self.lanes[self.turn]
         self.turn = (self.turn + 1) % len(self.lanes)
         ws = ln.workspace(m)
@@ -324,7 +329,8 @@ class UnitPipeline:
         st.wait_stream(torch.cuda.current_stream(self.dev))  # inputs written on the caller's stream
         with torch.cuda.stream(st):
             if G is not None:
-                run = _unit_tail(Ws, G, N, ws, [], X, None, self.bs, self.use_ssr, self.percdamp,
+                G = G.contiguous().float()
+                run = _unit_tail(Ws, G, N, ws, [], X, G, self.bs, self.use_ssr, self.percdamp,
                                  self.max_iter, torch.int8)
                 run.join = self.join
                 return run

@@ -79,13 +79,16 @@ class PT2LLMQuantizer:
         # the calibration forwards run wherever the model lives (main.py:281 moves samples to the
         # model's device); captured inputs stream to the GPU Grams either way
         model_dev = next(self.model.parameters()).device
+        # the units of one decoder layer are independent: their tails run on concurrent lanes
+        pipe = engine.UnitPipeline(self.device, self.block_size, self.use_ssr,
+                                   self.percdamp)
         for idx, layer in enumerate(layers):
             def run(cap):
                 for sample in calibration_samples:
                     self.model(sample.to(model_dev))
                     cap.next_pass()
             res = calibration.quantize_decoder_layer(layer, run, self.block_size, self.use_ssr,
-                                                     self.percdamp, idx, writeback, self.device)
+                                                     self.percdamp, idx, writeback, self.device, pipe)
             for name, p in res.items():
                 self.quantized_params[name] = {k: v.cpu() for k, v in p.items()}
         return self.quantized_params
