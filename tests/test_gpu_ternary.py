@@ -60,7 +60,13 @@ def test_correct_forward_matches_reconstruction(pt2q, name):
                                               (4096, 4096, 128, 7, torch.bfloat16),
                                               (1000, 1100, 128, 300, torch.float16),
                                               (640, 520, 520, 33, torch.bfloat16),
-                                              (4096, 11008, 128, 64, torch.float16)])
+                                              (4096, 11008, 128, 64, torch.float16),
+                                              # prefill kernel (>= 256 tokens): ragged features
+                                              # and tokens, per-channel bf16, 384-wide blocks
+                                              (1000, 1100, 128, 700, torch.float16),
+                                              (600, 640, 640, 513, torch.bfloat16),
+                                              (512, 1536, 384, 256, torch.float16),
+                                              (2048, 4096, 128, 2048, torch.float16)])
 def test_shapes_vs_oracle(pt2q, n, m, bs, tokens, dt):
     """Decode (1 token, K split), prefill, ragged m (padded positions), per-channel, bf16."""
     rng = np.random.default_rng(n + m + tokens)
