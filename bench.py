@@ -18,7 +18,10 @@ width is shared by the units of that width on a rank; every unit still computes 
 
 `extra` carries the single-layer numbers (s/layer and cols/s of the 4096x4096 q_proj layer at
 N = 262144 and N = 2048, one hipGraph replay each).  `--workload layer` times that single layer
-per rank instead (weak scaling, the round-1 bench line).
+per rank instead (weak scaling, the round-1 bench line).  `--workload split --n 4096 --m 11008`
+times ONE layer whose Gram is split over the ranks' calibration rows (strong scaling, SURVEY
+§8e(ii): sharding.quantize_layer_split — partial Grams, rank-ordered fold on rank 0, the rest of
+the layer there).
 """
 import argparse
 import json
@@ -47,7 +50,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["model", "layer"], default="model")
+    p.add_argument("--workload", choices=["model", "layer", "split"], default="model",
+                   help="model: LPT-sharded 7B step; layer: one layer per rank (weak); split: one n x m "
+                        "layer, its Gram data-parallel over the ranks (strong)")
     p.add_argument("--layers", type=int, default=32, help="decoder layers of the model workload")
     p.add_argument("--hidden", type=int, default=4096)
     p.add_argument("--inter", type=int, default=11008)
@@ -228,6 +233,25 @@ class LayerStep:
         return out
 
 
+class SplitStep:
+    """One n x m layer whose Gram is split over the ranks' calibration rows:
+    partial Grams -> rank-ordered fold on rank 0 -> Cholesky inverse and block loop there."""
+
+    def __init__(self, a, rank, world, dev, io):
+        lo, hi = sharding.row_slice(a.tokens, rank, world)
+        self.X = pt2q.fill_synthetic((hi - lo, a.m), 3000 + rank, std=1.0, outliers=True, device=dev).to(io)
+        self.W = pt2q.fill_synthetic((a.n, a.m), 1000, std=0.02, device=dev).to(io) if rank == 0 else None
+        self.bs, self.ssr = a.block_size, not a.no_ssr
+        self.units = [("layer", [("proj", a.n, a.m)], a.tokens)]
+
+    def step(self):
+        outs = sharding.quantize_layer_split([self.W], self.X, dst=0, block_size=self.bs,
+                                             use_ssr=self.ssr)
+        if outs is not None and not outs[0].spd:
+            raise RuntimeError("synthetic Hessian not SPD")
+        return outs
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -242,7 +266,7 @@ def main():
     use_ssr = not a.no_ssr
 
     t_setup = time.perf_counter()
-    work = ModelStep(a, rank, world, dev, io) if a.workload == "model" else LayerStep(a, rank, world, dev, io)
+    work = {"model": ModelStep, "layer": LayerStep, "split": SplitStep}[a.workload](a, rank, world, dev, io)
     log(rank, f"{a.workload} inputs resident ({time.perf_counter() - t_setup:.1f}s); warmup {a.warmup}")
     for i in range(a.warmup):
         work.step()
@@ -267,12 +291,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / max(a.steps, 1)
-    cols = sharding.units_cols(work.units) if a.workload == "model" else world * a.m
+    cols = {"model": sharding.units_cols(work.units), "layer": world * a.m, "split": a.m}[a.workload]
     log(rank, f"timed {a.steps} steps: {ms_per_step:.1f} ms/step")
 
     extra = {}
     roof = None
-    if rank == 0 and not a.no_extra:
+    if rank == 0 and not a.no_extra and a.workload != "split":
         # the d=4096 q_proj layer alone (s/layer at d=4096): one hipGraph replay per layer
         if a.workload == "model":
             Wl = pt2q.fill_synthetic((d, d), 1000, std=0.02, device=dev).to(io)
@@ -344,7 +368,8 @@ def main():
         model_desc = (f"llama-2-7b shapes: {a.layers} layers x (q,k,v,o {d}x{d}; gate,up {a.inter}x{d}; "
                       f"down {d}x{a.inter}) = {sum(len(l) for _, l, _ in work.units)} linears in "
                       f"{len(work.units)} shared-input units" if a.workload == "model" else
-                      f"one {a.n}x{a.m} linear per rank")
+                      f"one {a.n}x{a.m} linear per rank" if a.workload == "layer" else
+                      f"one {a.n}x{a.m} linear, its Gram split over {world} ranks' calibration rows")
         res = {
             "metric": "weight-columns quantized/sec (and s/layer) at d=4096",
             "value": cols / (ms_per_step * 1e-3),
@@ -354,7 +379,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong" if a.workload == "model" else "weak",
+            "scaling": "weak" if a.workload == "layer" else "strong",
             "vs_baseline": None,
             "dtype": "fp16->f32" if a.io_dtype != "fp32" else "f32",
             "data": ("synthetic (counter-hash fp16 weights std 0.02; fp16 activations, unit variance, "
@@ -363,8 +388,9 @@ def main():
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
                        "weight_columns_per_step": cols, "tokens": N, "io_dtype": a.io_dtype,
                        "block_size": bs,
-                       "parallelism": (f"LPT unit sharding x{world}" if a.workload == "model" else
-                                       f"layer per rank x{world}") + (", rccl gather" if world > 1 else "")
+                       "parallelism": ({"model": f"LPT unit sharding x{world}", "layer": f"layer per rank x{world}",
+                                        "split": f"Gram rows x{world}, rank-ordered fold on rank 0"}[a.workload])
+                                  + (", rccl gather" if world > 1 else "")
                                   + (f", {a.lanes} unit lanes (Grams chained, tails overlapped)"
                                      if a.workload == "model" and not a.no_overlap else "")},
         }
@@ -373,7 +399,7 @@ def main():
         if roof is not None:
             res["roofline"] = roof
         res["extra"] = extra
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and a.workload != "split":
             log(rank, "cpu baseline (oracle) ...")
             units = work.units if a.workload == "model" else [("layer", [("proj", a.n, a.m)], N)]
             res["cpu_baseline"] = cpu_baseline(units, N, bs, use_ssr, d if a.workload == "model" else a.m)

@@ -168,6 +168,15 @@ int pt2q_dequantize(const float* alpha, const float* mu, const void* T, int tdty
 int pt2q_pack_ternary(const int8_t* T, int64_t count, uint8_t* packed, void* stream);
 int pt2q_unpack_ternary(const uint8_t* packed, int64_t count, int8_t* T, void* stream);
 
+/* out = ((parts[0] + parts[1]) + parts[2]) + ... + parts[nparts-1], elementwise fp32 in rank order;
+ * part p starts at parts + p*stride (count floats each; count and stride multiples of 4, 16-byte
+ * aligned; out may be parts[0]).  The deterministic reduction of the intra-layer split
+ * (the Gram of main.py:128 data-parallel over the N calibration rows, one partial
+ * Gram per rank, folded on the destination rank in rank order) -- an all-reduce would leave the
+ * order to the ring schedule. */
+int pt2q_sum_partials(const float* parts, int64_t stride, int nparts, int64_t count, float* out,
+                      void* stream);
+
 /* Counter-based synthetic tensors (tests/synth.py): out[i] = c_i * scale with
  * c_i = (splitmix64(splitmix64(seed) + i) >> 40) - 2^23; when outlier_every > 0, columns j
  * (= i % cols) with splitmix64(splitmix64(seed ^ 0x5BD1E995) + j) % outlier_every == 0 use

@@ -330,6 +330,37 @@ def quantize_layer_m(W, X, block_size=128, use_ssr=True, percdamp=0.01, max_iter
     return out
 
 
+def sum_partials(parts):
+    """Rank-ordered fold ((P0 + P1) + P2) + ... in fp32 (the intra-layer split's reduction)."""
+    acc = _f32(parts[0]).copy()
+    for p in parts[1:]:
+        acc = (acc + _f32(p)).astype(np.float32)
+    return acc
+
+
+def row_slices(N, world):
+    """The calibration-row split of the intra-layer split: rank r takes rows
+    [r*N//world, (r+1)*N//world) (sharding.row_slice)."""
+    return [(r * N // world, (r + 1) * N // world) for r in range(world)]
+
+
+def quantize_layer_split(W, X, world, block_size=128, use_ssr=True, percdamp=0.01, max_iter=100):
+    """main.py:102-230 (variant M) with the Gram of main.py:128 data-parallel over `world` ranks
+    (SURVEY §8e(ii)): each rank's rows form their own Gram chain from +0, the partial Grams are
+    folded in rank order, the rest is the single-rank layer on that G with nsamples = N."""
+    if not is16(X):
+        X = _f32(X)
+    if X.ndim == 3:
+        X = X.reshape(-1, X.shape[-1])
+    G = sum_partials([gram_any(X[a:b]) for a, b in row_slices(X.shape[0], world)])
+    H, _ = prepare_hessian(G, X.shape[0], percdamp)
+    Hinv, spd = cholesky_inverse(H)
+    out = quantize_blocks(W, G, Hinv, block_size, use_ssr, 1, max_iter)
+    out["spd"] = spd
+    out["G"] = G
+    return out
+
+
 def quantize_layer_g(W, Hsum, nsamples, block_size=128, use_ssr=True, percdamp=0.01, max_iter=100):
     """GPTQ.quantize gptq.py:78-199 (variant G) given the accumulated H = Σ XᵢᵀXᵢ."""
     H, _ = prepare_hessian(Hsum, nsamples, percdamp)

@@ -22,7 +22,7 @@ from .ternary import (TernaryLinear, compute_bits_per_weight, load_quantized_mod
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, UnitRun, UnitWorkspace, cholesky_inverse,
                      dequantize, error_feedback, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
                      quantize_blocks, quantize_layer, quantize_shared, quantize_unit, unpack_ternary,
-                     UnitPipeline)
+                     UnitPipeline, sum_partials)
 
 __version__ = "0.1.0"
 __all__ = [
@@ -34,5 +34,5 @@ __all__ = [
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
     "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
     "UnitRun", "UnitWorkspace", "quantize_unit", "compute_bits_per_weight", "error_feedback",
-    "UnitPipeline",
+    "UnitPipeline", "sum_partials",
 ]

@@ -63,6 +63,7 @@ _SIGS = {
     "pt2q_pack_ternary": (I, [P, I64, P, P]),
     "pt2q_unpack_ternary": (I, [P, I64, P, P]),
     "pt2q_fill_synthetic": (I, [P, I64, ctypes.c_uint64, F, I64, I, F, P]),
+    "pt2q_sum_partials": (I, [P, I64, I, I64, P, P]),
     "pt2q_ternary_linear_positions": (SZ, [I]),
     "pt2q_ternary_pack": (I, [P, I64, I, I, P, I, P, P, P]),
     "pt2q_ternary_linear_workspace_bytes": (SZ, [I, I, I]),

@@ -218,6 +218,27 @@ __global__ void fill_kernel(float* out, long count, uint64_t base, float scale, 
   }
 }
 
+// out[i] = ((P_0[i] + P_1[i]) + P_2[i]) + ... : the rank-ordered fold of per-rank partial Grams
+// (intra-layer split, sharding.quantize_layer_split).  Four elements per thread (16-byte loads;
+// count % 4 == 0, 16-byte aligned parts), every part's load issued before the first add.  With
+// `acc0` the fold continues from acc0 (the result of the previous group of parts).
+template <int NP>
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* acc0, const float* P, long stride,
+                                                        long count4, int parts, float* out) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  for (long q = (long)blockIdx.x * 256 + threadIdx.x; q < count4; q += (long)gridDim.x * 256) {
+    f32x4 v[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if (p < parts) v[p] = *(const f32x4*)(P + p * stride + 4 * q);
+    f32x4 acc = acc0 ? *(const f32x4*)(acc0 + 4 * q) : v[0];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if (p < parts && (acc0 || p > 0)) acc = acc + v[p];
+    *(f32x4*)(out + 4 * q) = acc;
+  }
+}
+
 }  // namespace
 
 int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,
@@ -361,5 +382,28 @@ extern "C" int pt2q_fill_synthetic(float* out, int64_t count, uint64_t seed, flo
   hipLaunchKernelGGL(fill_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, out,
                      (long)count, base, scale, (long)cols, outlier_every, obase, scale_outlier);
   PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+// out = ((parts[0] + parts[1]) + ...) + parts[nparts-1], elementwise fp32, parts `stride`
+// floats apart (sharding.quantize_layer_split: the rank-ordered fold of partial Grams).
+extern "C" int pt2q_sum_partials(const float* parts, int64_t stride, int nparts, int64_t count,
+                                 float* out, void* stream) {
+  if (nparts <= 0 || count < 0 || !parts || !out || (nparts > 1 && stride < count)) return PT2Q_E_ARG;
+  if (count % 4 || stride % 4 || (uintptr_t)parts % 16 || (uintptr_t)out % 16) return PT2Q_E_UNSUPPORTED;
+  if (count == 0) return PT2Q_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const long c4 = count / 4;
+  const unsigned grid = (unsigned)std::min<long>(ceil_div(c4, 256), 4096);
+  constexpr int NP = 8;
+  const float* acc0 = nullptr;
+  for (int p0 = 0; p0 < nparts; p0 += NP) {  // groups of 8 parts; each group continues the fold
+    const int np = std::min(NP, nparts - p0);
+    if (np == 1 && !acc0 && out == parts) return PT2Q_OK;
+    hipLaunchKernelGGL(sum_parts_kernel<NP>, dim3(grid), dim3(256), 0, st, acc0, parts + (long)p0 * stride,
+                       (long)stride, c4, np, out);
+    PT2Q_LAUNCH_CHECK();
+    acc0 = out;
+  }
   return PT2Q_OK;
 }

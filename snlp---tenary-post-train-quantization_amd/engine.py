@@ -67,6 +67,22 @@ def gram(X: torch.Tensor, G: Optional[torch.Tensor] = None, accumulate=False,
     return G
 
 
+def sum_partials(parts: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """((parts[0] + parts[1]) + parts[2]) + ... elementwise in fp32, in index order (the
+    deterministic rank-ordered reduction of the intra-layer split; out may alias parts[0]).
+    parts: (P, ...) fp32, contiguous, on a HIP device."""
+    _lib.require_device(parts)
+    if parts.dtype != torch.float32 or not parts.is_contiguous():
+        raise _lib.Pt2qError("sum_partials: parts must be a contiguous fp32 (P, ...) device tensor")
+    P = parts.shape[0]
+    count = parts[0].numel()
+    if out is None:
+        out = torch.empty(parts.shape[1:], dtype=torch.float32, device=parts.device)
+    _lib.check(_lib.lib().pt2q_sum_partials(_lib.ptr(parts), count, P, count, _lib.ptr(out),
+                                            _lib.stream_of(parts.device)), "pt2q_sum_partials")
+    return out
+
+
 def prepare_hessian(G: torch.Tensor, nsamples: int, percdamp: float = 0.01):
     """H = G / nsamples + percdamp * mean(diag) * I (main.py:129-133, gptq.py:94-98)."""
     m = G.shape[0]

@@ -202,3 +202,58 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
     if not gather:
         return results, mine
     return gather_results(results, dst=dst, group=group), mine
+
+
+# ----------------------------------------------------------------- intra-layer split (§8e(ii))
+
+def row_slice(N: int, rank: int, world: int):
+    """Calibration rows [lo, hi) of `rank` in the intra-layer split (contiguous, balanced)."""
+    return rank * N // world, (rank + 1) * N // world
+
+
+def quantize_layer_split(Ws, X_local: torch.Tensor, dst: int = 0, group=None, block_size: int = 128,
+                         use_ssr: bool = True, percdamp: float = 0.01, max_iter: int = 100,
+                         gram_fn: Optional[Callable] = None, sum_fn: Optional[Callable] = None,
+                         layer_fn: Optional[Callable] = None):
+    """One layer (or a unit of linears sharing an input) too big for one GPU's share of the
+    step, its Gram data-parallel over the ranks (main.py:128-230).
+
+    Every rank holds its slice of the N calibration rows (row_slice) and forms its partial Gram
+    Xᵣᵀ Xᵣ (a chain from +0, engine.gram).  The partials go point-to-point to `dst`, which folds
+    them in rank order (engine.sum_partials: ((G₀ + G₁) + G₂) + …, deterministic -- an RCCL
+    all-reduce would leave the summation order to the ring schedule) and runs the rest of the
+    layer there: damping with nsamples = Σ rows, Cholesky inverse, block loops of every W in Ws.
+    The result is bit-identical to oracle.quantize_layer_split for the same row split.
+
+    gram_fn(X) -> G, sum_fn(parts (P, m, m)) -> G and layer_fn(Ws, G, nsamples) -> outputs
+    default to the libpt2q kernels (engine.gram / sum_partials / quantize_shared); tests on CPU
+    (gloo) substitute their own.  Returns layer_fn's outputs on dst, None elsewhere."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if gram_fn is None or sum_fn is None or layer_fn is None:
+        from . import engine
+        gram_fn = gram_fn or engine.gram
+        sum_fn = sum_fn or engine.sum_partials
+
+        def _layer(Ws_, G, nsamples):
+            return engine.quantize_shared(Ws_, G, nsamples, block_size, use_ssr, percdamp, max_iter)
+        layer_fn = layer_fn or _layer
+    X2 = X_local.reshape(-1, X_local.shape[-1])
+    m = X2.shape[1]
+    dev = X2.device
+    rows = torch.tensor([X2.shape[0]], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(rows, group=group)  # exact integer sum: nsamples of main.py:129
+    nsamples = int(rows.item())
+    if rank != dst:
+        G = gram_fn(X2).contiguous()
+        dist.send(G, dst=dst, group=group)
+        return None
+    parts = torch.empty((world, m, m), dtype=torch.float32, device=dev)
+    ops = [dist.P2POp(dist.irecv, parts[r], r, group) for r in range(world) if r != dst]
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    parts[dst].copy_(gram_fn(X2))
+    for req in reqs:
+        req.wait()
+    G = sum_fn(parts)
+    return layer_fn(list(Ws), G, nsamples)

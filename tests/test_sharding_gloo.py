@@ -185,3 +185,82 @@ def test_flatten_roundtrip_cpu():
     for k, v in res.items():
         for f, t in v.items():
             assert back[k][f].dtype == t.dtype and torch.equal(back[k][f], t)
+
+
+# ----------------------------------------------------------------- intra-layer split (§8e(ii))
+
+def _worker_split(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import numpy as np
+    import synth
+    from oracle import oracle as orc
+    sh = _sharding()
+    N, m = 203, 48  # ragged row split: 67 / 68 / 68
+    X = synth.activations(77, N, m).astype(np.float16)
+    lo, hi = sh.row_slice(N, rank, world)
+    calls = []
+
+    def gram_fn(Xr):
+        calls.append(Xr.shape[0])
+        return torch.from_numpy(orc.gram16(Xr.numpy()))
+
+    def sum_fn(parts):
+        return torch.from_numpy(orc.sum_partials([p.numpy() for p in parts]))
+
+    def layer_fn(Ws, G, nsamples):
+        return {"G": G.numpy().copy(), "nsamples": nsamples, "Ws": Ws}
+
+    out = sh.quantize_layer_split(["w"], torch.from_numpy(X[lo:hi]), dst=0, gram_fn=gram_fn,
+                                  sum_fn=sum_fn, layer_fn=layer_fn)
+    q.put(("rows", rank, calls))
+    if rank == 0:
+        q.put(("out", 0, out))
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_layer_split_rank_ordered_gram_world3():
+    """Each rank forms the Gram of its calibration rows; dst folds the partials in rank order and
+    runs the layer with nsamples = all rows (oracle.quantize_layer_split's G)."""
+    import numpy as np
+    import synth
+    from oracle import oracle as orc
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_split, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=90) for _ in range(world + 1)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rows = {r: c for k, r, c in got if k == "rows"}
+    out = [v for k, _, v in got if k == "out"][0]
+    N, m = 203, 48
+    assert rows == {r: [hi - lo] for r, (lo, hi) in enumerate(orc.row_slices(N, world))}
+    assert out["nsamples"] == N and out["Ws"] == ["w"]
+    X = synth.activations(77, N, m).astype(np.float16)
+    ref = orc.sum_partials([orc.gram16(X[a:b]) for a, b in orc.row_slices(N, world)])
+    assert np.array_equal(out["G"], ref)
+
+
+def test_oracle_split_one_rank_is_the_layer():
+    """oracle.quantize_layer_split with one rank is quantize_layer_m; with several ranks its G is
+    the rank-ordered fold of the slices' Grams (a different rounding, same matrix to ~1e-6)."""
+    import numpy as np
+    import synth
+    from oracle import oracle as orc
+    W = synth.weights(31, 64, 96)
+    X = synth.activations(32, 300, 96)
+    a, b = orc.quantize_layer_split(W, X, 1), orc.quantize_layer_m(W, X)
+    for k in ("T", "perm", "alpha", "mu"):
+        assert np.array_equal(a[k], b[k])
+    G3 = orc.quantize_layer_split(W, X, 3)["G"]
+    G1 = orc.gram(X)
+    assert np.allclose(G3, G1, rtol=1e-5, atol=1e-3)
