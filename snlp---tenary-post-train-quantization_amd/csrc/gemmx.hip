@@ -288,7 +288,10 @@ int pt2q_launch_gemmx(const GemmDesc& g, hipStream_t st) {
   } else {
     tiles = (long)X.tiles_m * X.tiles_n;
   }
-  hipLaunchKernelGGL(gemmx_kernel<3>, dim3((unsigned)tiles), dim3(256), 0, st, X);
+  if (pt2q_tuning().gemmx_stages == 2)  // 64 KiB of LDS: two workgroups per CU
+    hipLaunchKernelGGL(gemmx_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, X);
+  else
+    hipLaunchKernelGGL(gemmx_kernel<3>, dim3((unsigned)tiles), dim3(256), 0, st, X);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
