@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--io-dtype", choices=["fp16", "fp32", "bf16"], default="fp16")
     p.add_argument("--no-ssr", action="store_true")
     p.add_argument("--lanes", type=int, default=3, help="model workload: UnitPipeline lanes")
+    p.add_argument("--schedule", choices=["grams-first", "interleaved"], default="grams-first",
+                   help="model workload: every Gram of the step first, then the tails on the lanes "
+                        "(sharding.GramsFirst), or each unit's Gram on its lane before its tail")
     p.add_argument("--no-overlap", action="store_true",
                    help="model workload: run the units strictly one after another on one stream "
                         "(default: engine.UnitPipeline overlaps unit i+1's Gram with unit i's tail)")
@@ -183,6 +186,8 @@ class ModelStep:
         self.mine = self.shards[rank]
         self.bs, self.ssr = a.block_size, not a.no_ssr
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
+        self.schedule = a.schedule
+        self.gf = sharding.GramsFirst(self.pipe, dev) if self.pipe is not None else None
         self.X, self.W, self.ws = {}, {}, {}
         self.index = {u[0]: i for i, u in enumerate(self.units)}
         for i in self.mine:
@@ -209,8 +214,9 @@ class ModelStep:
                                   workspace=self.ws[X.shape[1]], defer=True)
 
     def step(self):
+        gf = self.gf if self.schedule == "grams-first" and self.pipe is not None else None
         res, _ = sharding.quantize_units_sharded(self.units, self.provider, run_unit=self.run_unit,
-                                                 pack=True, dst=0)
+                                                 pack=True, dst=0, grams_first=gf)
         return res
 
 
@@ -391,7 +397,9 @@ def main():
                        "parallelism": ({"model": f"LPT unit sharding x{world}", "layer": f"layer per rank x{world}",
                                         "split": f"Gram rows x{world}, rank-ordered fold on rank 0"}[a.workload])
                                   + (", rccl gather" if world > 1 else "")
-                                  + (f", {a.lanes} unit lanes (Grams chained, tails overlapped)"
+                                  + ((f", every Gram first then the tails on {a.lanes} unit lanes"
+                                      if a.schedule == "grams-first" else
+                                      f", {a.lanes} unit lanes (Grams chained, tails overlapped)")
                                      if a.workload == "model" and not a.no_overlap else "")},
         }
         if a.workload == "model":

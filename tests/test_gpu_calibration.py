@@ -119,3 +119,30 @@ def test_unit_pipeline_equals_sequential(pt2q, lanes):
         for o, r in zip(outs, want):
             for a, b in ((o.alpha, r.alpha), (o.mu, r.mu), (o.T, r.T), (o.perm, r.perm), (o.iters, r.iters)):
                 assert bits_equal(host(a), host(b))
+
+
+def test_grams_first_schedule_equals_sequential(pt2q):
+    """sharding.GramsFirst (every Gram of the step first, each into its own buffer, then the
+    tails on the pipeline lanes) through quantize_units_sharded == quantize_unit per unit."""
+    import importlib
+    sharding = importlib.import_module("pt2q.sharding")
+    specs = [(512, (384, 256), 1024, torch.float16), (768, (512,), 2048, torch.float16),
+             (512, (640,), 1024, torch.float32), (768, (256,), 1536, torch.float16)]
+    units, data = [], {}
+    for i, (m, ns, N, dt) in enumerate(specs):
+        X = cuda(synth.activations(800 + i, N, m)).to(dt)
+        Ws = {f"p{k}": cuda(synth.weights(900 + 10 * i + k, n, m)).to(dt) for k, n in enumerate(ns)}
+        units.append((f"u{i}", [(f"p{k}", n, m) for k, n in enumerate(ns)], N))
+        data[f"u{i}"] = (X, Ws)
+    pipe = pt2q.UnitPipeline("cuda", 128, True, lanes=3)
+    gf = sharding.GramsFirst(pipe, "cuda")
+    res, mine = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False,
+                                                grams_first=gf)
+    assert mine == list(range(len(units))) or sorted(mine) == list(range(len(units)))
+    for name, lins, _ in units:
+        X, Ws = data[name]
+        want = pt2q.quantize_unit([Ws[p] for p, _, _ in lins], X, block_size=128, use_ssr=True)
+        for (p, _, _), r in zip(lins, want):
+            o = res[f"{name}.{p}"]
+            for k, b in (("alpha", r.alpha), ("mu", r.mu), ("T", r.T), ("perm", r.perm)):
+                assert bits_equal(host(o[k]), host(b)), (name, p, k)

@@ -264,3 +264,30 @@ def test_oracle_split_one_rank_is_the_layer():
     G3 = orc.quantize_layer_split(W, X, 3)["G"]
     G1 = orc.gram(X)
     assert np.allclose(G3, G1, rtol=1e-5, atol=1e-3)
+
+
+def test_grams_first_orders_phases_single_process():
+    """quantize_units_sharded(grams_first=...) forms every unit's Gram before any tail, keeps
+    the per-unit pairing, and returns the same result dict as the per-unit path."""
+    sh = _sharding()
+    units = _mixed_units()
+    provider, run_unit = _fake_run(units)
+    log = []
+
+    class FakeGF:
+        def gram(self, key, X):
+            log.append(("gram", key))
+
+        def tail(self, key, Ws, N):
+            log.append(("tail", key))
+            return run_unit(Ws, None)
+
+    got, mine = sh.quantize_units_sharded(units, provider, pack=False, grams_first=FakeGF())
+    want, _ = sh.quantize_units_sharded(units, provider, run_unit=run_unit, pack=False)
+    kinds = [k for k, _ in log]
+    assert kinds == ["gram"] * len(mine) + ["tail"] * len(mine)
+    assert [i for _, i in log[:len(mine)]] == [i for _, i in log[len(mine):]] == mine
+    assert got.keys() == want.keys()
+    for k in got:
+        for f in got[k]:
+            assert torch.equal(got[k][f], want[k][f])
