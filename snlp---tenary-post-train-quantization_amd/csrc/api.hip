@@ -38,7 +38,7 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_EF_GEMM", t.ef_kernel);
   if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
     const long c = std::atol(e);
-    if (c >= 0) t.spin_cap_long = t.spin_cap_short = c;
+    if (c >= 0) t.spin_cap_long = t.spin_cap_short = t.spin_cap_fallback = c;
   }
   return t;
 }

@@ -201,6 +201,45 @@ struct BlockArgs {
   long cap;          // polls before a wait gives up
 };
 
+// S1 / d of the block formed by one wave itself, in the order of atq_s1_part (S1[j]: l-ascending
+// sum of G[blk_j][blk_l]; d: j-ascending sum of S1), so the values are the same bits.  The
+// fallback of a row wave whose wait for the leading workgroups gives up: under heavy concurrency
+// (several streams of launches with in-launch hand-offs) those workgroups can sit undispatched on
+// a full XCD while this wave holds its CU, so the wave computes instead of waiting or failing.
+// Lane (r, l) forms S1[l + 16 s]; d gathers S1[j] from lane (r, j & 15), slot j >> 4.
+template <int NS>
+PT2Q_DEV void s1_local(const BlockArgs& A, int l, float (&S1)[NS], float* dv) {
+  const int b = A.b;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = l + 16 * s;
+    float acc = 0.0f;
+    if (k < b) {
+      const long bj = (long)A.blk[k] * A.ldg;
+      int q = 0;
+      for (; q + 8 <= b; q += 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = A.G[bj + A.blk[q + u]];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + t[u];
+      }
+      for (; q < b; ++q) acc = acc + A.G[bj + A.blk[q]];
+    }
+    S1[s] = acc;
+  }
+  const int base = (int)(threadIdx.x & 63) & 48;
+  float d = 0.0f;
+  for (int j = 0; j < b; ++j) {
+    float x = 0.0f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if ((j >> 4) == s) x = S1[s];
+    d = d + __shfl(x, base | (j & 15));
+  }
+  *dv = d;
+}
+
 // Returns the wave's ITF iteration count (wave-uniform).
 template <int NS, bool F = false>
 PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_zero) {
@@ -241,15 +280,21 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   int it = 0;
   if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
   if (A.S1 && A.nS1 > 0) {  // S1 / d from this launch's leading workgroups (write-through)
-    if ((threadIdx.x & 63) == 0) wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, A.status, STALL_ATQ_S1);
+    int ready = 1;
+    if ((threadIdx.x & 63) == 0) ready = wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, nullptr, 0);
+    ready = __builtin_amdgcn_readfirstlane(ready);
     __builtin_amdgcn_wave_barrier();
+    if (ready) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int k = l + 16 * s;
-      const float x = __hip_atomic_load(&A.S1w[k < A.b ? k : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      S1[s] = k < A.b ? x : 0.0f;
+      for (int s = 0; s < NS; ++s) {
+        const int k = l + 16 * s;
+        const float x = __hip_atomic_load(&A.S1w[k < A.b ? k : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        S1[s] = k < A.b ? x : 0.0f;
+      }
+      dv = __hip_atomic_load(A.dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      s1_local<NS>(A, l, S1, &dv);
     }
-    dv = __hip_atomic_load(A.dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (A.S1) row_aga(R, S1, dv, &a, &m);
   if (!valid) return it;
@@ -807,7 +852,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   }
   const int nS1 = (G && S1 && s1sync && b <= 128) ? ceil_div(b, 8) : 0;
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part,
-              G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_short};
+              G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_fallback};
   int grid = ceil_div(n, ROWS_PER_WG);
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;

@@ -117,6 +117,7 @@ struct Pt2qTuning {
   // (0: every hand-off reports a stall -- tests force the reporting path with it).
   long spin_cap_long = 1l << 28;   // Gram partial-tile hand-offs (a long chain may be in flight)
   long spin_cap_short = 1l << 26;  // in-launch hand-offs (S1 / d, top-k picks)
+  long spin_cap_fallback = 1l << 13;  // ATQ S1 / d wait: polls before the wave forms S1 / d itself
 };
 const Pt2qTuning& pt2q_tuning();  // api.hip
 
