@@ -10,7 +10,9 @@ the model).  Linears that read the same input (q/k/v, gate/up) form one work uni
 Gram and one Cholesky inverse (128 units).  With N GPUs (torchrun, one rank per GPU) the units
 are split longest-processing-time first (sharding.assign_lpt) — the total work is fixed, so the
 scaling is STRONG — and every rank's results (2-bit packed codes, scales, permutation) are
-gathered to rank 0 over RCCL inside the timed step.
+gathered to rank 0 over RCCL inside the timed step.  Per rank, every Gram of its units runs first
+(one raw-Gram buffer per unit), then the units' tails on three stream lanes (sharding.GramsFirst;
+`--schedule interleaved` puts each Gram on its lane before its tail instead).
 
 Data: synthetic, resident in HBM before timing (fp16 weights, counter-hash, std 0.02; fp16
 activations, unit variance with 1 % x20 outlier channels).  One activation tensor per input
