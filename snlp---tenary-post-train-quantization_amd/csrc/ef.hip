@@ -29,7 +29,6 @@ constexpr int EF_STAGE = 2 * EF_PANEL;       // A + B
 constexpr int EF_DMA = 16;                   // DMA instructions per wave per stage
 constexpr int EF_CV = 16;                    // C float4 loads (= stores) per lane per tile
 constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropped access)
-constexpr int EF_MAX_NR = 16384;             // remaining columns staged in LDS (16-bit rows)
 
 __device__ uint4 ef_zero16;  // DMA source of the k rows past bs (zero-initialised)
 
@@ -146,12 +145,17 @@ PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm,
   return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
 }
 
-PT2Q_DEV void ef_rows(const EfArgs& a, const uint16_t* crow_lds, int e0, int (&wrow)[2]) {
+// the Wt rows of this lane's two output rows (crow from L2: two loads per lane, issued uniformly
+// by every wave and older than every operation a later hand-counted vmcnt wait covers)
+PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
+  int v[2];
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm) {
     const int e = ef_row(e0, rm);
-    wrow[rm] = e < a.nr ? (int)crow_lds[e] : -1;
+    v[rm] = a.crow[e < a.nr ? e : 0];
   }
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm) wrow[rm] = ef_row(e0, rm) < a.nr ? v[rm] : -1;
 }
 
 struct EfNoIO {
@@ -195,12 +199,10 @@ PT2Q_DEV void ef_vmcnt(int n) {
 
 __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
-  __shared__ uint16_t crow_lds[EF_MAX_NR];
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   int t = blockIdx.x;
   if (t >= a.ntile) return;
-  for (int e = threadIdx.x; e < a.nr; e += blockDim.x) crow_lds[e] = (uint16_t)a.crow[e];
   auto corner = [&](int t, int& e0, int& i0) {
     e0 = (t / a.ti) * EF_T;
     i0 = (t % a.ti) * EF_T;
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
   corner(t, e0, i0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  ef_rows(a, crow_lds, e0, wrow);
+  ef_rows(a, e0, wrow);
   ef_stage(a, e0, i0, 0, smem);
   if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
   int prow[2] = {-1, -1}, pi0 = 0;
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
       for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
     ef_vmcnt(S1);  // stage 0 landed (younger: stage 1)
     asm volatile("s_barrier" ::: "memory");
-    if (more) ef_rows(a, crow_lds, en, nrow);
+    if (more) ef_rows(a, en, nrow);
     {
       EfIO io{a, rc, prow, pi0, wrow, i0, pend, c};
       F.half(lds0, io);
@@ -282,7 +284,7 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   if (nr <= 0) return PT2Q_OK;
   const long wt_bytes = wt_rows * ldw * 4;
   if (bs <= 0 || bs > 2 * EF_KH || ldw % 4 || ldk % 4 || (uintptr_t)Ck % 16 || (uintptr_t)Et % 16 ||
-      (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP || nr > EF_MAX_NR || wt_rows > 65536)
+      (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP || wt_rows > 65536)
     return PT2Q_E_UNSUPPORTED;
   EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1};
   a.ntile = a.te * a.ti;
