@@ -4,12 +4,12 @@ Default workload (BASELINE.json metric "weight-columns quantized/sec (and s/laye
 1/2/4/8 MI355X", config C4 "Llama-2-7B fp16, full ATQ+SSR pipeline, layers sharded across
 8×MI355X via RCCL/xGMI"): one step quantises EVERY linear of a Llama-2-7B-shaped model (32
 decoder layers x {q,k,v,o 4096x4096; gate,up 11008x4096; down 4096x11008} = 224 linears,
-1,269,760 weight columns), each calibrated on N = 262144 activation rows (the reference CLI
+1,138,688 weight columns), each calibrated on N = 262144 activation rows (the reference CLI
 default 128 samples x 2048 tokens), variant M (main.py:102-230 per linear, main.py:257-304 over
 the model).  Linears that read the same input (q/k/v, gate/up) form one work unit sharing one
 Gram and one Cholesky inverse (128 units).  With N GPUs (torchrun, one rank per GPU) the units
-are split longest-processing-time first (sharding.assign_lpt) — the total work is fixed, so the
-scaling is STRONG — and every rank's results (2-bit packed codes, scales, permutation) are
+are split longest-processing-time first (sharding.assign_lpt on a measured-time cost model) — the
+total work is fixed, so the scaling is STRONG — and every rank's results (2-bit packed codes, scales, permutation) are
 gathered to rank 0 over RCCL inside the timed step.  Per rank, every Gram of its units runs first
 (one raw-Gram buffer per unit), then the units' tails on three stream lanes (sharding.GramsFirst;
 `--schedule interleaved` puts each Gram on its lane before its tail instead).
@@ -24,32 +24,40 @@ per rank instead (weak scaling, the round-1 bench line).  `--workload split --n 
 times ONE layer whose Gram is split over the ranks' calibration rows (strong scaling, SURVEY
 §8e(ii): sharding.quantize_layer_split — partial Grams, rank-ordered fold on rank 0, the rest of
 the layer there).
+
+Ranks: `python bench.py --gpus N` with no WORLD_SIZE in the environment starts the N ranks itself
+(a `torch.distributed.run` child with one process per GPU, launched before this process imports
+torch or touches the GPU; this process exits with the child's code).  Under an external launcher
+(torchrun / `python -m torch.distributed.run ... bench.py --gpus N`) the flag must equal
+WORLD_SIZE, else the run is refused; `n_gpus` in the line is `dist.get_world_size()`.
+`--dry-run` exercises the same multi-rank plumbing on CPU (gloo, stub units, no libpt2q) for tests.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-import pt2q_loader  # noqa: E402
 
-pt2q = pt2q_loader.load()
-from pt2q import sharding  # noqa: E402
+# Filled by _load_runtime() AFTER the launcher decision (no torch / HIP in a launching parent).
+np = torch = dist = pt2q = sharding = None
 
 MI355X_F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md (dense f32 MFMA)
 MI355X_F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md (dense fp16/bf16 MFMA, no sparsity)
+MI355X_HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md (HBM3E)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py starts "
+                        "them itself; default: WORLD_SIZE or 1")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU plumbing check: gloo ranks, stub units (no GPU, no libpt2q)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--workload", choices=["model", "layer", "split"], default="model",
@@ -74,7 +82,59 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the single-layer / Gram extras (profiling: keeps only the step's launches)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_or_check(a, argv):
+    """Rank plumbing, decided before torch is imported.  Returns None to run in this process, or
+    the exit code of the rank launcher this process started (the caller exits with it).
+
+    * WORLD_SIZE unset and --gpus N > 1: start `python -m torch.distributed.run` with N processes
+      on 127.0.0.1 as a CHILD process (this process has not touched the GPU and never execs).
+    * WORLD_SIZE set (torchrun / the driver's launcher): --gpus, when given, must equal it."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if a.gpus is not None and a.gpus != int(env_world):
+            print(f"[bench] refusing: --gpus {a.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
+            return 2
+        return None
+    if a.gpus is None or a.gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] starting {a.gpus} ranks: {' '.join(cmd[1:5])} ...", file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.call(cmd, env=env)
+
+
+def _load_runtime(dry):
+    """Heavy imports, after the launcher decision.  --dry-run loads sharding.py alone (no
+    libpt2q, no HIP)."""
+    global np, torch, dist, pt2q, sharding
+    import numpy
+    import torch as _torch
+    import torch.distributed as _dist
+    np, torch, dist = numpy, _torch, _dist
+    if dry:
+        import importlib.util
+        path = os.path.join(ROOT, "snlp---tenary-post-train-quantization_amd", "sharding.py")
+        spec = importlib.util.spec_from_file_location("pt2q_sharding_dry", path)
+        sharding = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(sharding)
+        return
+    import pt2q_loader
+    pt2q = pt2q_loader.load()
+    from pt2q import sharding as _sh
+    sharding = _sh
 
 
 def log(rank, msg):
@@ -84,13 +144,29 @@ def log(rank, msg):
 
 def cpu_model_name():
     try:
-        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
-        for line in out.splitlines():
-            if line.lower().startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except Exception:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
         pass
     return "unknown"
+
+
+def host_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota if one is
+    set (a GPU box's share of a large host).  Returns (cores, how it was found)."""
+    aff = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            if quota < aff:
+                return quota, f"cgroup cpu.max quota {quota} of {aff} in the affinity mask"
+    except (OSError, ValueError):
+        pass
+    return aff, f"sched_getaffinity: {aff} CPUs"
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle, "port")
@@ -104,7 +180,7 @@ def cpu_baseline(units, N, block_size, use_ssr, hidden):
     import synth
     from oracle import oracle as orc
     d = hidden
-    cores = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    cores, cores_how = host_cores()
     cols = sharding.units_cols(units)
 
     def scaled(tg, rows, tc, cm, tb, brow):
@@ -137,7 +213,8 @@ def cpu_baseline(units, N, block_size, use_ssr, hidden):
                       f"of {N} rows ({tg:.2f}s), Cholesky inverse ({tc:.2f}s), "
                       f"{-(-d // block_size)}-block loop in full ({tb:.2f}s); the workload's "
                       f"{len(units)} units = these stages scaled by N*m^2, m^3, n*m^2"),
-           "s_per_layer": layer, "s_workload": tot, "cpu_model": cpu_model_name()}
+           "s_per_layer": layer, "s_workload": tot, "cpu_model": cpu_model_name(),
+           "cores_source": cores_how}
     # one core: smaller samples of the same stages
     rows1, cm1, br1 = 128, 2048, 256
     _, tg1 = timed(1, lambda: orc.gram(X[:rows1]))
@@ -260,47 +337,133 @@ class SplitStep:
         return outs
 
 
-def main():
-    a = parse()
+class DryStep:
+    """--dry-run: the model workload's rank plumbing on CPU (gloo) -- the same unit list, LPT
+    shards, sharding.quantize_units_sharded and gather as ModelStep, with a stub run_unit that
+    returns small deterministic outputs instead of launching kernels."""
+
+    def __init__(self, a, rank, world, dev, io):
+        self.units = sharding.llama_units(a.layers, a.hidden, a.inter, a.tokens)
+        self.shards = sharding.assign_lpt([sharding.unit_cost(u) for u in self.units], world)
+        self.mine = self.shards[rank]
+        self.bs = a.block_size
+        self.ran = []
+
+    def provider(self, unit):
+        name, lins, _ = unit
+        return None, {p: (name, p, n, m) for p, n, m in lins}
+
+    def run_unit(self, Ws, X):
+        import zlib
+        from types import SimpleNamespace
+        outs = []
+        for name, p, n, m in Ws:
+            self.ran.append(f"{name}.{p}")
+            g = torch.Generator().manual_seed(zlib.crc32(f"{name}.{p}".encode()))
+            B = -(-m // self.bs)
+            outs.append(SimpleNamespace(alpha=torch.rand((n, B), generator=g), mu=torch.rand((n, B), generator=g),
+                                        T=(torch.randint(0, 3, (n, m), generator=g) - 1).to(torch.int8),
+                                        perm=torch.randperm(m, generator=g)))
+        return outs
+
+    def step(self):
+        res, _ = sharding.quantize_units_sharded(self.units, self.provider, run_unit=self.run_unit,
+                                                 pack=False, dst=0)
+        self.last = res
+        return res
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    rc = launch_or_check(a, argv)
+    if rc is not None:
+        return rc
+    _load_runtime(a.dry_run)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if a.dry_run:
+        if a.workload != "model":
+            raise SystemExit("--dry-run covers the model workload only")
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        if world > torch.cuda.device_count():
+            print(f"[bench] refusing: {world} ranks but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        sync = torch.cuda.synchronize
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        world, rank = dist.get_world_size(), dist.get_rank()
     io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[a.io_dtype]
     N, bs, d = a.tokens, a.block_size, a.hidden
     use_ssr = not a.no_ssr
 
     t_setup = time.perf_counter()
-    work = {"model": ModelStep, "layer": LayerStep, "split": SplitStep}[a.workload](a, rank, world, dev, io)
+    kind = DryStep if a.dry_run else {"model": ModelStep, "layer": LayerStep, "split": SplitStep}[a.workload]
+    work = kind(a, rank, world, dev, io)
     log(rank, f"{a.workload} inputs resident ({time.perf_counter() - t_setup:.1f}s); warmup {a.warmup}")
     for i in range(a.warmup):
         work.step()
-        torch.cuda.synchronize()
+        sync()
         log(rank, f"warmup step {i + 1}/{a.warmup} done")
     if a.workload == "layer" and not work.graph.spd():
         raise RuntimeError("synthetic Hessian not SPD")
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(a.steps):
         work.step()
         if a.steps > 3:
             log(rank, f"step {i + 1}/{a.steps}")
-    torch.cuda.synchronize()
+    sync()
+    t_rank = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ranks = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if a.workload == "model":
+        # per-rank shard and its own compute time (before the closing barrier): load balance
+        mine = getattr(work, "mine", [])
+        me = {"rank": rank, "units": len(mine),
+              "linears": sum(len(work.units[i][1]) for i in mine),
+              "cols": sharding.units_cols([work.units[i] for i in mine]),
+              "ms_per_step": 1e3 * t_rank / max(a.steps, 1)}
+        if a.dry_run:
+            me["ran"] = sorted(set(work.ran))
+        if world > 1:
+            ranks = [None] * world
+            dist.all_gather_object(ranks, me)
+        else:
+            ranks = [me]
     ms_per_step = 1e3 * elapsed / max(a.steps, 1)
     cols = {"model": sharding.units_cols(work.units), "layer": world * a.m, "split": a.m}[a.workload]
     log(rank, f"timed {a.steps} steps: {ms_per_step:.1f} ms/step")
+    if a.dry_run:
+        if rank == 0:
+            got = work.last
+            res = {"metric": "weight-columns quantized/sec (and s/layer) at d=4096 [DRY RUN: CPU stub units]",
+                   "value": cols / (ms_per_step * 1e-3), "unit": "cols/s", "n_gpus": world,
+                   "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms_per_step,
+                   "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "none",
+                   "data": "dry run (no kernels)", "ranks": ranks,
+                   "gathered_linears": sorted(got) if got is not None else None,
+                   "config": {"workload": "dry run", "weight_columns_per_step": cols}}
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
     extra = {}
     roof = None
@@ -406,6 +569,7 @@ def main():
         }
         if a.workload == "model":
             res["s_model"] = ms_per_step / 1e3
+            res["ranks"] = ranks
         if roof is not None:
             res["roofline"] = roof
         res["extra"] = extra
@@ -416,7 +580,8 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

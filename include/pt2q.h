@@ -12,10 +12,10 @@
  *   - `stream` is a hipStream_t passed as void*; every call is stream-ordered and asynchronous
  *     (no host synchronisation, no allocation), so a caller may capture it into a hipGraph.
  *     The Cholesky inverse of an order m > 6144 (pt2q_cholesky_inverse, pt2q_quantize_layer)
- *     forks part of its work onto an internal low-priority stream of the device (created once)
- *     and joins it back with events before the call's last kernel: to the caller it is still
- *     one ordered sequence on `stream`, and under graph capture the side stream joins the
- *     capture.  PT2Q_CHOL_LOOKAHEAD=0 keeps everything on `stream`.
+ *     forks part of its work onto an internal low-priority stream (one per device and caller
+ *     stream, created once) and joins it back with events before the call's last kernel: to the
+ *     caller it is still one ordered sequence on `stream`, and under graph capture the side
+ *     stream joins the capture.  PT2Q_CHOL_LOOKAHEAD=0 keeps everything on `stream`.
  *   - Matrices are row-major with explicit leading dimensions (in elements).
  *   - Return value: PT2Q_OK or an error code; launch-time argument errors only.  Numerical
  *     status discovered on the device (Cholesky breakdown) is written to `info_dev`; a stalled

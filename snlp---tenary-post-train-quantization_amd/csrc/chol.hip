@@ -12,7 +12,9 @@
 // the LDS-DMA f32 GEMM (gemmx.hip).  Their k-ordered chains keep every element bit-identical to
 // the unblocked definition above (oracle/pt2q_oracle.c).
 #include <cstdlib>
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "common.hpp"
 #include "internal.hpp"
@@ -246,21 +248,23 @@ int launch_big(const GemmDesc& g, hipStream_t st) {
 
 }  // namespace
 
-// The side stream of the look-ahead below (one per device, created on first use) and its two
-// events: `fork` (main -> side) and `join` (side -> main).  Under hipGraph capture the event
-// wait pulls the side stream into the capture and the final join brings it back.
+// The side stream of the look-ahead below and its two events, `fork` (main -> side) and `join`
+// (side -> main): one set per (device, caller stream), created on first use, so concurrent
+// callers on different streams (UnitPipeline lanes, host threads) neither serialise their side
+// work behind each other nor share events.  Under hipGraph capture the event wait pulls the side
+// stream into the capture and the final join brings it back.
 struct CholSide {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
-int chol_side(CholSide*& out) {
-  static CholSide sides[64];
+int chol_side(hipStream_t caller, CholSide*& out) {
+  static std::map<std::pair<int, hipStream_t>, CholSide> sides;
   static std::mutex mu;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PT2Q_E_HIP;
+  if (hipGetDevice(&dev) != hipSuccess) return PT2Q_E_HIP;
   std::lock_guard<std::mutex> lock(mu);
-  CholSide& c = sides[dev];
+  CholSide& c = sides[{dev, caller}];  // std::map: references stay valid as entries are added
   if (!c.st) {
     int lo = 0, hi = 0;  // the side stream yields to the critical path: the lowest priority
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
@@ -319,7 +323,7 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   const bool ahead = tu.chol_lookahead && m > 6144;
   const int CP = tp >= NB ? tp / NB * NB : (m > 6144 && !ahead ? 1024 : 512);
   CholSide* side = nullptr;
-  if (ahead && m > CP + CP && (rc = chol_side(side)) != PT2Q_OK) return rc;
+  if (ahead && m > CP + CP && (rc = chol_side(st, side)) != PT2Q_OK) return rc;
   bool factored = false, pending = false;  // pending: side-stream terms not yet joined
   auto join = [&]() -> int {
     if (pending && hipStreamWaitEvent(st, side->join, 0) != hipSuccess) return PT2Q_E_HIP;

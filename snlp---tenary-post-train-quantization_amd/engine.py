@@ -496,6 +496,15 @@ def error_feedback(W: torch.Tensor, blk: torch.Tensor, rem: torch.Tensor, E: tor
     bs, r = blk.numel(), rem.numel()
     if E.shape != (n, bs) or Hinv.shape != (m, m):
         raise ValueError("error_feedback: E must be n x len(blk) and Hinv m x m")
+    # the kernels gather Hinv / W rows with these indices: out-of-range or overlapping sets would
+    # read or write out of bounds where the reference's torch indexing raises (one host read)
+    idx = torch.cat([blk, rem])
+    if idx.numel():
+        lo, hi = (int(v) for v in torch.stack([idx.min(), idx.max()]).cpu())
+        if lo < 0 or hi >= m:
+            raise IndexError(f"error_feedback: column index out of range [0, {m}) (got {lo}..{hi})")
+        if torch.unique(idx).numel() != idx.numel():
+            raise ValueError("error_feedback: blk and rem must be disjoint sets of distinct columns")
     ws = _lib.workspace(_lib.lib().pt2q_error_feedback_workspace_bytes(n, m, max(bs, 1)), W.device)
     _lib.check(_lib.lib().pt2q_error_feedback(_lib.ptr(W), m, n, m, _lib.ptr(blk), bs, _lib.ptr(rem), r,
                                               _lib.ptr(E), bs, _lib.ptr(Hinv), m, _lib.ptr(ws),

@@ -18,11 +18,6 @@ import torch
 import torch.distributed as dist
 
 
-def layer_cost(n: int, m: int, N: int, block_size: int = 128) -> float:
-    """Relative cost of one linear: symmetric Gram N·m² + Cholesky/inverse m³ + block loop n·m²."""
-    return float(N) * m * m + float(m) ** 3 + float(n) * m * m
-
-
 def assign_lpt(costs: Sequence[float], world_size: int) -> List[List[int]]:
     """Longest-processing-time-first assignment of work units to ranks (deterministic)."""
     order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
@@ -50,25 +45,26 @@ def llama_units(num_layers: int, hidden: int = 4096, inter: int = 11008, tokens:
     return units
 
 
-def unit_cost(unit) -> float:
+# Measured single-MI355X rates behind unit_cost (profiles/r02f_summary.md): the
+# 16-bit Gram moves ~1.05e15 N·m² per second; the Cholesky inverse costs m³ at ~1e14/s plus a
+# ~25 µs critical-path step per 64 columns; a block of the block loop costs ~30 µs of launch
+# latency plus n·r·7.5e-12 s (error-feedback MFMA + SSR passes over the r remaining columns).
+_GRAM_RATE, _CHOL_RATE, _CHOL_STEP = 1.05e15, 1.0e14, 25e-6
+_BLOCK_FIXED, _BLOCK_NR = 30e-6, 7.5e-12
+
+
+def unit_cost(unit, block_size: int = 128) -> float:
+    """Modelled seconds of one work unit on one MI355X (its Gram, Cholesky inverse and every
+    linear's block loop).  LPT balances ranks on this; a pure flop count (N·m² dominates) would
+    put a q/k/v unit level with an o unit although its three block loops make it ~1.6x longer."""
     _, linears, N = unit
     m = linears[0][2]
-    return float(N) * m * m + float(m) ** 3 + sum(float(n) * m * m for _, n, _ in linears)
-
-
-def gather_to_root(tensors: Dict[str, torch.Tensor], dst: int = 0, group=None):
-    """Gather same-shaped tensors from every rank to `dst` (one dist.gather per entry).
-    Returns {name: [tensor from rank 0, 1, ...]} on dst, None elsewhere."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    out = {} if rank == dst else None
-    for name in sorted(tensors):
-        t = tensors[name].contiguous()
-        bucket = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
-        dist.gather(t, bucket, dst=dst, group=group)
-        if rank == dst:
-            out[name] = bucket
-    return out
+    t = float(N) * m * m / _GRAM_RATE + float(m) ** 3 / _CHOL_RATE + (m / 64.0) * _CHOL_STEP
+    nblk = -(-m // block_size) if block_size < m else 1
+    rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))  # remaining columns per block
+    for _, n, _ in linears:
+        t += nblk * _BLOCK_FIXED + float(n) * rsum * _BLOCK_NR
+    return t
 
 
 # ----------------------------------------------------------------- heterogeneous result gather
@@ -113,11 +109,13 @@ def _unflatten(manifest, flat: torch.Tensor) -> Dict[str, Dict[str, torch.Tensor
     return out
 
 
-def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, group=None):
+def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, group=None,
+                   device=None):
     """Gather heterogeneous per-rank results ({unit.linear: {key: tensor}}, any shapes/dtypes) to
     `dst`: one small object gather of the shape manifests, then ONE size-exact byte buffer per
     rank point-to-point (send/recv; RCCL over xGMI on GPUs, gloo on CPU).  Returns the merged dict
-    on dst (tensors on dst's device), None elsewhere."""
+    on dst, None elsewhere.  The receive buffers go on `device`, else on the device of dst's own
+    results, else (dst holds none) the current HIP device under RCCL / the CPU under gloo."""
     manifest, flat = _flatten(results)
     if not dist.is_initialized():
         return _unflatten(manifest, flat)
@@ -132,7 +130,14 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
             dist.send(flat, dst=dst, group=group)
         return None
     merged = _unflatten(manifest, flat)
-    dev = flat.device
+    dev = device
+    if dev is None:
+        if manifest:
+            dev = flat.device
+        elif dist.get_backend(group) == "nccl":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        else:
+            dev = torch.device("cpu")
     ops, bufs = [], {}
     for r in range(world):
         if r == dst:
@@ -199,9 +204,11 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
         name, lins, _ = units[i]
         X, Wd = provider(units[i])
         runs.append((name, [p for p, _, _ in lins], run_unit([Wd[p] for p, _, _ in lins], X)))
+    finished = [(name, projs, run.finish() if hasattr(run, "finish") else run) for name, projs, run in runs]
+    if grams_first is not None and hasattr(grams_first, "check"):
+        grams_first.check()  # every Gram's stall bits of the step, one host read
     results = {}
-    for name, projs, run in runs:
-        outs = run.finish() if hasattr(run, "finish") else run
+    for name, projs, outs in finished:
         for p, out in zip(projs, outs):
             r = {"alpha": out.alpha, "mu": out.mu, "perm": out.perm,
                  "shape": torch.tensor(list(out.T.shape), dtype=torch.int64, device=out.T.device)}
@@ -278,12 +285,17 @@ class GramsFirst:
     (Σ m² fp32: 21.7 GB for Llama-2-7B), then the units' tails on the lanes of an
     engine.UnitPipeline.  A Gram holds every CU for its whole duration, so interleaving the Grams
     with other units' tails only stalls those tails; keeping the phases apart measured 2.80 s
-    against 2.95 s per 7B step.  Results are bit-identical to any other order."""
+    against 2.95 s per 7B step.  Results are bit-identical to any other order.
+
+    Stall reporting: the Grams of one width share a workspace, and every pt2q_gram call zeroes
+    its status word first, so after each Gram its word is OR-ed (on the stream) into one
+    per-step device word; check() reads that word once and clears it."""
 
     def __init__(self, pipe, device):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         self.G, self.ws = {}, {}
+        self.stall = torch.zeros(1, dtype=torch.int32, device=self.dev)
 
     def gram(self, key, X):
         X2 = X.reshape(-1, X.shape[-1])
@@ -293,23 +305,13 @@ class GramsFirst:
         if m not in self.ws:
             self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
         self.engine.gram(X2, G=self.G[key], workspace=self.ws[m], check=False)
+        torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
 
     def tail(self, key, Ws, nsamples):
-        return _CheckedRun(self.pipe.run(Ws, G=self.G[key], nsamples=nsamples), self)
+        return self.pipe.run(Ws, G=self.G[key], nsamples=nsamples)
 
     def check(self):
-        """Raise if a Gram's stream-K hand-off stalled (reads the status words: one sync)."""
-        for w in self.ws.values():
-            self.lib.check_status(w, "pt2q_gram")
-
-
-class _CheckedRun:
-    """A UnitRun whose finish() also checks the Gram status words of the GramsFirst step."""
-
-    def __init__(self, run, gf):
-        self.run, self.gf = run, gf
-
-    def finish(self):
-        outs = self.run.finish()
-        self.gf.check()
-        return outs
+        """Raise if any Gram since the last check stalled in a stream-K hand-off (one host read)."""
+        status = int(self.stall.item())
+        self.stall.zero_()
+        self.lib.raise_stall(status, "pt2q_gram")

@@ -45,45 +45,39 @@ def test_lpt_assignment_balances_llama_units():
     assert [p for p, _, _ in units[0][1]] == ["q_proj", "k_proj", "v_proj"]
 
 
-def _worker(rank, world, port, q):
+def _worker_empty_dst(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sh = _sharding()
-    n, m, B = 16, 40, 2
-    gen = torch.Generator().manual_seed(rank)
-    T = (torch.randint(0, 3, (n, m), generator=gen) - 1).to(torch.int8)
-    flat = (T.flatten() + 1).to(torch.uint8)
-    pad = (-flat.numel()) % 4
-    flat = torch.cat([flat, torch.zeros(pad, dtype=torch.uint8)]).reshape(-1, 4)
-    packed = flat[:, 0] | (flat[:, 1] << 2) | (flat[:, 2] << 4) | (flat[:, 3] << 6)
-    res = {"T2": packed, "alpha": torch.full((n, B), float(rank)), "mu": torch.zeros(n, B),
-           "perm": torch.randperm(m, generator=gen)}
-    out = sh.gather_to_root(res, dst=0)
+    res = {}
+    if rank == 1:  # only the sender holds results: dst must still size its receive buffers
+        gen = torch.Generator().manual_seed(5)
+        res = {"u.p": {"alpha": torch.rand((16, 2), generator=gen), "perm": torch.randperm(40, generator=gen)}}
+    out = sh.gather_results(res, dst=0)
     if rank == 0:
-        q.put({k: [t.clone() for t in v] for k, v in out.items()})
+        q.put({k: {f: t.numpy().copy() for f, t in v.items()} for k, v in out.items()})
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_gather_to_root_world2():
+def test_gather_results_dst_without_results_world2():
+    """dst holding no results of its own receives into buffers on a valid device
+    (gloo: CPU) instead of on the device of an empty flat tensor."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_empty_dst, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=90)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert len(got["alpha"]) == world
-    for r in range(world):
-        assert torch.all(got["alpha"][r] == float(r))
-        gen = torch.Generator().manual_seed(r)
-        torch.randint(0, 3, (16, 40), generator=gen)
-        assert torch.equal(got["perm"][r], torch.randperm(40, generator=gen))
+    gen = torch.Generator().manual_seed(5)
+    assert torch.equal(torch.from_numpy(got["u.p"]["alpha"]), torch.rand((16, 2), generator=gen))
+    assert torch.equal(torch.from_numpy(got["u.p"]["perm"]), torch.randperm(40, generator=gen))
 
 
 class _FakeOut:
@@ -291,3 +285,73 @@ def test_grams_first_orders_phases_single_process():
     for k in got:
         for f in got[k]:
             assert torch.equal(got[k][f], want[k][f])
+
+
+# ----------------------------------------------------------------- bench.py rank plumbing
+
+def _last_json(text):
+    import json
+    for line in reversed(text.strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError("no JSON line in bench output:\n" + text[-2000:])
+
+
+@pytest.mark.timeout(180)
+def test_bench_gpus2_launches_two_ranks_dry_run():
+    """`python bench.py --gpus 2` (no WORLD_SIZE) starts two ranks itself; each runs exactly its
+    LPT shard of the model's units, rank 0 gathers every linear and prints ONE JSON line with
+    n_gpus from the process group (--dry-run: gloo, stub units)."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = ["--layers", "2", "--hidden", "64", "--inter", "96", "--tokens", "256", "--steps", "2",
+            "--warmup", "1", "--dry-run"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + args,
+                       capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert sum(1 for l in p.stdout.splitlines() if l.startswith("{")) == 1
+    d = _last_json(p.stdout)
+    sh = _sharding()
+    units = sh.llama_units(2, 64, 96, 256)
+    shards = sh.assign_lpt([sh.unit_cost(u) for u in units], 2)
+    assert d["n_gpus"] == 2 and len(d["ranks"]) == 2
+    for r in d["ranks"]:
+        want = sorted(f"{units[i][0]}.{p}" for i in shards[r["rank"]] for p, _, _ in units[i][1])
+        assert r["ran"] == want and r["units"] == len(shards[r["rank"]])
+    assert d["gathered_linears"] == sorted(f"{n}.{p}" for n, lins, _ in units for p, _, _ in lins)
+    assert d["config"]["weight_columns_per_step"] == sh.units_cols(units)
+
+
+def test_bench_refuses_gpus_world_size_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--dry-run"],
+                       capture_output=True, text=True, timeout=60, env=env, cwd=ROOT)
+    assert p.returncode == 2 and "refusing" in p.stderr
+
+
+# ----------------------------------------------------------------- GramsFirst stall reporting
+
+def test_grams_first_keeps_an_early_stall():
+    """Grams of one width share a workspace whose status word every pt2q_gram zeroes
+    first; a stall in an EARLY Gram must survive the later Grams and raise once at check()."""
+    import types
+
+    import pt2q_loader
+    pt2q = pt2q_loader.load()  # ctypes load of libpt2q.so works without a GPU
+    from pt2q import sharding as sh
+    gf = sh.GramsFirst(pipe=None, device="cpu")
+    stalls = iter([1, 0, 0])  # the first Gram of the width stalls, the next two do not
+
+    def fake_gram(X, G=None, workspace=None, check=False):
+        pt2q._lib.status_view(workspace).fill_(next(stalls))  # take_status zeroes, kernel may set
+        return G
+
+    gf.engine = types.SimpleNamespace(gram=fake_gram)
+    for k in range(3):
+        gf.gram(k, torch.zeros(8, 16))
+    with pytest.raises(pt2q._lib.Pt2qError, match="Gram partial-tile"):
+        gf.check()
+    gf.check()  # cleared after the read
