@@ -79,6 +79,9 @@ def parse(argv=None):
     p.add_argument("--no-overlap", action="store_true",
                    help="model workload: run the units strictly one after another on one stream "
                         "(default: engine.UnitPipeline overlaps unit i+1's Gram with unit i's tail)")
+    p.add_argument("--no-batched-inverse", action="store_true",
+                   help="model workload, grams-first: each unit's Cholesky inverse on its lane instead of "
+                        "batched per width (engine.hessian_inverse_batched)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the single-layer / Gram extras (profiling: keeps only the step's launches)")
@@ -266,7 +269,8 @@ class ModelStep:
         self.bs, self.ssr = a.block_size, not a.no_ssr
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.schedule = a.schedule
-        self.gf = sharding.GramsFirst(self.pipe, dev) if self.pipe is not None else None
+        self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse)
+                   if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.index = {u[0]: i for i, u in enumerate(self.units)}
         for i in self.mine:

@@ -104,6 +104,20 @@ int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples, f
 int pt2q_cholesky_inverse(const float* H, int64_t ldh, int m, float* Hinv, int64_t ldhi,
                           void* workspace, size_t workspace_bytes, int* info_dev, void* stream);
 
+/* A batch of units' inverse Hessians in one launch sequence (main.py:129-139 for each unit of a
+ * model step whose raw Grams are all at hand): for z < batch, H_z = G_z / nsamples + damping
+ * (as pt2q_prepare_hessian), Hinv_z = cholesky_inverse(cholesky(H_z)).  G, H, Hinv are packed
+ * batch x m x m fp32 (item z at + z*m*m); H is scratch and holds the factors U_z on return.  Every
+ * step of the blocked factorisation serves all items in one launch (grid.y = item), so the
+ * latency-bound diagonal and panel steps of small m fill the chip; each item's result is
+ * bit-identical to pt2q_prepare_hessian + pt2q_cholesky_inverse on it alone.  info_dev: batch
+ * ints (0, or k+1 at the first non-positive pivot; then that item falls back to pinv on the host,
+ * main.py:140-141).  workspace: pt2q_hessian_inverse_batched_workspace_bytes(m, batch). */
+size_t pt2q_hessian_inverse_batched_workspace_bytes(int m, int batch);
+int pt2q_hessian_inverse_batched(const float* G, int m, int batch, int64_t nsamples, float percdamp,
+                                 float* H, float* Hinv, void* workspace, size_t workspace_bytes,
+                                 int* info_dev, void* stream);
+
 /* The block loop of main.py:158-230 (flags & PT2Q_AGA_ACT) or gptq.py:124-199 (PT2Q_AGA_HESS).
  *   W      n x m weights (row-major, wdtype), read only.
  *   A      AGA matrix: raw Gram XᵀX (ACT) or damped H (HESS); m x m; may be NULL for NONE.

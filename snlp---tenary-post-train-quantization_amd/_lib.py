@@ -50,6 +50,8 @@ _SIGS = {
     "pt2q_gram": (I, [P, I, I64, I, I64, P, I64, I, P, SZ, P]),
     "pt2q_prepare_hessian": (I, [P, I64, I, I64, F, P, I64, P, P]),
     "pt2q_cholesky_inverse": (I, [P, I64, I, P, I64, P, SZ, P, P]),
+    "pt2q_hessian_inverse_batched_workspace_bytes": (SZ, [I, I]),
+    "pt2q_hessian_inverse_batched": (I, [P, I, I, I64, F, P, P, P, SZ, P, P]),
     "pt2q_quantize_blocks": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, I, P, P, P, I, P, P, P,
                                  SZ, P]),
     "pt2q_quantize_layer": (I, [P, I, I64, I, I, P, I, I64, I64, I, I, F, I, P, P, P, I, P, P, P,

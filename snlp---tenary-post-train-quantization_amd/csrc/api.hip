@@ -355,6 +355,34 @@ extern "C" int pt2q_cholesky_inverse(const float* H, int64_t ldh, int m, float* 
   return pt2q_launch_cholesky_inverse(H, ldh, m, Hinv, ldhi, U, Ui, info_dev, (hipStream_t)stream);
 }
 
+// ---- a batch of units' damped Hessian inverses (main.py:129-139 per unit, one launch sequence)
+extern "C" size_t pt2q_hessian_inverse_batched_workspace_bytes(int m, int batch) {
+  if (m <= 0 || batch <= 0) return 0;
+  return (((size_t)m * m * batch * 4 + 255) & ~(size_t)255) + (((size_t)batch * 4 + 255) & ~(size_t)255);
+}
+
+extern "C" int pt2q_hessian_inverse_batched(const float* G, int m, int batch, int64_t nsamples,
+                                            float percdamp, float* H, float* Hinv, void* workspace,
+                                            size_t workspace_bytes, int* info_dev, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!G || !H || !Hinv || !info_dev || m <= 0 || batch <= 0 || nsamples <= 0 || G == H || H == Hinv)
+    return PT2Q_E_ARG;
+  Carve c{(char*)workspace, workspace_bytes};
+  float* Ui = c.take<float>((size_t)m * m * batch);
+  float* damp = c.take<float>((size_t)batch);
+  if (!c.ok) return PT2Q_E_WORKSPACE;
+  const long mm = (long)m * m;
+  // H written as the Cholesky work matrix at once (strictly lower part zero) where the damping
+  // pass can (m <= SUMN_LDS_MAX); else in full form, then made upper in place by the factor
+  const bool upper = m <= SUMN_LDS_MAX;
+  int rc;
+  for (int z = 0; z < batch; ++z)
+    if ((rc = pt2q_launch_prepare_hessian(G + z * mm, m, m, nsamples, percdamp, H + z * mm, m, damp + z, st,
+                                          upper)) != PT2Q_OK)
+      return rc;
+  return pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st, upper, batch);
+}
+
 extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int n, int m, int b,
                                     int flags, const float* A, int64_t lda, const float* Hinv,
                                     int64_t ldhi, int max_iter, float* alpha, float* mu, void* T,

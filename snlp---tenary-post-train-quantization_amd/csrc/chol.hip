@@ -27,8 +27,10 @@ using pt2q_chol::NB;
 // Diagonal-block factor (chol_diag.hpp) as a kernel of its own: the first block, and any block
 // whose producing update did not run the fused factor.
 __global__ __launch_bounds__(256) void chol_diag_kernel(float* A, long lda, int p0, int nb,
-                                                        int* info) {
+                                                        int* info, long bst) {
   __shared__ __attribute__((aligned(16))) float urow[3][pt2q_chol::DG][NB];
+  A += (long)blockIdx.y * bst;  // batch item (grid.y)
+  info += blockIdx.y;
   const float* D = A + (long)p0 * lda + p0;
   pt2q_chol::diag_factor([&](int r, int c) { return D[(long)r * lda + c]; }, A, lda, p0, nb, info, urow);
 }
@@ -180,9 +182,11 @@ PT2Q_DEV void trtri_inblock(float* Ui, long ldi, int c0, int nb, int bid, float 
 // right of it), the rest run the in-block triangular inverse of block J (which needs only the
 // factored diagonal block and the inverse chains of earlier blocks) -- one launch.
 __global__ __launch_bounds__(256) void chol_panel_trtri_kernel(float* U, long ld, int p0, int nb,
-                                                               int m, float* Ui, int npanel) {
+                                                               int m, float* Ui, int npanel, long bst) {
   __shared__ __attribute__((aligned(16))) float Dus[NB][NB + 4];
   __shared__ float dg[NB];
+  U += (long)blockIdx.y * bst;  // batch item (grid.y)
+  Ui += (long)blockIdx.y * bst;
   const bool panel = (int)blockIdx.x < npanel;
   float x[SEG];  // this thread's chains, loaded together with the diagonal block
   if (panel)
@@ -197,7 +201,9 @@ __global__ __launch_bounds__(256) void chol_panel_trtri_kernel(float* U, long ld
     trtri_inblock(Ui, ld, p0, nb, blockIdx.x - npanel, Dus, dg, x);
 }
 
-__global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m) {
+__global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m, long bst) {
+  H += (long)blockIdx.y * bst;  // batch item (grid.y)
+  A += (long)blockIdx.y * bst;
   long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (long)m * m) return;
   int r = (int)(q / m), c = (int)(q % m);
@@ -212,8 +218,9 @@ namespace {
 // (one or two blocks; chains continue from U, k ascending).  upper: the square trailing
 // triangle; otherwise the full rectangle (the strictly-lower part of U is scratch).
 GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int c0, int cols,
-                       bool upper = true) {
+                       bool upper = true, int batch = 1) {
   GemmDesc g{};
+  g.batch = batch; g.bstride = ld * ld;
   g.M = rows; g.N = cols; g.K = nb;
   g.A = U + (long)p0 * ld + r0; g.lda = ld; g.a_layout = LAY_KMAJOR;
   g.B = U + (long)p0 * ld + c0; g.ldb = ld; g.b_layout = LAY_KMAJOR;
@@ -225,8 +232,10 @@ GemmDesc trailing_desc(float* U, long ld, int p0, int nb, int r0, int rows, int 
 
 // Inverse chains of columns [c1, c1 + cols) (rows of UiT), over rows k < nk of Uinv, get the terms
 // j in [j0, j0 + K) (ascending):  UiT[c][k] += sum_j U[j][c] * UiT[j][k].
-GemmDesc trtri_desc(const float* U, float* UiT, long ld, int j0, int K, int c1, int cols, int nk) {
+GemmDesc trtri_desc(const float* U, float* UiT, long ld, int j0, int K, int c1, int cols, int nk,
+                    int batch = 1) {
   GemmDesc g{};
+  g.batch = batch; g.bstride = ld * ld;
   g.M = cols; g.N = nk; g.K = K;
   g.A = U + (long)j0 * ld + c1; g.lda = ld; g.a_layout = LAY_KMAJOR;   // (c, j) = U[j0+j][c1+c]
   g.B = UiT + (long)j0 * ld; g.ldb = ld; g.b_layout = LAY_KMAJOR;      // (j, k) = UiT[j0+j][k]
@@ -287,27 +296,30 @@ int chol_side(hipStream_t caller, CholSide*& out) {
 // inverse (kept transposed, UiT) is built right-looking by column blocks as soon as rows of
 // block J are final.
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
-                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form) {
+                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form,
+                                 int batch) {
   const long ld = m;  // U and Ui are packed m x m
-  if (hipMemsetAsync(info, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
-  if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m, st) != hipSuccess) return PT2Q_E_HIP;
+  const long bst = ld * ld;  // batch item stride of every matrix (batch > 1: all packed)
+  if (batch < 1 || (batch > 1 && (ldh != ld || ldhi != ld))) return PT2Q_E_ARG;
+  if (hipMemsetAsync(info, 0, sizeof(int) * batch, st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(Ui, 0, sizeof(float) * (size_t)m * m * batch, st) != hipSuccess) return PT2Q_E_HIP;
   if (!(h_upper_form && H == U && ldh == ld)) {  // (else H already is the upper work matrix)
-    hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, H, ldh,
-                       U, ld, m);
+    hipLaunchKernelGGL(copy_upper_kernel, dim3(ceil_div((long)m * m, 256), batch), dim3(256), 0, st, H, ldh,
+                       U, ld, m, bst);
     PT2Q_LAUNCH_CHECK();
   }
   int rc;
   // panel solve + in-block inverse of the block at p0 (its diagonal factor done: `factored`)
   auto factor = [&](int p0, int nb, bool factored) -> int {
     if (!factored) {
-      hipLaunchKernelGGL(chol_diag_kernel, dim3(1), dim3(256), 0, st, U, ld, p0, nb, info);
+      hipLaunchKernelGGL(chol_diag_kernel, dim3(1, batch), dim3(256), 0, st, U, ld, p0, nb, info, bst);
       PT2Q_LAUNCH_CHECK();
     }
     const int rest = m - p0 - nb;
     const int npanel = rest > 0 ? (int)ceil_div((long)rest * LPR, 256) : 0;
     const int ninv = (int)ceil_div((long)(p0 + nb) * LPR, 256);
-    hipLaunchKernelGGL(chol_panel_trtri_kernel, dim3(npanel + ninv), dim3(256), 0, st, U, ld, p0, nb,
-                       m, Ui, npanel);
+    hipLaunchKernelGGL(chol_panel_trtri_kernel, dim3(npanel + ninv, batch), dim3(256), 0, st, U, ld, p0, nb,
+                       m, Ui, npanel, bst);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };
@@ -320,7 +332,8 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   const int tp = tu.chol_panel;
   // look-ahead from m > 6144 (measured: 4096 3.07 -> 3.24 ms with it, 11008 19.7 -> 18.6 ms with
   // it and 512-row panels); panel rows (a multiple of NB): 512, or 1024 for a large m alone
-  const bool ahead = tu.chol_lookahead && m > 6144;
+  // (a batch fills the chip by itself: no look-ahead)
+  const bool ahead = tu.chol_lookahead && m > 6144 && batch == 1;
   const int CP = tp >= NB ? tp / NB * NB : (m > 6144 && !ahead ? 1024 : 512);
   CholSide* side = nullptr;
   if (ahead && m > CP + CP && (rc = chol_side(st, side)) != PT2Q_OK) return rc;
@@ -340,8 +353,8 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
       if (p1 >= Pend) break;
       const int nb1 = (Pend - p1 < NB) ? Pend - p1 : NB;
       // U rows [p1, Pend) x columns [p1, m) and inverse columns [p1, Pend) x rows [0, p1)
-      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, Pend - p1, p1, m - p1, false),
-                                  trtri_desc(U, Ui, ld, p0, nb, p1, Pend - p1, p1), st, U, ld, p1,
+      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, Pend - p1, p1, m - p1, false, batch),
+                                  trtri_desc(U, Ui, ld, p0, nb, p1, Pend - p1, p1, batch), st, U, ld, p1,
                                   nb1, info, &factored)) != PT2Q_OK)
         return rc;
     }
@@ -351,10 +364,10 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     if ((rc = join()) != PT2Q_OK) return rc;
     // the next panel's rows [Pend, Pend2) -- or all remaining rows without a side stream
     const int Pend2 = side ? std::min(m, Pend + CP) : m;
-    if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend, Pend2 - Pend, Pend, rest, Pend2 < m ? false : true),
-                         st)) != PT2Q_OK)
+    if ((rc = launch_big(trailing_desc(U, ld, P0, K, Pend, Pend2 - Pend, Pend, rest, Pend2 < m ? false : true,
+                                       batch), st)) != PT2Q_OK)
       return rc;
-    if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend, Pend2 - Pend, Pend), st)) != PT2Q_OK) return rc;
+    if ((rc = launch_big(trtri_desc(U, Ui, ld, P0, K, Pend, Pend2 - Pend, Pend, batch), st)) != PT2Q_OK) return rc;
     if (Pend2 < m) {  // every row beyond, on the side stream
       if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->st, side->fork, 0) != hipSuccess)
         return PT2Q_E_HIP;
@@ -375,5 +388,6 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   g.in_dtype = PT2Q_F32;
   g.C = Hinv; g.ldc = ldhi;
   g.mode = GEMM_STORE; g.upper = 1; g.mirror = 1; g.kstart_diag = 2;
+  g.batch = batch; g.bstride = bst;
   return launch_big(g, st);
 }

@@ -950,6 +950,10 @@ struct RuDiag {
 
 PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4], float (*Bs)[RU_T + 4],
                       const RuDiag& diag = RuDiag{nullptr, 0, 0, 0, nullptr}) {
+  const long zo = (long)blockIdx.y * g.bstride;  // batch item (grid.y)
+  const float* const Az = (const float*)g.A + zo;
+  const float* const Bz = (const float*)g.B + zo;
+  float* const Cz = g.C + zo;
   int ti, tj;
   if (g.upper) {
     upper_tile(bid, tn, ti, tj);
@@ -960,7 +964,7 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
   const int i0 = ti * RU_T, j0 = tj * RU_T;
   Frag<RU_T, RU_T, true> F;
   // C tile (16-byte groups of 4 columns: launch checks ldc % 4 == 0, N % 4 == 0, alignment)
-  const float* Cr = g.C;
+  const float* Cr = Cz;
   {
     const int row = F.row_of(i0, 0, 0);
 #pragma unroll
@@ -974,11 +978,11 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
   }
   const bool k128 = g.K > 64, neg = g.mode == GEMM_CHAIN_NEG;
   if (k128) {
-    ru_panel<128>((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
-    ru_panel<128>((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+    ru_panel<128>(Az, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
+    ru_panel<128>(Bz, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
   } else {
-    ru_panel<64>((const float*)g.A, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
-    ru_panel<64>((const float*)g.B, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
+    ru_panel<64>(Az, g.lda, g.a_layout, i0, g.M, g.K, As, neg);
+    ru_panel<64>(Bz, g.ldb, g.b_layout, j0, g.N, g.K, Bs);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1002,8 +1006,8 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
       for (int e = 0; e < 4; ++e) D[row - i0][col + e] = F.acc[0][0][4 * q + e];
     }
     __syncthreads();
-    pt2q_chol::diag_factor([&](int r, int c) { return D[r][c]; }, diag.A, diag.lda, diag.p0, diag.nb,
-                           diag.info, (float (*)[pt2q_chol::DG][pt2q_chol::NB])&Bs[0][0]);
+    pt2q_chol::diag_factor([&](int r, int c) { return D[r][c]; }, diag.A + zo, diag.lda, diag.p0, diag.nb,
+                           diag.info + blockIdx.y, (float (*)[pt2q_chol::DG][pt2q_chol::NB])&Bs[0][0]);
     return;
   }
   if (row < g.M) {
@@ -1014,7 +1018,7 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
       f32x4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = F.acc[0][0][4 * q + e];
-      *(f32x4*)(g.C + (long)row * g.ldc + col) = v;
+      *(f32x4*)(Cz + (long)row * g.ldc + col) = v;
     }
   }
 }
@@ -1068,6 +1072,8 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
                       int dp0, int dnb, int* info, bool* fused) {
   if (fused) *fused = false;
   if (g0.in_dtype != PT2Q_F32 || g1.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
+  const int nb = g0.batch > 1 ? g0.batch : 1;
+  if (nb != (g1.batch > 1 ? g1.batch : 1) || (nb > 1 && g0.bstride != g1.bstride)) return PT2Q_E_ARG;
   if (ru_ok(g0) && ru_ok(g1) && pt2q_tuning().rank_update) {
     int tm0, tn0, tm1, tn1;
     const long n0 = tiles_of<RU_T, RU_T>(g0, tm0, tn0), n1 = tiles_of<RU_T, RU_T>(g1, tm1, tn1);
@@ -1076,10 +1082,21 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
     const bool fuse = dA && n0 > 0 && g0.C == dA + (long)dp0 * dld + dp0 && g0.ldc == dld &&
                       dnb > 0 && dnb <= RU_T && g0.M >= dnb && g0.N >= dnb;
     RuDiag d{fuse ? dA : nullptr, dld, dp0, dnb, info};
-    hipLaunchKernelGGL(rank_update2_kernel, dim3((unsigned)(n0 + n1)), dim3(256), 0, st, g0, tn0,
-                       (int)n0, g1, tn1, d);
+    hipLaunchKernelGGL(rank_update2_kernel, dim3((unsigned)(n0 + n1), (unsigned)nb), dim3(256), 0, st, g0,
+                       tn0, (int)n0, g1, tn1, d);
     PT2Q_LAUNCH_CHECK();
     if (fused) *fused = fuse;
+    return PT2Q_OK;
+  }
+  if (nb > 1) {  // the generic kernels run one item per launch
+    for (int z = 0; z < nb; ++z) {
+      GemmDesc h0 = g0, h1 = g1;
+      const long o = (long)z * g0.bstride;
+      h0.A = (const float*)g0.A + o; h0.B = (const float*)g0.B + o; h0.C = g0.C + o; h0.batch = 1;
+      h1.A = (const float*)g1.A + o; h1.B = (const float*)g1.B + o; h1.C = g1.C + o; h1.batch = 1;
+      const int rc = pt2q_launch_gemm2(h0, h1, st);
+      if (rc != PT2Q_OK) return rc;
+    }
     return PT2Q_OK;
   }
   int a, b;
@@ -1094,6 +1111,17 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PT2Q_OK;
   if (g.K < 0 || !g.A || !g.B || !g.C) return PT2Q_E_ARG;
+  if (g.batch > 1) {  // one item per launch
+    if (g.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
+    for (int z = 0; z < g.batch; ++z) {
+      GemmDesc h = g;
+      const long o = (long)z * g.bstride;
+      h.A = (const float*)g.A + o; h.B = (const float*)g.B + o; h.C = g.C + o; h.batch = 1;
+      const int rc = pt2q_launch_gemm(h, st);
+      if (rc != PT2Q_OK) return rc;
+    }
+    return PT2Q_OK;
+  }
   switch (g.in_dtype) {
     case PT2Q_F32:
       return launch_dt<float>(g, st);

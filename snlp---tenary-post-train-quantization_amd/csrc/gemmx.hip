@@ -172,8 +172,10 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
   const int kbeg = g.kstart_diag == 2 ? j0 : (g.kstart_diag == 1 ? i0 : 0);
   const int kend = g.K;
   const int nst = kend > kbeg ? (kend - kbeg + XK - 1) / XK : 0;
-  const float* Ab = (const float*)g.A;
-  const float* Bb = (const float*)g.B;
+  const long zo = (long)blockIdx.y * g.bstride;  // batch item (grid.y)
+  const float* Ab = (const float*)g.A + zo;
+  const float* Bb = (const float*)g.B + zo;
+  float* const Cz = g.C + zo;
   // the C tile (chain modes) is loaded first, so that waiting for it does not wait for the DMA
   // prologue issued after it; accumulators: lane <-> C row, register groups of 4 <-> 4
   // consecutive C columns
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
       for (int q = 0; q < 4; ++q) {
         const int col = j0 + wc * 64 + rn * 32 + 8 * q + 4 * lk;
         const bool in = chain && row < g.M && col < g.N;
-        cv[rm][rn][q] = *(const f32x4*)(g.C + (in ? (long)row * g.ldc + col : 0));
+        cv[rm][rn][q] = *(const f32x4*)(Cz + (in ? (long)row * g.ldc + col : 0));
       }
     }
   asm volatile("" ::: "memory");
@@ -258,10 +260,10 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = csg * acc[rm][rn][4 * q + e];
-        *(f32x4*)(g.C + (long)row * g.ldc + col) = v;
+        *(f32x4*)(Cz + (long)row * g.ldc + col) = v;
         if (mirror) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) g.C[(long)(col + e) * g.ldc + row] = v[e];
+          for (int e = 0; e < 4; ++e) Cz[(long)(col + e) * g.ldc + row] = v[e];
         }
       }
     }
@@ -288,10 +290,11 @@ int pt2q_launch_gemmx(const GemmDesc& g, hipStream_t st) {
   } else {
     tiles = (long)X.tiles_m * X.tiles_n;
   }
+  const dim3 grid((unsigned)tiles, (unsigned)(g.batch > 1 ? g.batch : 1));
   if (pt2q_tuning().gemmx_stages == 2)  // 64 KiB of LDS: two workgroups per CU
-    hipLaunchKernelGGL(gemmx_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, st, X);
+    hipLaunchKernelGGL(gemmx_kernel<2>, grid, dim3(256), 0, st, X);
   else
-    hipLaunchKernelGGL(gemmx_kernel<3>, dim3((unsigned)tiles), dim3(256), 0, st, X);
+    hipLaunchKernelGGL(gemmx_kernel<3>, grid, dim3(256), 0, st, X);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

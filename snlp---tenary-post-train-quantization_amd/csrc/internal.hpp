@@ -51,6 +51,8 @@ struct GemmDesc {
   int upper;        // compute only tiles with tile_i <= tile_j
   int mirror;       // with upper: also write C[j][i] (full symmetric output)
   int kstart_diag;  // skip K below min(tile row start): exact for triangular operands (zeros)
+  int batch;        // > 1: that many independent GEMMs, item z at A/B/C + z * bstride elements
+  long bstride;     //      (gemmx and the rank-<=128 update run them in one launch, grid.y = z)
 };
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
 // block error feedback Wt[crow[e]][i] -= sum_k Ck[k][e] Et[k][i] (ef.hip); E_UNSUPPORTED if bs > 128
@@ -84,5 +86,7 @@ int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, 
                                 float* H, long ldh, float* damp, hipStream_t st, bool upper_only = false);
 
 // ---- Cholesky (chol.hip)
+// batch > 1: that many independent inverses, all packed (ld = m, item z at + z * m * m, info + z)
 int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, long ldhi,
-                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form = false);
+                                 float* U, float* Ui, int* info, hipStream_t st, bool h_upper_form = false,
+                                 int batch = 1);

@@ -145,6 +145,40 @@ def hessian_inverse(G: torch.Tensor, nsamples: int, percdamp: float = 0.01):
     return Hinv, spd
 
 
+def hessian_inverse_batched(G: torch.Tensor, nsamples: int, percdamp: float = 0.01,
+                            Hinv: Optional[torch.Tensor] = None, info: Optional[torch.Tensor] = None,
+                            scratch: Optional[dict] = None, chunk: int = 32):
+    """main.py:129-139 for a batch of units of one width whose raw Grams are packed in G
+    (batch, m, m), all over `nsamples` rows: damping and Cholesky inverse of every item, `chunk`
+    items per pt2q_hessian_inverse_batched launch sequence (each step of the blocked
+    factorisation serves all items of a chunk in one launch).  Stream-ordered, no host read:
+    returns (Hinv (batch, m, m), info (batch,) int32 on the device -- non-zero items need the
+    pinv fallback, see UnitRun.finish).  Item z is bit-identical to hessian_inverse(G[z]).
+    scratch: a dict reused across calls for the per-chunk H and workspace buffers."""
+    _lib.require_device(G)
+    if G.dim() != 3 or G.shape[1] != G.shape[2] or G.dtype != torch.float32 or not G.is_contiguous():
+        raise _lib.Pt2qError("hessian_inverse_batched: G must be a contiguous fp32 (batch, m, m) device tensor")
+    batch, m, dev = G.shape[0], G.shape[1], G.device
+    if Hinv is None:
+        Hinv = torch.empty_like(G)
+    if info is None:
+        info = torch.empty(batch, dtype=torch.int32, device=dev)
+    c = max(1, min(chunk, batch))
+    sc = scratch if scratch is not None else {}
+    key = (m, c)
+    if key not in sc:
+        sc[key] = (torch.empty((c, m, m), dtype=torch.float32, device=dev),
+                   _lib.workspace(_lib.lib().pt2q_hessian_inverse_batched_workspace_bytes(m, c), dev))
+    H, ws = sc[key]
+    L, st = _lib.lib(), _lib.stream_of(dev)
+    for z0 in range(0, batch, c):
+        k = min(c, batch - z0)
+        _lib.check(L.pt2q_hessian_inverse_batched(_lib.ptr(G[z0]), m, k, int(nsamples), float(percdamp),
+                                                  _lib.ptr(H), _lib.ptr(Hinv[z0]), _lib.ptr(ws), ws.numel(),
+                                                  _lib.ptr(info[z0:]), st), "pt2q_hessian_inverse_batched")
+    return Hinv, info
+
+
 def quantize_shared(Ws, G: torch.Tensor, nsamples: int, block_size: int = 128,
                     use_ssr: bool = True, percdamp: float = 0.01, max_iter: int = 100,
                     t_dtype=torch.int8):
@@ -242,18 +276,25 @@ def quantize_unit(Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor
     return run if defer else run.finish()
 
 
-def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percdamp, max_iter, t_dtype):
+def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percdamp, max_iter, t_dtype,
+               Hinv=None, info=None):
     """Damping, Cholesky inverse and every weight's block loop of a unit whose raw Gram is Gm,
-    on the current stream; returns the deferred UnitRun.  The pinv redo rebuilds the Gram from
-    the caller's X (or G): Gm may be a reused buffer by the time the status is read."""
+    on the current stream; returns the deferred UnitRun.  With Hinv (and its device info word)
+    given -- an item of hessian_inverse_batched -- only the block loops run.  The pinv redo
+    rebuilds the Gram from the caller's X (or G): Gm may be a reused buffer by the time the
+    status is read."""
     m, dev = Ws[0].shape[1], Ws[0].device
     L = _lib.lib()
     st = _lib.stream_of(dev)
-    _lib.check(L.pt2q_prepare_hessian(_lib.ptr(Gm), m, m, int(nsamples), float(percdamp),
-                                      _lib.ptr(ws.H), m, _lib.ptr(ws.damp), st), "pt2q_prepare_hessian")
-    info = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.check(L.pt2q_cholesky_inverse(_lib.ptr(ws.H), m, m, _lib.ptr(ws.Hinv), m, _lib.ptr(ws.chol_ws),
-                                       ws.chol_ws.numel(), _lib.ptr(info), st), "pt2q_cholesky_inverse")
+    if Hinv is None:
+        _lib.check(L.pt2q_prepare_hessian(_lib.ptr(Gm), m, m, int(nsamples), float(percdamp),
+                                          _lib.ptr(ws.H), m, _lib.ptr(ws.damp), st), "pt2q_prepare_hessian")
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L.pt2q_cholesky_inverse(_lib.ptr(ws.H), m, m, _lib.ptr(ws.Hinv), m, _lib.ptr(ws.chol_ws),
+                                           ws.chol_ws.numel(), _lib.ptr(info), st), "pt2q_cholesky_inverse")
+        Hinv = ws.Hinv
+    elif info is None:
+        raise ValueError("_unit_tail: a given Hinv needs its info word")
     flags = (_lib.FLAG_SSR if use_ssr else 0) | _lib.AGA_ACT
     outs = []
     for W in Ws:
@@ -267,7 +308,7 @@ def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percda
         bws = ws.blocks(n)
         rc = L.pt2q_quantize_blocks(
             _lib.ptr(W), _lib.dtype_code(W), m, n, m, int(block_size), flags, _lib.ptr(Gm), m,
-            _lib.ptr(ws.Hinv), m, int(max_iter), _lib.ptr(out.alpha), _lib.ptr(out.mu), _lib.ptr(out.T),
+            _lib.ptr(Hinv), m, int(max_iter), _lib.ptr(out.alpha), _lib.ptr(out.mu), _lib.ptr(out.T),
             _lib.dtype_code(out.T), _lib.ptr(out.perm), _lib.ptr(out.iters), _lib.ptr(bws), bws.numel(), st)
         _lib.check(rc, "pt2q_quantize_blocks")
         statuses.append(_lib.status_view(bws).clone())
@@ -328,9 +369,11 @@ class UnitPipeline:
         return self.lanes[0].workspace(m)
 
     def run(self, Ws, X: Optional[torch.Tensor] = None, G: Optional[torch.Tensor] = None,
-            nsamples: Optional[int] = None):
+            nsamples: Optional[int] = None, Hinv: Optional[torch.Tensor] = None,
+            info: Optional[torch.Tensor] = None):
         """Issue one unit: its Gram from X, or -- with G (a raw Gram over nsamples rows, e.g. a
-        GramAccumulator's, read in place and not modified) -- its tail alone."""
+        GramAccumulator's, read in place and not modified) -- its tail alone; with Hinv and info
+        as well (an item of hessian_inverse_batched), only its block loops."""
         Ws = [_float_input(W) for W in Ws]
         if X is not None:
             X = _float_input(X.reshape(-1, X.shape[-1]))
@@ -347,7 +390,7 @@ class UnitPipeline:
             if G is not None:
                 G = G.contiguous().float()
                 run = _unit_tail(Ws, G, N, ws, [], X, G, self.bs, self.use_ssr, self.percdamp,
-                                 self.max_iter, torch.int8)
+                                 self.max_iter, torch.int8, Hinv=Hinv, info=info)
                 run.join = self.join
                 return run
             if self.gram_done is not None:

@@ -193,8 +193,12 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
     runs = []
     if grams_first is not None:  # every Gram of this rank first, then the tails (GramsFirst)
         inputs = {i: provider(units[i]) for i in mine}
+        if hasattr(grams_first, "begin"):
+            grams_first.begin([(i, units[i][1][0][2], units[i][2]) for i in mine])
         for i in mine:
             grams_first.gram(i, inputs[i][0])
+        if hasattr(grams_first, "inverses"):
+            grams_first.inverses()
         for i in mine:
             name, lins, N = units[i]
             Wd = inputs[i][1]
@@ -281,33 +285,86 @@ def quantize_layer_split(Ws, X_local: torch.Tensor, dst: int = 0, group=None, bl
 class GramsFirst:
     """The step schedule for independent units whose activations are all at hand (synthetic or
     pre-captured; within one decoder layer of the real flow, calibration.quantize_decoder_layer):
-    every unit's Gram back to back on the caller's stream, each into a raw-Gram buffer of its own
-    (Σ m² fp32: 21.7 GB for Llama-2-7B), then the units' tails on the lanes of an
-    engine.UnitPipeline.  A Gram holds every CU for its whole duration, so interleaving the Grams
-    with other units' tails only stalls those tails; keeping the phases apart measured 2.80 s
-    against 2.95 s per 7B step.  Results are bit-identical to any other order.
+
+    1. every unit's Gram back to back on the caller's stream, each into its slot of a packed
+       (units, m, m) raw-Gram buffer per (width, rows) group (Σ m² fp32: 21.7 GB for Llama-2-7B);
+    2. (batched=True) every group's damped Hessian inverses by engine.hessian_inverse_batched:
+       each step of the blocked Cholesky factorisation serves all units of a chunk in one launch,
+       instead of 64-172 latency-bound steps per unit;
+    3. the units' block loops on the lanes of an engine.UnitPipeline (with batched=False the
+       lanes also run each unit's own damping and Cholesky inverse).
+
+    A Gram holds every CU for its whole duration, so interleaving the Grams with other units'
+    tails only stalls those tails; keeping the phases apart measured 2.80 s against 2.95 s per 7B
+    step.  Results are bit-identical to any other order.
 
     Stall reporting: the Grams of one width share a workspace, and every pt2q_gram call zeroes
     its status word first, so after each Gram its word is OR-ed (on the stream) into one
     per-step device word; check() reads that word once and clears it."""
 
-    def __init__(self, pipe, device):
+    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
+        self.batched, self.chunk, self.percdamp = batched, chunk, percdamp
         self.G, self.ws = {}, {}
+        self.slot = {}       # key -> (group, index)
+        self.groups = {}     # (m, N) -> {"G", "Hinv", "info"} packed over the group's units
+        self.scratch = {}
         self.stall = torch.zeros(1, dtype=torch.int32, device=self.dev)
+
+    def begin(self, units):
+        """Slots for this step's units [(key, m, N)]: one packed buffer per (m, N) group,
+        reused while the step's shape does not change."""
+        count = {}
+        self.slot = {}
+        for key, m, N in units:
+            g = (m, int(N))
+            self.slot[key] = (g, count.get(g, 0))
+            count[g] = count.get(g, 0) + 1
+        for g, c in count.items():
+            have = self.groups.get(g)
+            if have is None or have["G"].shape[0] != c:
+                m = g[0]
+                self.groups[g] = {"G": torch.empty((c, m, m), dtype=torch.float32, device=self.dev),
+                                  "Hinv": torch.empty((c, m, m), dtype=torch.float32, device=self.dev)
+                                  if self.batched else None,
+                                  "info": torch.zeros(c, dtype=torch.int32, device=self.dev)}
+        for g in [g for g in self.groups if g not in count]:
+            del self.groups[g]
+        self.G = {}
+
+    def _gbuf(self, key, m):
+        if key in self.slot:
+            g, z = self.slot[key]
+            return self.groups[g]["G"][z]
+        if key not in self.G or self.G[key].shape[0] != m:  # no begin(): a buffer of its own
+            self.G[key] = torch.empty((m, m), dtype=torch.float32, device=self.dev)
+        return self.G[key]
 
     def gram(self, key, X):
         X2 = X.reshape(-1, X.shape[-1])
         m = X2.shape[1]
-        if key not in self.G or self.G[key].shape[0] != m:
-            self.G[key] = torch.empty((m, m), dtype=torch.float32, device=self.dev)
         if m not in self.ws:
             self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
-        self.engine.gram(X2, G=self.G[key], workspace=self.ws[m], check=False)
+        self.engine.gram(X2, G=self._gbuf(key, m), workspace=self.ws[m], check=False)
         torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
 
+    def inverses(self):
+        """Step 2: every group's Hessian inverses, batched (no-op with batched=False)."""
+        if not self.batched:
+            return
+        for (m, N), grp in self.groups.items():
+            self.engine.hessian_inverse_batched(grp["G"], N, self.percdamp, Hinv=grp["Hinv"], info=grp["info"],
+                                                scratch=self.scratch, chunk=self.chunk)
+
     def tail(self, key, Ws, nsamples):
+        if key in self.slot:
+            g, z = self.slot[key]
+            grp = self.groups[g]
+            if self.batched:
+                return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples, Hinv=grp["Hinv"][z],
+                                     info=grp["info"][z:z + 1])
+            return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples)
         return self.pipe.run(Ws, G=self.G[key], nsamples=nsamples)
 
     def check(self):

@@ -121,9 +121,11 @@ def test_unit_pipeline_equals_sequential(pt2q, lanes):
                 assert bits_equal(host(a), host(b))
 
 
-def test_grams_first_schedule_equals_sequential(pt2q):
-    """sharding.GramsFirst (every Gram of the step first, each into its own buffer, then the
-    tails on the pipeline lanes) through quantize_units_sharded == quantize_unit per unit."""
+@pytest.mark.parametrize("batched,chunk", [(False, 32), (True, 32), (True, 1)])
+def test_grams_first_schedule_equals_sequential(pt2q, batched, chunk):
+    """sharding.GramsFirst (every Gram of the step first into packed per-width slots, then --
+    batched -- every width's Hessian inverses in batched launches, then the block loops on the
+    pipeline lanes) through quantize_units_sharded == quantize_unit per unit."""
     import importlib
     sharding = importlib.import_module("pt2q.sharding")
     specs = [(512, (384, 256), 1024, torch.float16), (768, (512,), 2048, torch.float16),
@@ -135,9 +137,14 @@ def test_grams_first_schedule_equals_sequential(pt2q):
         units.append((f"u{i}", [(f"p{k}", n, m) for k, n in enumerate(ns)], N))
         data[f"u{i}"] = (X, Ws)
     pipe = pt2q.UnitPipeline("cuda", 128, True, lanes=3)
-    gf = sharding.GramsFirst(pipe, "cuda")
+    gf = sharding.GramsFirst(pipe, "cuda", batched=batched, chunk=chunk)
     res, mine = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False,
                                                 grams_first=gf)
+    res2, _ = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False,
+                                              grams_first=gf)  # second step reuses the slots
+    for k in res:
+        for f in res[k]:
+            assert bits_equal(host(res[k][f]), host(res2[k][f])), (k, f)
     assert mine == list(range(len(units))) or sorted(mine) == list(range(len(units)))
     for name, lins, _ in units:
         X, Ws = data[name]

@@ -119,6 +119,29 @@ def test_hessian_cholesky_inverse_bitexact(pt2q, m, N):
     assert bits_equal(host(Hinv), Hinv_r)
 
 
+@pytest.mark.parametrize("m,batch,chunk", [(100, 3, 32), (384, 4, 3), (2200, 2, 32), (4096, 3, 32),
+                                            (6400, 2, 32), (11008, 2, 32)])
+def test_hessian_inverse_batched_equals_per_item(pt2q, m, batch, chunk):
+    """engine.hessian_inverse_batched (one launch per factorisation step for all items of a
+    chunk) == prepare_hessian + cholesky_inverse per item, bit for bit; an item whose Hessian is
+    not positive definite reports its own pivot and leaves the others intact (m = 6400: the
+    per-item call uses the look-ahead, the batch does not -- same bits)."""
+    Gs = []
+    for z in range(batch):
+        N = m + 37 * z
+        Gs.append(pt2q.gram(pt2q.fill_synthetic((N, m), 50 + m + z, outliers=True, device="cuda")))
+    Gs[1] = -Gs[1]  # damping a negative definite Gram: breakdown at the first pivot
+    G = torch.stack(Gs).contiguous()
+    Hinv, info = pt2q.engine.hessian_inverse_batched(G, 4096, 0.01, chunk=chunk)
+    info = host(info)
+    for z in range(batch):
+        H, _ = pt2q.prepare_hessian(G[z], 4096, 0.01)
+        want, spd = pt2q.cholesky_inverse(H)
+        assert (info[z] == 0) == spd == (z != 1), (z, info[z])
+        if spd:
+            assert bits_equal(host(Hinv[z]), host(want)), z
+
+
 def test_cholesky_breakdown_reports_and_falls_back(pt2q):
     H = np.eye(80, dtype=np.float32)
     H[37, 37] = -1.0

@@ -1,0 +1,46 @@
+"""Per-phase kernel totals of the LAST grams-first step in a rocprofv3 kernel trace (dev tool):
+python tools/phase_kstats.py <kernel_trace.csv> [--top 20]
+Phases: gram (gram16* launches), inverse (after the last Gram up to the first block-loop kernel),
+tails (the rest).  Prints the span, busy time and per-kernel totals of each phase."""
+import argparse
+import csv
+from collections import defaultdict
+
+from kstats import short
+
+LOOP = ("ssr_", "atq_", "ef_gemm")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--top", type=int, default=15)
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    isg = [("gram16" in r["Kernel_Name"] or "gram_streamk" in r["Kernel_Name"]) for r in rows]
+    starts = [i for i in range(len(rows)) if isg[i] and (i == 0 or not isg[i - 1])]
+    # a step starts at a Gram run preceded by block-loop kernels
+    steps = [i for i in starts if i == 0 or any(k in rows[i - 1]["Kernel_Name"] for k in LOOP + ("transpose", "pack"))]
+    rows = rows[steps[-1]:]
+    lastg = max(i for i, r in enumerate(rows) if "gram16" in r["Kernel_Name"] or "gram_streamk" in r["Kernel_Name"])
+    firstl = min(i for i, r in enumerate(rows) if i > lastg and any(k in r["Kernel_Name"] for k in LOOP))
+    phases = {"gram": rows[:lastg + 1], "inverse": rows[lastg + 1:firstl], "tails": rows[firstl:]}
+    for ph, rs in phases.items():
+        if not rs:
+            continue
+        tot, cnt = defaultdict(float), defaultdict(int)
+        busy = 0.0
+        for r in rs:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            tot[short(r["Kernel_Name"])] += d
+            cnt[short(r["Kernel_Name"])] += 1
+            busy += d
+        span = (max(int(r["End_Timestamp"]) for r in rs) - int(rs[0]["Start_Timestamp"])) / 1e3
+        print(f"== {ph}: launches {len(rs)}  span {span / 1e3:.2f} ms  kernel-busy {busy / 1e3:.2f} ms")
+        for k, v in sorted(tot.items(), key=lambda x: -x[1])[:a.top]:
+            print(f"{v / 1e3:10.3f} ms {cnt[k]:7d}x avg {v / cnt[k]:9.2f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
