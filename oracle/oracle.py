@@ -58,6 +58,8 @@ def lib():
             "orc_quantize_blocks": (I, [f32p, L, I, I, I, I, I, f32p, L, f32p, L, I,
                                         f32p, f32p, i8p, i64p, i32p]),
             "orc_error_feedback": (None, [f32p, L, I, i64p, I, i64p, I, f32p, f32p, L]),
+            "orc_matvec16": (None, [f32p, L, I, I, f32p, f32p]),
+            "orc_rowsum_seq": (None, [f32p, L, I, I, f32p]),
             "orc_set_threads": (None, [I]),
             "orc_get_threads": (I, []),
         }
@@ -117,6 +119,22 @@ def iterative_ternary_fitting(W, alpha, mu, T, max_iter=100):
     a = _f32(np.reshape(alpha, -1)).copy(); m = _f32(np.reshape(mu, -1)).copy(); T = _f32(T).copy()
     it = lib().orc_itf(W, b, n, b, int(max_iter), a, m, T, b)
     return a[:, None], m[:, None], T, int(it)
+
+
+def matvec16(A, x):
+    """y[i] = DOT16(A[i], x): the contract order of the ATQ row products (fixture generator)."""
+    A = _f32(A)
+    y = np.empty(A.shape[0], np.float32)
+    lib().orc_matvec16(A, A.shape[1], A.shape[0], A.shape[1], _f32(x).reshape(-1), y)
+    return y
+
+
+def rowsum_seq(A):
+    """y[i] = l-ascending sum of A[i] (S1 = S·1 in the contract order; fixture generator)."""
+    A = _f32(A)
+    y = np.empty(A.shape[0], np.float32)
+    lib().orc_rowsum_seq(A, A.shape[1], A.shape[0], A.shape[1], y)
+    return y
 
 
 def s1_from_x(X):

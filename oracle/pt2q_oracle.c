@@ -71,6 +71,21 @@ static float sumsqn(const float* v, long n) {
   return butterfly(p, 64);
 }
 
+/* Canonical-order matrix-vector products for the fixture generator (tests/golden/gen_golden.py
+ * substitutes them for the reference's MKL sgemv inside its AGA, whose summation order is
+ * internal to MKL and CPU-dependent): y[i] = DOT16(A[i][:], x) (quantizer.py:224-233 v, WS1,
+ * (W∘T)S1, T²S1), and y[i] = l-ascending sum of A[i][:] (S1 = S·1, quantizer.py:216). */
+void orc_matvec16(const float* A, long lda, int n, int b, const float* x, float* y) {
+  for (int i = 0; i < n; ++i) y[i] = dot16(A + (long)i * lda, 1, x, b);
+}
+void orc_rowsum_seq(const float* A, long lda, int n, int b, float* y) {
+  for (int i = 0; i < n; ++i) {
+    float s = 0.0f;
+    for (int l = 0; l < b; ++l) s = s + A[(long)i * lda + l];
+    y[i] = s;
+  }
+}
+
 /* ---------------------------------------------------------------- ATQ (quantizer.py) */
 
 /* ternary_init quantizer.py:32-69 on W (n x b, row stride ldw). T as float. */

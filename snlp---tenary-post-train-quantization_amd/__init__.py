@@ -6,7 +6,7 @@ Drop-in for the reference's hot-path surface:
     GPTQ, GPTQQuantizer                                                            (gptq.py)
     PT2LLMQuantizer.quantize_layer                                                 (main.py)
     pack_ternary, unpack_ternary, save/load_quantized_model,
-    compute_bits_per_weight                                                        (utils.py)
+    compute_bits_per_weight, evaluate_perplexity                                   (utils.py)
     TernaryLinear, replace_linear_with_ternary                                     (model.py)
 All compute runs in libpt2q.so (HIP, gfx950); importing fails loudly if it is not built.
 """
@@ -19,6 +19,7 @@ from .calibration import (GramAccumulator, GramCapture, find_linear_layers, get_
                           quantize_decoder_layer)
 from .ternary import (TernaryLinear, compute_bits_per_weight, load_quantized_model,
                       replace_linear_with_ternary, save_quantized_model)
+from .evaluation import evaluate_perplexity
 from .engine import (LayerGraph, LayerOutput, LayerWorkspace, UnitRun, UnitWorkspace, cholesky_inverse,
                      dequantize, error_feedback, fill_synthetic, gram, hessian_inverse, pack_ternary, prepare_hessian,
                      quantize_blocks, quantize_layer, quantize_shared, quantize_unit, unpack_ternary,
@@ -34,5 +35,5 @@ __all__ = [
     "GramCapture", "find_linear_layers", "get_llm_layers", "quantize_decoder_layer",
     "TernaryLinear", "replace_linear_with_ternary", "save_quantized_model", "load_quantized_model",
     "UnitRun", "UnitWorkspace", "quantize_unit", "compute_bits_per_weight", "error_feedback",
-    "UnitPipeline", "sum_partials",
+    "UnitPipeline", "sum_partials", "evaluate_perplexity",
 ]

@@ -429,10 +429,175 @@ def gen_model():
     save("model_llama2l", **kw)
 
 
+@contextlib.contextmanager
+def canonical_matvecs():
+    """Inside the block, while the reference's AGA method runs (quantizer.py:177-248), every
+    matrix-VECTOR product it issues through Tensor.__matmul__ (S·1, 1ᵀS1, T·S1, W·S1, (W∘T)·S1,
+    T²·S1 -- MKL sgemv, whose summation order is internal to MKL and differs by CPU code path)
+    runs in the PT2Q contract order instead (oracle.rowsum_seq / sequential / oracle.matvec16).
+    Also torch.topk (reorder.py:133), whose order among EXACTLY tied similarities is
+    std::nth_element's, takes ties by position (the contract's total order).  Every other
+    operation of the reference, the SSR similarity's product included, is untouched.  On ill-conditioned AGA rows (the random-init
+    model's layer-1 activations) the 2x2 solve amplifies the ulp-level order differences of
+    those sums far beyond the 1e-5 scale contract, so a bit-level pin needs one fixed order."""
+    from oracle import oracle as orc
+    mm = torch.Tensor.__matmul__
+
+    def canon(a, b):
+        if a.dim() == 2 and b.dim() == 2 and b.shape[1] == 1 and a.shape[1] == b.shape[0] \
+                and a.dtype == torch.float32 and b.dtype == torch.float32:
+            A, x = a.detach().contiguous().numpy(), b.detach().contiguous().numpy()[:, 0]
+            if a.shape[0] == 1 and bool(np.all(A == 1.0)):  # d = 1ᵀS1: j-ascending sum
+                y = orc.rowsum_seq(x[None, :])
+            elif bool(np.all(x == 1.0)):                     # S1 = S·1: l-ascending sums
+                y = orc.rowsum_seq(A)
+            else:                                            # row products: DOT16
+                y = orc.matvec16(A, x)
+            return torch.from_numpy(np.asarray(y, np.float32).reshape(-1, 1))
+        return mm(a, b)
+    cls = rq.AsymmetricTernaryQuantizer
+    aga = cls.activation_aware_grid_alignment
+
+    def aga_canon(self, *args, **kw):
+        torch.Tensor.__matmul__ = canon
+        try:
+            return aga(self, *args, **kw)
+        finally:
+            torch.Tensor.__matmul__ = mm
+    cls.activation_aware_grid_alignment = aga_canon
+    # torch.topk (reorder.py:133) breaks exact ties in std::nth_element's order; the contract
+    # (and the oracle) order ties by position: value descending, then position ascending
+    topk = torch.topk
+
+    def stable_topk(x, k, *args, **kw):
+        if args or kw:
+            return topk(x, k, *args, **kw)
+        idx = torch.sort(x, descending=True, stable=True).indices[:k]
+        return torch.return_types.topk((x[idx], idx))
+    torch.topk = stable_topk
+    try:
+        yield
+    finally:
+        cls.activation_aware_grid_alignment = aga
+        torch.topk = topk
+
+
+def gen_model_tf():
+    """Teacher-forced pin of decoder layer 1 of the model loop: the reference's
+    PT2LLMQuantizer.quantize on the 2-layer Llama of gen_model, with its quantize_layer wrapped to
+    record the activations each layer-1 linear receives (captured after layer 0's write-back,
+    main.py:262-299) -- one array per distinct input (q/k/v share one, gate/up share one).
+    For each layer-1 linear the fixture also holds the reference's own loop components run on
+    exactly those inputs and the layer's ORIGINAL weight with the engine's canonical H^-1
+    (ref_loop_with_hinv, as gen_loop16) and the AGA's matrix-vector sums in the contract order
+    (canonical_matvecs), so the GPU engine fed the same inputs must reproduce codes and
+    permutation exactly and scales within the contract.  The reference's own quantize_layer
+    output on the same inputs (MKL H^-1 and sums) is stored beside it (ref_*)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle import oracle as orc
+    orc.set_threads(8)
+    print("teacher-forced model-loop fixture (layer 1 inputs, main.py:262-299)")
+    model, samples = tiny_llama_and_samples()
+    q = rm.PT2LLMQuantizer(model, None, model_type="llama", block_size=128, use_ssr=True,
+                           device="cpu")
+    q.get_calibration_data = lambda: samples
+    seen = {}
+    orig = q.quantize_layer
+
+    def rec(layer, name, acts):
+        if name.startswith("layer_1."):
+            seen[name] = (layer.weight.data.clone().numpy(), acts.detach().clone().numpy())
+        return orig(layer, name, acts)
+    q.quantize_layer = rec
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        params = q.quantize()
+    names = sorted(seen)
+    inputs, kw = {}, {"names": np.array(names)}
+    for i, name in enumerate(names):
+        W, A = seen[name]
+        X = np.ascontiguousarray(A.reshape(-1, A.shape[-1]).astype(np.float32))
+        key = next((k for k, v in inputs.items() if v.shape == X.shape and np.array_equal(v, X)), None)
+        if key is None:
+            key = f"X{len(inputs)}"
+            inputs[key] = X
+        kw[f"xkey{i}"] = key
+        G = orc.gram(X)
+        H, _ = orc.prepare_hessian(G, X.shape[0])
+        Hinv, spd = orc.cholesky_inverse(H)
+        assert spd
+        with canonical_matvecs():
+            r = ref_loop_with_hinv(W, X, Hinv)
+        kw[f"alpha{i}"], kw[f"mu{i}"], kw[f"perm{i}"] = r["alpha"], r["mu"], r["perm"]
+        kw[f"T2_{i}"] = pack2(r["T"])
+        kw[f"m{i}"] = W.shape[1]
+        # the reference's own quantize_layer on the same inputs (its MKL H^-1)
+        p = params[name]
+        kw[f"ref_perm{i}"] = p["perm"].numpy()
+        kw[f"ref_T2_{i}"] = pack2(p["T"].numpy())
+        kw[f"ref_alpha{i}"], kw[f"ref_mu{i}"] = p["alpha"].numpy(), p["mu"].numpy()
+        o = orc.quantize_layer_m(W, X)
+        print(f"    {name}: oracle vs common-H^-1 reference loop: perm "
+              f"{'==' if np.array_equal(o['perm'], r['perm']) else '!='}, codes "
+              f"{(o['T'] == r['T']).mean():.6f}, alpha max|d| {np.abs(o['alpha'] - r['alpha']).max():.2e}")
+    kw.update(inputs)
+    save("model_llama2l_tf", **kw)
+
+
+def gen_ppl():
+    """The reference's evaluate_perplexity (utils.py:128-186) with its data source replaced
+    (load_dataset -> fixed text, the tokenizer -> a stub returning fixed token ids; there is no
+    network), on the tiny Llama of gen_model: (a) the fp32 model as built, for two window lengths
+    (a ragged last window; seq_len > L); (b) the model after the reference's own
+    replace_linear_with_ternary (model.py:174-225) with per-block ATQ params of every decoder
+    linear (stored, 2-bit packed)."""
+    import utils as ru
+    import model as rmod
+    print("perplexity fixture (utils.py:128-186)")
+    torch.manual_seed(2)
+    ids = torch.randint(0, TINY_LLAMA["vocab_size"], (1, 300))
+
+    class StubTok:
+        def __call__(self, text, return_tensors="pt"):
+            return {"input_ids": ids.clone()}
+    orig = ru.load_dataset
+    ru.load_dataset = lambda *a, **k: {"text": ["offline", "stub"]}
+    try:
+        model, samples = tiny_llama_and_samples()
+        ppl = {s_: ru.evaluate_perplexity(model, StubTok(), seq_len=s_, device=torch.device("cpu"))
+               for s_ in (128, 512)}
+        # ternary params: the reference's ATQ per 128-column block without activations
+        # (quantizer.py:250-277, X = None: no AGA -- the AGA of this random-init model yields
+        # alphas up to ~1e28 and a NaN perplexity), columns in order (perm = arange)
+        atq = rq.AsymmetricTernaryQuantizer()
+        params, kw = {}, {}
+        for name, mod in sorted(model.named_modules()):
+            if isinstance(mod, torch.nn.Linear) and ".layers." in f".{name}":
+                W = mod.weight.data.clone()
+                a_, m_, T_ = [], [], []
+                for c0 in range(0, W.shape[1], 128):
+                    a, mu, T = atq.quantize(W[:, c0:c0 + 128])
+                    a_.append(a); m_.append(mu); T_.append(T)
+                params[name] = {"alpha": torch.cat(a_, 1), "mu": torch.cat(m_, 1),
+                                "T": torch.cat(T_, 1).to(torch.int8), "perm": torch.arange(W.shape[1])}
+        for i, name in enumerate(sorted(params)):
+            kw[f"tname{i}"] = name
+            kw[f"talpha{i}"] = params[name]["alpha"].numpy()
+            kw[f"tmu{i}"] = params[name]["mu"].numpy()
+            kw[f"tT2_{i}"] = pack2(params[name]["T"].numpy())
+        rmod.replace_linear_with_ternary(model, params, block_size=128)
+        ppl_t = ru.evaluate_perplexity(model, StubTok(), seq_len=128, device=torch.device("cpu"))
+    finally:
+        ru.load_dataset = orig
+    print(f"    ppl fp32 {ppl}, ternary (reference TernaryLinear, {len(params)} linears) {ppl_t}")
+    save("ppl_llama2l", ids=ids.numpy(), seq_lens=np.array([128, 512]),
+         ppl=np.array([ppl[128], ppl[512]], np.float64), ppl_ternary_128=np.float64(ppl_t),
+         nlin=len(params), **kw)
+
+
 GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
               "trace": gen_trace, "examples": gen_examples, "wide": gen_wide,
               "ternary": gen_ternary, "fp16": gen_fp16, "loop16": gen_loop16,
-              "model": gen_model}
+              "model": gen_model, "model_tf": gen_model_tf, "ppl": gen_ppl}
 
 if __name__ == "__main__":
     # `python gen_golden.py [group ...]` regenerates only the named groups (default: all)

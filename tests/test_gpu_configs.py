@@ -98,6 +98,33 @@ def test_headline_bench_workload(pt2q):
         assert bits_equal(host(a), host(b))
 
 
+@pytest.mark.parametrize("m", [4096, 11008])
+def test_gram16_full_length_vs_oracle_and_f64(pt2q, m):
+    """the bench's own Gram launches at full length (fp16, N = 262144 rows; m =
+    4096: gram16x_kernel, 128 x 256 tiles; m = 11008: gram16w_kernel, 256 x 256 tiles) on sampled
+    column blocks: bit-exact to the oracle's 16-bit MFMA arithmetic, and at least as accurate
+    as the fp32 k-ascending chain (the reference's fp32 arithmetic, main.py:128) against an f64
+    Gram of the same columns -- error of each entry scaled by sqrt(G_ii G_jj)."""
+    N = 262144
+    Xd = pt2q.fill_synthetic((N, m), 2000 + m, std=1.0, outliers=True).half()
+    G = pt2q.gram(Xd)
+    torch.cuda.synchronize()
+    S = sample_cols(m)
+    Xs = host(Xd[:, torch.from_numpy(S).to(Xd.device)].contiguous())
+    del Xd
+    Gs = host(G)[np.ix_(S, S)]
+    del G
+    orc.set_threads(16)
+    assert bits_equal(Gs, orc.gram16(Xs)), "sampled full-length Gram tiles differ from the oracle"
+    X64 = Xs.astype(np.float64)
+    G64 = X64.T @ X64
+    scale = np.sqrt(np.outer(np.diag(G64), np.diag(G64)))
+    err16 = np.abs(Gs - G64) / scale
+    err32 = np.abs(orc.gram(Xs.astype(np.float32)) - G64) / scale
+    assert err16.max() <= err32.max(), (float(err16.max()), float(err32.max()))
+    assert err16.max() < 1e-4
+
+
 CONFIGS = [
     # C2 GPT-2-small (Conv1D weights transposed to n x m), N = 2048, SSR on
     ("c2_attn_c_proj", 768, 768, 2048, torch.float32, 128),

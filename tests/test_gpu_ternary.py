@@ -123,3 +123,26 @@ def test_replace_save_load_roundtrip(pt2q, tmp_path):
 
 def host_t(t):
     return t.detach().cpu()
+
+
+def test_perplexity_ternary_model_vs_reference(pt2q):
+    """f4 on the ternary path: the tiny Llama with every decoder linear swapped for the libpt2q
+    TernaryLinear (per-block ATQ params of the fixture, fp16 MFMA kernel) evaluated on the GPU
+    by evaluate_perplexity, vs the reference's evaluate_perplexity of the same model built with
+    its own fp32 TernaryLinear on the CPU (gen_golden.gen_ppl): the perplexities agree to the
+    fp16 activation rounding of the kernel (relative 5e-3)."""
+    from conftest import load_golden, unpack2
+    from test_gpu_model import tiny_llama_and_samples
+    g = load_golden("ppl_llama2l")
+    model = tiny_llama_and_samples()[0].cuda()
+    params = {}
+    for i in range(int(g["nlin"])):
+        a = torch.from_numpy(g[f"talpha{i}"])
+        params[str(g[f"tname{i}"])] = {"alpha": a, "mu": torch.from_numpy(g[f"tmu{i}"]),
+                                       "T": torch.from_numpy(unpack2(g[f"tT2_{i}"], a.shape[1] * 128)),
+                                       "perm": torch.arange(a.shape[1] * 128)}
+    pt2q.replace_linear_with_ternary(model, params, block_size=128, compat=True)
+    assert sum(isinstance(m, pt2q.TernaryLinear) for m in model.modules()) == int(g["nlin"])
+    got = pt2q.evaluate_perplexity(model, seq_len=128, input_ids=torch.from_numpy(g["ids"]))
+    want = float(g["ppl_ternary_128"])
+    assert np.isfinite(got) and abs(got - want) <= 5e-3 * want, (got, want)

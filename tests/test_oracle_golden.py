@@ -323,3 +323,44 @@ def test_gram16_chain_properties():
     ref = X.astype(np.float64).T @ X.astype(np.float64)
     scale = np.sqrt(np.outer(np.diag(ref), np.diag(ref)))
     assert np.max(np.abs(G - ref) / scale) < 1e-6
+
+
+# ----------------------------------------------------------------- teacher-forced model layer 1
+
+def layer1_inputs_tf():
+    """(names, [(W, X)]) of the teacher-forced layer-1 fixture: W = the linear's weight when the
+    reference quantized it (layer 1 is untouched before then: the rebuilt model's own weight,
+    state-dict checksum checked), X = the activations the reference captured for it (after
+    layer 0's write-back, main.py:262-299)."""
+    import torch
+    pytest.importorskip("transformers")
+    from test_gpu_model import tiny_llama_and_samples
+    g = load_golden("model_llama2l_tf")
+    model, _ = tiny_llama_and_samples()
+    csum = np.array([float(p.detach().double().sum()) for p in model.state_dict().values()])
+    np.testing.assert_array_equal(csum, load_golden("model_llama2l")["checksum"])
+    sd = model.state_dict()
+    names = [str(n) for n in g["names"]]
+    out = []
+    for i, name in enumerate(names):
+        W = sd["model.layers.1." + name.split(".", 1)[1] + ".weight"].numpy().astype(np.float32)
+        out.append((W, np.ascontiguousarray(g[str(g[f"xkey{i}"])])))
+    del torch
+    return g, names, out
+
+
+def test_oracle_model_layer1_teacher_forced():
+    """Layer 1 of the model loop on the reference's own captured inputs: the
+    oracle reproduces the reference's loop -- run with the engine's H^-1 and with the two orders
+    the reference leaves to its libraries fixed to the contract's (MKL sgemv sums inside the AGA,
+    std::nth_element among exact top-k ties; tests/golden/gen_golden.py canonical_matvecs) --
+    bit for bit: permutation, codes, alpha and mu."""
+    from conftest import unpack2
+    g, names, data = layer1_inputs_tf()
+    assert len(names) == 7
+    for i, (name, (W, X)) in enumerate(zip(names, data)):
+        o = orc.quantize_layer_m(W, X)
+        m = int(g[f"m{i}"])
+        np.testing.assert_array_equal(o["perm"], g[f"perm{i}"], err_msg=name)
+        np.testing.assert_array_equal(o["T"], unpack2(g[f"T2_{i}"], m), err_msg=name)
+        assert np.array_equal(o["alpha"], g[f"alpha{i}"]) and np.array_equal(o["mu"], g[f"mu{i}"]), name

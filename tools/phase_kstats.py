@@ -18,12 +18,21 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    isg = [("gram16" in r["Kernel_Name"] or "gram_streamk" in r["Kernel_Name"]) for r in rows]
-    starts = [i for i in range(len(rows)) if isg[i] and (i == 0 or not isg[i - 1])]
-    # a step starts at a Gram run preceded by block-loop kernels
-    steps = [i for i in starts if i == 0 or any(k in rows[i - 1]["Kernel_Name"] for k in LOOP + ("transpose", "pack"))]
+    def isg(r):
+        return "gram16" in r["Kernel_Name"] or "gram_streamk" in r["Kernel_Name"]
+
+    def neutral(r):  # torch elementwise ops and fills between the Grams (status OR, memsets)
+        return "elementwise" in r["Kernel_Name"] or "fill" in r["Kernel_Name"].lower()
+    # a step starts at a Gram whose previous non-neutral kernel is not a Gram
+    steps, prev = [], None
+    for i, r in enumerate(rows):
+        if neutral(r):
+            continue
+        if isg(r) and (prev is None or not isg(prev)):
+            steps.append(i)
+        prev = r
     rows = rows[steps[-1]:]
-    lastg = max(i for i, r in enumerate(rows) if "gram16" in r["Kernel_Name"] or "gram_streamk" in r["Kernel_Name"])
+    lastg = max(i for i, r in enumerate(rows) if isg(r))
     firstl = min(i for i, r in enumerate(rows) if i > lastg and any(k in r["Kernel_Name"] for k in LOOP))
     phases = {"gram": rows[:lastg + 1], "inverse": rows[lastg + 1:firstl], "tails": rows[firstl:]}
     for ph, rs in phases.items():

@@ -11,4 +11,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
 cat $OUT/phase.txt
 f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
 python3 $R/tools/phase_kstats.py $f > $OUT/phase_kstats.txt && cat $OUT/phase_kstats.txt
-rm -f $f
+gzip -f $f
