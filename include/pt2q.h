@@ -132,6 +132,26 @@ int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int n, int m, i
                          int64_t* perm, int* iters_dev, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* The block loops of `count` (1..16) linears of one shape in ONE launch sequence: every block
+ * step's selection, ATQ and error-feedback launches serve all of them (grid.z = linear), so the
+ * latency-bound per-block kernels of small layers fill the chip and the error feedback's
+ * persistent workgroups stream the tiles of every linear.  Linear z: weights W[z], AGA matrix
+ * A[z] (raw Gram, PT2Q_AGA_ACT) and Hinv[z] (each m x m, leading dims lda / ldhi), outputs
+ * alpha[z], mu[z], T[z], perm[z], iters_dev[z] (nullable array / entries) exactly as
+ * pt2q_quantize_blocks on that linear alone -- bit for bit.  The pointer arrays are HOST arrays of
+ * device pointers, read during the call only.  Supports blocks of <= 128 columns with b < m,
+ * PT2Q_AGA_ACT or PT2Q_AGA_NONE, n <= 16384 with n % 4 == 0; else PT2Q_E_UNSUPPORTED (use
+ * pt2q_quantize_blocks per linear).  Replaces main.py:158-230 run over a list of linears (the
+ * q/k/v of several decoder layers, main.py:289-299).  workspace:
+ * pt2q_quantize_blocks_group_workspace_bytes(count, n, m, b, flags). */
+size_t pt2q_quantize_blocks_group_workspace_bytes(int count, int n, int m, int b, int flags);
+int pt2q_quantize_blocks_group(int count, const void* const* W, int wdtype, int64_t ldw, int n, int m,
+                               int b, int flags, const float* const* A, int64_t lda,
+                               const float* const* Hinv, int64_t ldhi, int max_iter,
+                               float* const* alpha, float* const* mu, void* const* T, int tdtype,
+                               int64_t* const* perm, int* const* iters_dev, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* Whole layer, variant M (main.py:102-230): gram -> prepare -> cholesky_inverse -> blocks.
  * If info_dev reports a breakdown the outputs are undefined; the caller recomputes Hinv with
  * pinv and calls pt2q_quantize_blocks (the staged path). */

@@ -19,6 +19,7 @@ STALL_BITS = {0x1: "Gram partial-tile hand-off", 0x2: "ATQ S1/d hand-off", 0x4: 
 F32, F16, BF16, I8 = 0, 1, 2, 3
 FLAG_SSR = 0x1
 AGA_NONE, AGA_ACT, AGA_HESS = 0x0, 0x10, 0x20
+AGA_MASK = 0x30
 STAGE_INIT, STAGE_GRID, STAGE_ROUND, STAGE_ITF, STAGE_AGA, STAGE_FULL = range(6)
 
 _DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.int8: I8}
@@ -54,6 +55,9 @@ _SIGS = {
     "pt2q_hessian_inverse_batched": (I, [P, I, I, I64, F, P, P, P, SZ, P, P]),
     "pt2q_quantize_blocks": (I, [P, I, I64, I, I, I, I, P, I64, P, I64, I, P, P, P, I, P, P, P,
                                  SZ, P]),
+    "pt2q_quantize_blocks_group_workspace_bytes": (SZ, [I, I, I, I, I]),
+    "pt2q_quantize_blocks_group": (I, [I, P, I, I64, I, I, I, I, P, I64, P, I64, I, P, P, P, I, P, P, P,
+                                       SZ, P]),
     "pt2q_quantize_layer": (I, [P, I, I64, I, I, P, I, I64, I64, I, I, F, I, P, P, P, I, P, P, P,
                                 P, SZ, P]),
     "pt2q_atq_stage": (I, [I, P, I64, I, I, P, P, P, I64, P, P, I, P, P, SZ, P]),
@@ -144,6 +148,12 @@ def compute_device(*tensors):
         raise Pt2qError("pt2q kernels need an MI355X (HIP device); none is visible and there is "
                         "no CPU path")
     return torch.device("cuda", torch.cuda.current_device())
+
+
+def ptr_array(tensors):
+    """A host array of device pointers (the pointer-array arguments of the grouped entries)."""
+    arr = (ctypes.c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
+    return ctypes.cast(arr, ctypes.c_void_p), arr  # keep `arr` alive across the call
 
 
 def workspace(nbytes, device):

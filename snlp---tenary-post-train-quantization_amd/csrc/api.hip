@@ -4,6 +4,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "common.hpp"
@@ -263,6 +264,96 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   return PT2Q_OK;
 }
 
+// ---- grouped block loops (pt2q_quantize_blocks_group): per-linear workspace slices of one size
+
+// A linear's slice: the block-loop buffers plus its permutation (int64, written by the
+// selection launches and copied out at the end).
+size_t group_slice_bytes(int n, int m, int b, int flags) {
+  return blocks_bytes(n, m, b, flags) + (((size_t)m * 8 + 255) & ~(size_t)255);
+}
+
+// Every linear's counters and ITF iteration slots zeroed, its remaining set = [0, m).
+__global__ void group_init_kernel(int* counters, int ncnt, int* iters, int B, int* rem0, int m, long zs) {
+  counters = zws(counters, zs);
+  iters = zws(iters, zs);
+  rem0 = zws(rem0, zs);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ncnt) counters[t] = 0;
+  if (t < B) iters[t] = 0;
+  if (t < m) rem0[t] = t;
+}
+
+int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, int n, int m, int b,
+                     int flags, const float* const* A, long lda, const float* const* Hinv, long ldhi,
+                     int max_iter, float* const* alpha, float* const* mu, void* const* T, int tdtype,
+                     int64_t* const* perm, int* const* iters_dev, BlockWs& w, int64_t* perm64,
+                     long zs, hipStream_t st) {
+  int rc;
+  const int B = ceil_div(m, b);
+  const bool ssr = (flags & PT2Q_FLAG_SSR) != 0;
+  const bool act = (flags & PT2Q_AGA_MASK) == PT2Q_AGA_ACT;
+  Grp g{};
+  g.ws = zs;
+  g.count = count;
+  for (int z = 0; z < count; ++z) {
+    g.G[z] = act ? A[z] : nullptr;
+    g.Hinv[z] = Hinv[z];
+    // W (n x m) -> Wt (m x ldw, fp32) of every linear
+    if ((rc = pt2q_launch_transpose_to_f32(W[z], wdtype, ldw_in, n, m, (float*)((char*)w.Wt + z * zs), w.ldw,
+                                           st)) != PT2Q_OK)
+      return rc;
+  }
+  const int ncnt = 4 * B + pt2q_ssr_counter_ints(n);
+  hipLaunchKernelGGL(group_init_kernel, dim3(ceil_div(std::max(std::max(ncnt, B), m), 256), 1, count), dim3(256),
+                     0, st, w.counters, ncnt, w.iters, B, w.rem[0], m, zs);
+  PT2Q_LAUNCH_CHECK();
+  float* part = w.ssr;
+  float* wn = part + (size_t)ceil_div(m, 128) * n;
+  float* sim = wn + n;
+  int processed = 0, r = m, cur = 0;
+  for (int k = 0; k < B; ++k) {
+    const int bs = r < b ? r : b;
+    const int nr = r - bs;
+    int* rem = w.rem[cur];
+    int* nrem = w.rem[cur ^ 1];
+    if (ssr && r > b) {
+      if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B, &g)) !=
+          PT2Q_OK)
+        return rc;
+      if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm64 + processed, st, nullptr, 0, nullptr,
+                                     nullptr, nullptr, w.status, &g)) != PT2Q_OK)
+        return rc;
+    } else if ((rc = pt2q_launch_select_seq(ssr ? 1 : 0, ssr ? 0 : processed, bs, m, ssr ? rem : nullptr, w.blk,
+                                            nrem, perm64 + processed, st, &g)) != PT2Q_OK) {
+      return rc;
+    }
+    // variant M: S1/d of every linear's block formed inside its ATQ launch (table g.G)
+    if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, act ? w.S1 : nullptr, w.d, max_iter,
+                                    w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
+                                    nr > 0 ? w.Et : nullptr, w.ldw, w.iters + k, w.counters + 2 * k, st,
+                                    Hinv[0], ldhi, nrem, nr, w.Ck, m, w.iters_part, act ? A[0] : nullptr, lda,
+                                    act ? w.counters + 2 * B + 2 * k : nullptr, w.status, &g)) != PT2Q_OK)
+      return rc;
+    if (nr > 0 && (rc = pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, &g)) != PT2Q_OK)
+      return rc;
+    processed += bs;
+    r = nr;
+    cur ^= 1;
+  }
+  for (int z = 0; z < count; ++z) {  // outputs: T (n x m), alpha / mu (n x B), perm, iters
+    auto sl = [&](auto* p) { return (decltype(p))((char*)p + z * zs); };
+    if ((rc = pt2q_launch_transpose_i8(sl(w.Tt), w.ldw, m, n, T[z], tdtype, m, st)) != PT2Q_OK) return rc;
+    if ((rc = pt2q_launch_transpose_f32(sl(w.alpha_t), n, B, n, alpha[z], B, st)) != PT2Q_OK) return rc;
+    if ((rc = pt2q_launch_transpose_f32(sl(w.mu_t), n, B, n, mu[z], B, st)) != PT2Q_OK) return rc;
+    if (hipMemcpyAsync(perm[z], sl(perm64), sizeof(int64_t) * m, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return PT2Q_E_HIP;
+    if (iters_dev && iters_dev[z] &&
+        hipMemcpyAsync(iters_dev[z], sl(w.iters), sizeof(int) * B, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      return PT2Q_E_HIP;
+  }
+  return PT2Q_OK;
+}
+
 bool dtype_ok(int dt) { return dt == PT2Q_F32 || dt == PT2Q_F16 || dt == PT2Q_BF16; }
 
 // The status word every workspace-taking call reserves first (PT2Q_STATUS_BYTES), zeroed on the
@@ -402,6 +493,49 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
   if (!carve_blocks(c, n, m, b, w, flags)) return PT2Q_E_WORKSPACE;
   return run_blocks(W, wdtype, ldw, n, m, b, flags, A, lda, Hinv, ldhi, max_iter, alpha, mu, T,
                     tdtype, perm, iters_dev, w, (hipStream_t)stream);
+}
+
+extern "C" size_t pt2q_quantize_blocks_group_workspace_bytes(int count, int n, int m, int b, int flags) {
+  if (count <= 0 || n <= 0 || m <= 0 || b <= 0) return 0;
+  return PT2Q_STATUS_BYTES + (size_t)count * group_slice_bytes(n, m, b, flags);
+}
+
+extern "C" int pt2q_quantize_blocks_group(int count, const void* const* W, int wdtype, int64_t ldw, int n,
+                                          int m, int b, int flags, const float* const* A, int64_t lda,
+                                          const float* const* Hinv, int64_t ldhi, int max_iter,
+                                          float* const* alpha, float* const* mu, void* const* T, int tdtype,
+                                          int64_t* const* perm, int* const* iters_dev, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int aga = flags & PT2Q_AGA_MASK;
+  if (count <= 0 || count > PT2Q_GROUP_MAX || !W || !Hinv || !alpha || !mu || !T || !perm || n <= 0 ||
+      m <= 0 || b <= 0 || !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0 ||
+      ldw < m || ldhi < m)
+    return PT2Q_E_ARG;
+  if (aga == PT2Q_AGA_ACT && (!A || lda < m)) return PT2Q_E_ARG;
+  for (int z = 0; z < count; ++z)
+    if (!W[z] || !Hinv[z] || !alpha[z] || !mu[z] || !T[z] || !perm[z] || (aga == PT2Q_AGA_ACT && !A[z]))
+      return PT2Q_E_ARG;
+  // grouped launches: blocks of at most 128 columns, several blocks (the error feedback runs),
+  // variant M (S1/d in the ATQ launch) or no AGA, the fused w-bar, the EF kernel
+  const Pt2qTuning& tu = pt2q_tuning();
+  if (b > 128 || b >= m || m >= 65536 || (aga != PT2Q_AGA_ACT && aga != PT2Q_AGA_NONE) || !tu.s1_in_atq ||
+      !tu.ef_kernel || !tu.wbar_fused || n > 16384 || n % 4)
+    return PT2Q_E_UNSUPPORTED;
+  Carve c{(char*)workspace, workspace_bytes};
+  BlockWs w;
+  int rc;
+  w.status = take_status(c, st, rc);
+  if (rc != PT2Q_OK) return rc;
+  const size_t slice = group_slice_bytes(n, m, b, flags);
+  char* base = c.p;
+  if (!c.ok || !base || c.left < slice * count) return PT2Q_E_WORKSPACE;
+  Carve s0{base, slice};
+  if (!carve_blocks(s0, n, m, b, w, flags)) return PT2Q_E_WORKSPACE;
+  int64_t* perm64 = s0.take<int64_t>((size_t)m);
+  if (!s0.ok) return PT2Q_E_WORKSPACE;
+  return run_blocks_group(count, W, wdtype, ldw, n, m, b, flags, A, lda, Hinv, ldhi, max_iter, alpha, mu, T,
+                          tdtype, perm, iters_dev, w, perm64, (long)slice, st);
 }
 
 extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n, int m,

@@ -201,6 +201,28 @@ struct BlockArgs {
   long cap;          // polls before a wait gives up
 };
 
+// Grouped launch (grid.z = linear): this linear's pointers -- its workspace slice, its raw Gram.
+PT2Q_DEV BlockArgs at_linear(BlockArgs A, const Grp& g) {
+  if (g.count == 0) return A;
+  const long zs = g.ws;
+  A.Wt = zws(A.Wt, zs);
+  A.blk = zws(A.blk, zs);
+  A.S1 = zws(A.S1, zs);
+  A.d = zws(A.d, zs);
+  A.alpha = zws(A.alpha, zs);
+  A.mu = zws(A.mu, zs);
+  A.Tt = zws(A.Tt, zs);
+  A.Et = zws(A.Et, zs);
+  A.iters = zws(A.iters, zs);
+  A.counters = zws(A.counters, zs);
+  A.iters_part = zws(A.iters_part, zs);
+  A.s1sync = zws(A.s1sync, zs);
+  A.S1w = zws(A.S1w, zs);
+  A.dw = zws(A.dw, zs);
+  if (A.G) A.G = g.G[blockIdx.z];
+  return A;  // status: one word for the whole call
+}
+
 // S1 / d of the block formed by one wave itself, in the order of atq_s1_part (S1[j]: l-ascending
 // sum of G[blk_j][blk_l]; d: j-ascending sum of S1), so the values are the same bits.  The
 // fallback of a row wave whose wait for the leading workgroups gives up: under heavy concurrency
@@ -365,7 +387,8 @@ PT2Q_DEV void atq_s1_part(const BlockArgs& A) {
 }
 
 template <int NS, bool F>
-__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A) {
+__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A0, Grp g) {
+  const BlockArgs A = at_linear(A0, g);
   if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
     atq_s1_part(A);
     return;
@@ -401,7 +424,8 @@ PT2Q_DEV void finish_iters(const BlockArgs& A, int nparts) {
 // redoes every row without ITF.  (A last-arriving-workgroup repair inside atq_block_kernel cost
 // an agent-scope release fence - an L2 write-back - per workgroup.)
 template <int NS>
-__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A, int nparts) {
+__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A0, int nparts, Grp g) {
+  const BlockArgs A = at_linear(A0, g);
   finish_iters(A, nparts);
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
@@ -422,7 +446,13 @@ struct CoeffArgs {
 };
 
 template <int NS>
-__global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A, CoeffArgs K, int fix_wgs) {
+__global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A0, CoeffArgs K, int fix_wgs, Grp g) {
+  const BlockArgs A = at_linear(A0, g);
+  if (g.count > 0) {
+    K.Hinv = g.Hinv[blockIdx.z];
+    K.rem = zws(K.rem, g.ws);
+    K.C = zws(K.C, g.ws);
+  }
   finish_iters(A, fix_wgs);
   const long q = (long)blockIdx.x * 256 + threadIdx.x;
   if (q < (long)K.nr * K.bs) {
@@ -839,7 +869,10 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv, long ldh, const int* rem, int nr,
                           float* C, long ldc, int* iters_part, const float* G, long ldg,
-                          int* s1sync, int* status) {
+                          int* s1sync, int* status, const Grp* grp) {
+  const unsigned nz = grp_z(grp);
+  const Grp g = grp_or_none(grp);
+  if (nz > 1 && b > 512) return PT2Q_E_UNSUPPORTED;  // grouped launches: blocks <= 512 columns
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
@@ -857,17 +890,17 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
     if (b == 16 * NS)
-      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid + nS1), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid + nS1, 1, nz), dim3(256), 0, st, A, g);
     else
-      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid + nS1), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid + nS1, 1, nz), dim3(256), 0, st, A, g);
     PT2Q_LAUNCH_CHECK();
     if (Hinv && nr > 0) {  // zero-block repair + EF coefficients in one launch
       CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc};
       const int cgrid = ceil_div((long)nr * b, 256);
-      hipLaunchKernelGGL(atq_post_kernel<NS>, dim3(cgrid > grid ? cgrid : grid), dim3(256), 0, st, A,
-                         K, grid);
+      hipLaunchKernelGGL(atq_post_kernel<NS>, dim3(cgrid > grid ? cgrid : grid, 1, nz), dim3(256), 0, st, A,
+                         K, grid, g);
     } else {
-      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid), dim3(256), 0, st, A, grid);
+      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid, 1, nz), dim3(256), 0, st, A, grid, g);
     }
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;

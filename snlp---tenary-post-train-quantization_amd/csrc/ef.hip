@@ -40,7 +40,20 @@ struct EfArgs {
   long ldw;
   const int* crow;  // rem (nr entries)
   int nr, bs, te, ti, ntile, nh;
+  long zs;          // grouped: bytes between the linears' workspace slices (Ck, Et, Wt, crow)
+  int nz;           // linears; the work line is nz * ntile tiles, linear-major
 };
+
+// The arguments of linear z (its workspace slice).
+PT2Q_DEV EfArgs ef_linear(const EfArgs& a0, int z) {
+  EfArgs a = a0;
+  const long o = (long)z * a0.zs;
+  a.Ck = (const float*)((const char*)a0.Ck + o);
+  a.Et = (const float*)((const char*)a0.Et + o);
+  a.Wt = (float*)((char*)a0.Wt + o);
+  a.crow = (const int*)((const char*)a0.crow + o);
+  return a;
+}
 
 // One stage (K half h) of tile (e0, i0) into LDS: 8 DMA of A (2 k-rows of 512 B each), 8 of B.
 // k rows past bs come from a zero chunk (their MFMA steps are then exact no-ops); columns past
@@ -169,7 +182,8 @@ struct EfNoIO {
 // before the first tile (stores dropped, counts unchanged).
 struct EfIO {
   const EfArgs& a;
-  __amdgpu_buffer_rsrc_t rc;
+  __amdgpu_buffer_rsrc_t rc;   // this tile's Wt (old values)
+  __amdgpu_buffer_rsrc_t prc;  // the previous tile's Wt (its results), possibly another linear's
   const int (&prow)[2];
   int pi0;
   const int (&wrow)[2];
@@ -181,7 +195,7 @@ struct EfIO {
   PT2Q_DEV void at() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
-      __builtin_amdgcn_raw_buffer_store_b128(pend[j], rc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
       c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
     }
   }
@@ -197,18 +211,24 @@ PT2Q_DEV void ef_vmcnt(int n) {
   }
 }
 
-__global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
+__global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  const int total = a0.ntile * a0.nz;
   int t = blockIdx.x;
-  if (t >= a.ntile) return;
-  auto corner = [&](int t, int& e0, int& i0) {
-    e0 = (t / a.ti) * EF_T;
-    i0 = (t % a.ti) * EF_T;
+  if (t >= total) return;
+  // tile t of the work line: linear t / ntile, corner (e0, i0) of its output
+  auto corner = [&](int t, EfArgs& a, int& e0, int& i0) {
+    const int z = t / a0.ntile, tl = t - z * a0.ntile;
+    a = ef_linear(a0, z);
+    e0 = (tl / a0.ti) * EF_T;
+    i0 = (tl % a0.ti) * EF_T;
   };
+  auto rsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000); };
+  EfArgs a;
   int e0, i0, wrow[2];
-  corner(t, e0, i0);
+  corner(t, a, e0, i0);
+  __amdgpu_buffer_rsrc_t rc = rsrc(a), prc = rc;
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   ef_rows(a, e0, wrow);
@@ -223,9 +243,10 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
   const int S1 = a.nh == 2 ? EF_DMA : 0;
   for (;;) {
     const int tn = t + (int)gridDim.x;
-    const bool more = tn < a.ntile;
+    const bool more = tn < total;
     int en = 0, in = 0, nrow[2] = {-1, -1};
-    if (more) corner(tn, en, in);
+    EfArgs an = a;
+    if (more) corner(tn, an, en, in);
     EfAcc F;
 #pragma unroll
     for (int rm = 0; rm < 2; ++rm)
@@ -233,20 +254,20 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
       for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
     ef_vmcnt(S1);  // stage 0 landed (younger: stage 1)
     asm volatile("s_barrier" ::: "memory");
-    if (more) ef_rows(a, en, nrow);
+    if (more) ef_rows(an, en, nrow);
     {
-      EfIO io{a, rc, prow, pi0, wrow, i0, pend, c};
+      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c};
       F.half(lds0, io);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
-    if (more) ef_stage(a, en, in, 0, smem);
+    if (more) ef_stage(an, en, in, 0, smem);
     if (a.nh == 2) {
       ef_vmcnt(2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
       asm volatile("s_barrier" ::: "memory");
       EfNoIO nio;
       F.half(lds0 + EF_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (more) ef_stage(a, en, in, 1, smem + EF_STAGE);
+      if (more) ef_stage(an, en, in, 1, smem + EF_STAGE);
     }
     ef_vmcnt(more ? EF_DMA + S1 : 0);  // the old values landed (younger: the next tile's stages)
 #pragma unroll
@@ -263,8 +284,11 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
     prow[0] = wrow[0];
     prow[1] = wrow[1];
     pi0 = i0;
+    prc = rc;
     if (!more) break;
     t = tn;
+    a = an;
+    rc = rsrc(a);
     e0 = en;
     i0 = in;
     wrow[0] = nrow[0];
@@ -272,7 +296,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
   }
 #pragma unroll
   for (int j = 0; j < EF_CV; ++j)
-    __builtin_amdgcn_raw_buffer_store_b128(pend[j], rc, ef_coff(a, prow, pi0, j >> 3, (j >> 2) & 1, j & 3), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, j >> 3, (j >> 2) & 1, j & 3), 0, 0);
 }
 
 }  // namespace
@@ -280,17 +304,18 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a, long wt_bytes) {
 // Wt[crow[e]][i] -= sum_k Ck[k][e] * Et[k][i] for e < nr, i < ldw (the padding columns of Wt
 // beyond n are scratch), k < bs <= 128.  Wt has wt_rows rows of ldw floats.
 int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
-                   const int* crow, int nr, int bs, hipStream_t st) {
+                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp) {
   if (nr <= 0) return PT2Q_OK;
   const long wt_bytes = wt_rows * ldw * 4;
   if (bs <= 0 || bs > 2 * EF_KH || ldw % 4 || ldk % 4 || (uintptr_t)Ck % 16 || (uintptr_t)Et % 16 ||
       (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP || wt_rows > 65536)
     return PT2Q_E_UNSUPPORTED;
-  EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1};
+  EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1,
+           grp ? grp->ws : 0l, (int)grp_z(grp)};
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int grid = std::min(a.ntile, cus);
+  const int grid = std::min(a.ntile * a.nz, cus);
   hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;

@@ -3,6 +3,28 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// ---- Grouped block loops (pt2q_quantize_blocks_group): one launch per block step serves up to
+// PT2Q_GROUP_MAX linears of one shape, grid.z = linear z.  Every per-linear pointer that lives
+// in the linear's workspace slice moves by z * ws bytes; the raw Gram and the inverse Hessian
+// come from per-linear tables.  count == 0 (and blockIdx.z == 0): a plain single-linear launch.
+constexpr int PT2Q_GROUP_MAX = 16;
+struct Grp {
+  long ws;     // bytes between consecutive linears' workspace slices
+  int count;   // linears in the group (0: not a grouped launch)
+  const float* G[PT2Q_GROUP_MAX];     // raw Gram of linear z (AGA S1 source)
+  const float* Hinv[PT2Q_GROUP_MAX];  // inverse Hessian of linear z (error-feedback coefficients)
+};
+template <class T>
+__device__ __forceinline__ T* zws(T* p, long ws) {  // nullptr stays nullptr
+  return p ? (T*)((char*)p + (long)blockIdx.z * ws) : p;
+}
+inline unsigned grp_z(const Grp* g) { return g && g->count > 0 ? (unsigned)g->count : 1u; }
+inline Grp grp_or_none(const Grp* g) {
+  if (g) return *g;
+  Grp z{};
+  return z;
+}
+
 // ---- ATQ (atq.hip)
 int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
@@ -13,19 +35,21 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           // variant M, b <= 128: S1/d (into S1, d) formed inside the launch from
                           // the raw Gram G; s1sync: 2 zeroed ints
                           const float* G = nullptr, long ldg = 0, int* s1sync = nullptr,
-                          int* status = nullptr);  // status word (stall reporting), nullable
+                          int* status = nullptr,  // status word (stall reporting), nullable
+                          const Grp* grp = nullptr);
 
 // ---- SSR / selection (ssr.hip)
 // cnt (nullable): pt2q_ssr_counter_ints(n) zeroed ints -> one fused wbar launch (self-resetting)
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
-                               float* part, float* wn, float* sim, hipStream_t st, int* cnt = nullptr);
+                               float* part, float* wn, float* sim, hipStream_t st, int* cnt = nullptr,
+                               const Grp* grp = nullptr);
 inline int pt2q_ssr_counter_ints(int n) { return (n + 255) / 256 + 1; }
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
                          float* S1 = nullptr, float* d = nullptr, int* sync = nullptr,
-                         int* status = nullptr);
+                         int* status = nullptr, const Grp* grp = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
-                           int* newrem, int64_t* perm_out, hipStream_t st);
+                           int* newrem, int64_t* perm_out, hipStream_t st, const Grp* grp = nullptr);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st);
 int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, const int* rem,
@@ -57,7 +81,7 @@ struct GemmDesc {
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
 // block error feedback Wt[crow[e]][i] -= sum_k Ck[k][e] Et[k][i] (ef.hip); E_UNSUPPORTED if bs > 128
 int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
-                   const int* crow, int nr, int bs, hipStream_t st);
+                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp = nullptr);
 // two independent f32 GEMMs in one launch (either may be empty)
 // dA != nullptr: also factor the diagonal block (dp0, dp0) of dA (nb dnb) in the same launch if
 // g0's first tile is that block; *fused reports whether it did (else launch the factor).

@@ -49,8 +49,13 @@ __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, 
 // last arrivers put them back to zero.
 __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, long ldw, int n,
                                                              const int* rem, int r, float* part,
-                                                             float* wn, int* cnt) {
+                                                             float* wn, int* cnt, long zs) {
   __shared__ long rows[CHUNK];
+  Wt = zws(Wt, zs);  // grouped launch: linear blockIdx.z's slice
+  rem = zws(rem, zs);
+  part = zws(part, zs);
+  wn = zws(wn, zs);
+  cnt = zws(cnt, zs);
   __shared__ int last;
   const int c = blockIdx.x, nchunks = gridDim.x, nsl = gridDim.y;
   const int e0 = c * CHUNK, ce = min(r, e0 + CHUNK) - e0;
@@ -199,7 +204,11 @@ __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) 
 template <int NV>
 __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw, int n,
                                                       const int* rem, int r, const float* wn,
-                                                      float* sim) {
+                                                      float* sim, long zs) {
+  Wt = zws(Wt, zs);  // grouped launch: linear blockIdx.z's slice
+  rem = zws(rem, zs);
+  wn = zws(wn, zs);
+  sim = zws(sim, zs);
   const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int t = threadIdx.x & 63;
   if (e >= r) return;
@@ -425,8 +434,13 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
                                                                 int64_t* perm_out, const float* G,
                                                                 long ldg, float* S1, float* d,
                                                                 int region0, int* sync, int* status,
-                                                                long cap) {
+                                                                long cap, long zs) {
   extern __shared__ uint32_t vals[];
+  sim = zws(sim, zs);  // grouped launch (no S1 helpers): linear blockIdx.z's slice
+  rem = zws(rem, zs);
+  blk = zws(blk, zs);
+  newrem = zws(newrem, zs);
+  perm_out = zws(perm_out, zs);
   if (blockIdx.x > 0) {
     s1_helper(G, ldg, blk, b, S1, d, sync, (float*)vals, status, cap);
     return;
@@ -570,7 +584,11 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
 // Sequential block (use_ssr=False: main.py:167-169, gptq.py:135-137) or "take the rest"
 // (reorder.py:125-126 when |rem| <= b).
 __global__ void select_seq_kernel(int mode, int p0, int bs, int m, const int* rem, int* blk,
-                                  int* newrem, int64_t* perm_out) {
+                                  int* newrem, int64_t* perm_out, long zs) {
+  rem = zws(rem, zs);  // grouped launch: linear blockIdx.z's slice
+  blk = zws(blk, zs);
+  newrem = zws(newrem, zs);
+  perm_out = zws(perm_out, zs);
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < bs) {
     int j = (mode == 0) ? p0 + t : rem[t];
@@ -758,13 +776,19 @@ size_t pt2q_ssr_scratch_floats(int n, int m) {
 }
 
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
-                               float* part, float* wn, float* sim, hipStream_t st, int* cnt) {
+                               float* part, float* wn, float* sim, hipStream_t st, int* cnt,
+                               const Grp* grp) {
   if (r <= 0 || n <= 0) return PT2Q_E_ARG;
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
-  if (cnt && n <= 16384 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 && pt2q_tuning().wbar_fused) {
-    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(64), 0, st, Wt, ldw,
-                       n, rem, r, part, wn, cnt);
+  const unsigned nz = grp_z(grp);
+  const long zs = grp ? grp->ws : 0;
+  const bool fused = cnt && n <= 16384 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 &&
+                     pt2q_tuning().wbar_fused;
+  if (nz > 1 && !fused) return PT2Q_E_UNSUPPORTED;  // grouped launches use the fused w-bar only
+  if (fused) {
+    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256), nz), dim3(64), 0, st, Wt, ldw,
+                       n, rem, r, part, wn, cnt, zs);
     PT2Q_LAUNCH_CHECK();
   } else {
     hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
@@ -784,15 +808,17 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   const bool v4 = (n & 3) == 0 && (ldw & 3) == 0;
   auto sim_k = !v4 ? ssr_sim_kernel<0> : n <= 4096 ? ssr_sim_kernel<16> : n <= 12288 ? ssr_sim_kernel<48>
                                                                                    : ssr_sim_kernel<0>;
-  hipLaunchKernelGGL(sim_k, dim3(ceil_div(r, 4)), dim3(256), 0, st, Wt, ldw, n, rem, r, wn, sim);
+  hipLaunchKernelGGL(sim_k, dim3(ceil_div(r, 4), 1, nz), dim3(256), 0, st, Wt, ldw, n, rem, r, wn, sim, zs);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
 
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G, long ldg, float* S1,
-                         float* d, int* sync, int* status) {
+                         float* d, int* sync, int* status, const Grp* grp) {
   if (G && b > 128) return PT2Q_E_ARG;
+  const unsigned nz = grp_z(grp);
+  if (nz > 1 && G) return PT2Q_E_UNSUPPORTED;  // grouped: S1/d are formed in the ATQ launch
   if (b <= 0 || b > r || r >= 65536) return PT2Q_E_UNSUPPORTED;
   if (G && !sync) return PT2Q_E_ARG;  // sync: 2 ints the caller zeroed before this launch
   const int region0 = (r + 32 * TOPK_HPAD + 3) & ~3;  // >= S1_ROWS * 129 for the helpers
@@ -800,20 +826,20 @@ int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* bl
                      (size_t)b * 4 * sizeof(int);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   const int grid = G ? 1 + ceil_div(b, S1_ROWS) : 1;
-  hipLaunchKernelGGL(ssr_topk_kernel, dim3(grid), dim3(TOPK_THREADS), lds, st, sim, rem, r, b, blk,
+  hipLaunchKernelGGL(ssr_topk_kernel, dim3(grid, 1, nz), dim3(TOPK_THREADS), lds, st, sim, rem, r, b, blk,
                      newrem, perm_out, G, ldg, S1, d, region0, sync, status,
-                     pt2q_tuning().spin_cap_short);
+                     pt2q_tuning().spin_cap_short, grp ? grp->ws : 0l);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
 
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
-                           int* newrem, int64_t* perm_out, hipStream_t st) {
+                           int* newrem, int64_t* perm_out, hipStream_t st, const Grp* grp) {
   int work = (mode == 0) ? (m - p0) : bs;
   int grid = ceil_div(work > 0 ? work : 1, 256);
   if (grid > 64) grid = 64;
-  hipLaunchKernelGGL(select_seq_kernel, dim3(grid), dim3(256), 0, st, mode, p0, bs, m, rem, blk,
-                     newrem, perm_out);
+  hipLaunchKernelGGL(select_seq_kernel, dim3(grid, 1, grp_z(grp)), dim3(256), 0, st, mode, p0, bs, m, rem,
+                     blk, newrem, perm_out, grp ? grp->ws : 0l);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

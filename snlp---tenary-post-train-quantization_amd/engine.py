@@ -135,6 +135,55 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: torch.Tens
     return LayerOutput(alpha, mu, T, perm, iters)
 
 
+GROUP_MAX = 16  # linears per pt2q_quantize_blocks_group call (PT2Q_GROUP_MAX)
+
+
+def group_supported(n: int, m: int, block_size: int, flags: int = _lib.FLAG_SSR | _lib.AGA_ACT) -> bool:
+    """Whether pt2q_quantize_blocks_group takes linears of this shape (else per-linear loops)."""
+    return (block_size <= 128 and block_size < m and m < 65536 and n <= 16384 and n % 4 == 0
+            and (flags & _lib.AGA_MASK) in (_lib.AGA_ACT, _lib.AGA_NONE))
+
+
+def quantize_blocks_group(Ws, As, Hinvs, block_size: int = 128, use_ssr: bool = True,
+                          aga: int = _lib.AGA_ACT, max_iter: int = 100, t_dtype=torch.int8,
+                          workspace: Optional[torch.Tensor] = None, outs=None, check: bool = True):
+    """The block loops of several linears of one shape (n x m) in one launch sequence
+    (pt2q_quantize_blocks_group): linear z is W = Ws[z] with AGA matrix As[z] (raw Gram, variant
+    M) and inverse Hessian Hinvs[z]; each result is bit-identical to
+    quantize_blocks(Ws[z], As[z], Hinvs[z]).  Up to GROUP_MAX linears per call.  check=False
+    leaves the status word to the caller (_lib.check_status(workspace))."""
+    Ws = [_float_input(W) for W in Ws]
+    count = len(Ws)
+    if not 1 <= count <= GROUP_MAX:
+        raise ValueError(f"quantize_blocks_group: 1..{GROUP_MAX} linears (got {count})")
+    n, m = Ws[0].shape
+    dev = Ws[0].device
+    if any(W.shape != (n, m) or W.dtype != Ws[0].dtype for W in Ws):
+        raise ValueError("quantize_blocks_group: every W must have the same shape and dtype")
+    B = num_blocks(m, block_size)
+    flags = (_lib.FLAG_SSR if use_ssr else 0) | aga
+    Hinvs = [H.contiguous().float() for H in Hinvs]
+    As = [None if A is None else A.contiguous().float() for A in As] if As is not None else [None] * count
+    if outs is None:
+        outs = [LayerOutput(torch.empty((n, B), dtype=torch.float32, device=dev),
+                            torch.empty((n, B), dtype=torch.float32, device=dev),
+                            torch.empty((n, m), dtype=t_dtype, device=dev),
+                            torch.empty(m, dtype=torch.int64, device=dev),
+                            torch.zeros(B, dtype=torch.int32, device=dev)) for _ in range(count)]
+    nbytes = _lib.lib().pt2q_quantize_blocks_group_workspace_bytes(count, n, m, int(block_size), flags)
+    ws = workspace if workspace is not None and workspace.numel() >= nbytes else _lib.workspace(nbytes, dev)
+    arrs = [_lib.ptr_array(x) for x in (Ws, As, Hinvs, [o.alpha for o in outs], [o.mu for o in outs],
+                                        [o.T for o in outs], [o.perm for o in outs], [o.iters for o in outs])]
+    p = [a[0] for a in arrs]
+    rc = _lib.lib().pt2q_quantize_blocks_group(
+        count, p[0], _lib.dtype_code(Ws[0]), m, n, m, int(block_size), flags, p[1], m, p[2], m, int(max_iter),
+        p[3], p[4], p[5], _lib.dtype_code(outs[0].T), p[6], p[7], _lib.ptr(ws), ws.numel(), _lib.stream_of(dev))
+    _lib.check(rc, "pt2q_quantize_blocks_group")
+    if check:
+        _lib.check_status(ws, "pt2q_quantize_blocks_group")
+    return outs
+
+
 def hessian_inverse(G: torch.Tensor, nsamples: int, percdamp: float = 0.01):
     """main.py:129-141 on a raw Gram: damped H, then Hinv (pinv on Cholesky breakdown).
     Returns (Hinv, spd)."""

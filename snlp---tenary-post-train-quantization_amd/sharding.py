@@ -53,6 +53,13 @@ _GRAM_RATE, _CHOL_RATE, _CHOL_STEP = 1.05e15, 1.0e14, 25e-6
 _BLOCK_FIXED, _BLOCK_NR = 30e-6, 7.5e-12
 
 
+def block_loop_cost(n: int, m: int, block_size: int = 128) -> float:
+    """Modelled seconds of one n x m linear's block loop (see unit_cost)."""
+    nblk = -(-m // block_size) if block_size < m else 1
+    rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))  # remaining columns per block
+    return nblk * _BLOCK_FIXED + float(n) * rsum * _BLOCK_NR
+
+
 def unit_cost(unit, block_size: int = 128) -> float:
     """Modelled seconds of one work unit on one MI355X (its Gram, Cholesky inverse and every
     linear's block loop).  LPT balances ranks on this; a pure flop count (N·m² dominates) would
@@ -60,10 +67,8 @@ def unit_cost(unit, block_size: int = 128) -> float:
     _, linears, N = unit
     m = linears[0][2]
     t = float(N) * m * m / _GRAM_RATE + float(m) ** 3 / _CHOL_RATE + (m / 64.0) * _CHOL_STEP
-    nblk = -(-m // block_size) if block_size < m else 1
-    rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))  # remaining columns per block
     for _, n, _ in linears:
-        t += nblk * _BLOCK_FIXED + float(n) * rsum * _BLOCK_NR
+        t += block_loop_cost(n, m, block_size)
     return t
 
 
@@ -199,11 +204,14 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
             grams_first.gram(i, inputs[i][0])
         if hasattr(grams_first, "inverses"):
             grams_first.inverses()
-        for i in mine:
-            name, lins, N = units[i]
-            Wd = inputs[i][1]
-            runs.append((name, [p for p, _, _ in lins],
-                         grams_first.tail(i, [Wd[p] for p, _, _ in lins], N)))
+        jobs = [(i, [inputs[i][1][p] for p, _, _ in units[i][1]], units[i][2]) for i in mine]
+        if getattr(grams_first, "grouped", False):
+            tails = grams_first.tails(jobs)  # block loops grouped across units by shape
+        else:
+            tails = [grams_first.tail(i, Ws, N) for i, Ws, N in jobs]
+        for i, run in zip(mine, tails):
+            name, lins, _ = units[i]
+            runs.append((name, [p for p, _, _ in lins], run))
     for i in ([] if grams_first is not None else mine):
         name, lins, _ = units[i]
         X, Wd = provider(units[i])
@@ -302,10 +310,16 @@ class GramsFirst:
     its status word first, so after each Gram its word is OR-ed (on the stream) into one
     per-step device word; check() reads that word once and clears it."""
 
-    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01):
+    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01,
+                 group: int = 16):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         self.batched, self.chunk, self.percdamp = batched, chunk, percdamp
+        # step 3 grouped: the block loops of up to `group` same-shape linears (across units) per
+        # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
+        self.group = group if batched else 0
+        self.grouped = self.group > 1
+        self.gws = {}
         self.G, self.ws = {}, {}
         self.slot = {}       # key -> (group, index)
         self.groups = {}     # (m, N) -> {"G", "Hinv", "info"} packed over the group's units
@@ -367,8 +381,111 @@ class GramsFirst:
             return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples)
         return self.pipe.run(Ws, G=self.G[key], nsamples=nsamples)
 
+    def tails(self, jobs):
+        """Step 3, grouped: jobs [(key, [W], nsamples)] in unit order.  Every linear whose shape
+        the grouped entry takes joins a group of same-shape, same-dtype linears (in job order, at
+        most `group` per group); groups go round-robin onto the pipeline's lanes.  Returns one
+        run per job (finish() -> [LayerOutput]); results are bit-identical to tail()."""
+        eng, lib = self.engine, self.lib
+        bs, ssr, mi = self.pipe.bs, self.pipe.use_ssr, self.pipe.max_iter
+        flags = (lib.FLAG_SSR if ssr else 0) | lib.AGA_ACT
+        state = _GroupState(self)
+        runs = []
+        classes = {}
+        for j, (key, Ws, N) in enumerate(jobs):
+            g, z = self.slot[key]
+            grp = self.groups[g]
+            Ws = [eng._float_input(W) for W in Ws]
+            run = _GroupedRun(state, key, Ws, grp["G"][z], N, grp["info"][z:z + 1])
+            runs.append(run)
+            for k, W in enumerate(Ws):
+                n, m = W.shape
+                if eng.group_supported(n, m, bs, flags):
+                    classes.setdefault((n, m, W.dtype), []).append((run, k, W, grp["G"][z], grp["Hinv"][z]))
+                else:  # a lone linear of an unsupported shape: its own loop on the next lane
+                    classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], grp["Hinv"][z]))
+        caller = torch.cuda.current_stream(self.dev)
+        lanes = self.pipe.lanes
+        # groups: at most `group` linears, and small enough that every lane gets work; issued
+        # longest first onto the least-loaded lane (LPT on the block-loop cost model)
+        plan = []
+        for ckey, items in classes.items():
+            size = max(1, min(self.group, -(-len(items) // len(lanes))))
+            for c0 in range(0, len(items), size):
+                chunk = items[c0:c0 + size]
+                n, m = chunk[0][2].shape
+                plan.append((len(chunk) * block_loop_cost(n, m, bs), ckey, chunk))
+        plan.sort(key=lambda x: -x[0])
+        load = [0.0] * len(lanes)
+        for cost, ckey, chunk in plan:
+            li = min(range(len(lanes)), key=lambda i: (load[i], i))
+            load[li] += cost
+            ln = lanes[li]
+            ln.stream.wait_stream(caller)
+            with torch.cuda.stream(ln.stream):
+                if ckey[0] == "one":
+                    run, k, W, G, H = chunk[0]
+                    out = eng.quantize_blocks(W, G, H, bs, ssr, lib.AGA_ACT, mi)  # checks its status
+                    run.outs[k] = out
+                    continue
+                n, m, _ = ckey
+                wkey = (id(ln), n, m)
+                nbytes = lib.lib().pt2q_quantize_blocks_group_workspace_bytes(len(chunk), n, m, bs, flags)
+                if wkey not in self.gws or self.gws[wkey].numel() < nbytes:
+                    self.gws[wkey] = lib.workspace(
+                        lib.lib().pt2q_quantize_blocks_group_workspace_bytes(self.group, n, m, bs, flags), self.dev)
+                ws = self.gws[wkey]
+                outs = eng.quantize_blocks_group([c[2] for c in chunk], [c[3] for c in chunk],
+                                                 [c[4] for c in chunk], bs, ssr, lib.AGA_ACT, mi,
+                                                 workspace=ws, check=False)
+                state.statuses.append(lib.status_view(ws).clone())
+                for (run, k, _, _, _), out in zip(chunk, outs):
+                    run.outs[k] = out
+        state.join = lambda: [caller.wait_stream(ln.stream) for ln in lanes]
+        return runs
+
     def check(self):
         """Raise if any Gram since the last check stalled in a stream-K hand-off (one host read)."""
         status = int(self.stall.item())
         self.stall.zero_()
         self.lib.raise_stall(status, "pt2q_gram")
+
+
+class _GroupState:
+    """The device words of one grouped tail phase, read once by the first finish()."""
+
+    def __init__(self, gf):
+        self.gf, self.statuses, self.join, self.read = gf, [], None, None
+
+
+class _GroupedRun:
+    """One unit's outputs from GramsFirst.tails: finish() joins the lanes, reads every group's
+    stall word and every unit's Cholesky status once (the first call), and re-runs this unit
+    with pinv (main.py:140-141) if its Hessian was not positive definite."""
+
+    def __init__(self, state, key, Ws, G, nsamples, info):
+        self.state, self.key, self.Ws, self.G, self.N, self.info = state, key, Ws, G, nsamples, info
+        self.outs = [None] * len(Ws)
+        self.spd = None
+
+    def finish(self):
+        if self.spd is not None:
+            return self.outs
+        st = self.state
+        if st.read is None:
+            if st.join is not None:
+                st.join()
+            words = torch.cat([s.reshape(1) for s in st.statuses]).cpu().tolist() if st.statuses else []
+            for v in words:
+                st.gf.lib.raise_stall(int(v), "pt2q_quantize_blocks_group")
+            st.read = True
+        self.spd = int(self.info.item()) == 0
+        if not self.spd:
+            eng, pipe = self.state.gf.engine, self.state.gf.pipe
+            H, _ = eng.prepare_hessian(self.G, self.N, pipe.percdamp)
+            Hinv = torch.linalg.pinv(H)
+            self.outs = [eng.quantize_blocks(W, self.G, Hinv, pipe.bs, pipe.use_ssr, eng._lib.AGA_ACT,
+                                             pipe.max_iter) for W in self.Ws]
+        for o in self.outs:
+            o.spd = self.spd
+        return self.outs

@@ -555,3 +555,28 @@ def test_reference_call_shapes_with_cpu_tensors(pt2q):
     np.testing.assert_array_equal(perm.numpy(), ref["perm"])
     np.testing.assert_array_equal(T.numpy(), ref["T"])
     assert gq.get_quantized_weight().device.type == "cpu"
+
+
+@pytest.mark.parametrize("n,m,count,ssr,dt", [(256, 512, 3, True, torch.float32), (384, 700, 5, True, torch.float16),
+                                             (512, 384, 2, False, torch.float32), (1024, 1024, 16, True, torch.float16),
+                                             (4096, 4096, 3, True, torch.float16)])
+def test_blocks_group_equals_per_linear(pt2q, n, m, count, ssr, dt):
+    """pt2q_quantize_blocks_group (one launch per block step for all linears, grid.z = linear)
+    == quantize_blocks on each linear alone, bit for bit: every linear has its own W, raw Gram
+    and H^-1 (and some share them, as q/k/v do); ragged m, fp16 weights, sequential blocks, and a
+    full group of 16."""
+    Ws, Gs, Hs = [], [], []
+    for z in range(count):
+        X = pt2q.fill_synthetic((2 * m + 64 * z, m), 300 + 7 * z, outliers=True, device="cuda").half()
+        G = pt2q.gram(X) if z % 3 != 2 else Gs[-1]  # every third linear shares its input's Gram
+        Hinv, spd = pt2q.hessian_inverse(G, X.shape[0]) if z % 3 != 2 else (Hs[-1], True)
+        assert spd
+        Gs.append(G)
+        Hs.append(Hinv)
+        Ws.append(pt2q.fill_synthetic((n, m), 900 + z, std=0.02, device="cuda").to(dt))
+    got = pt2q.engine.quantize_blocks_group(Ws, Gs, Hs, 128, ssr)
+    for z in range(count):
+        want = pt2q.quantize_blocks(Ws[z], Gs[z], Hs[z], 128, ssr)
+        for a, b in ((got[z].perm, want.perm), (got[z].T, want.T), (got[z].alpha, want.alpha),
+                     (got[z].mu, want.mu), (got[z].iters, want.iters)):
+            assert bits_equal(host(a), host(b)), z

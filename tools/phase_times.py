@@ -34,10 +34,8 @@ def step(timed):
     torch.cuda.synchronize()
     t["inverse"] = time.perf_counter() - t1
     t2 = time.perf_counter()
-    runs = []
-    for i in mine:
-        name, lins, N = units[i]
-        runs.append(gf.tail(i, [inputs[i][1][p] for p, _, _ in lins], N))
+    jobs = [(i, [inputs[i][1][p] for p, _, _ in units[i][1]], units[i][2]) for i in mine]
+    runs = gf.tails(jobs) if gf.grouped else [gf.tail(i, Ws, N) for i, Ws, N in jobs]
     for r in runs:
         r.finish()
     torch.cuda.synchronize()
