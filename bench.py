@@ -305,6 +305,99 @@ class ModelStep:
                                                  pack=True, dst=0, grams_first=gf)
         return res
 
+    def phase_step(self):
+        """One grams-first step of this rank's units with a device synchronisation between the
+        three phases (Grams; batched Hessian inverses; block loops) -> wall seconds of each.
+        Outside the timed region (the syncs add a little idle time)."""
+        gf, units = self.gf, self.units
+        t = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        inputs = {i: self.provider(units[i]) for i in self.mine}
+        gf.begin([(i, units[i][1][0][2], units[i][2]) for i in self.mine])
+        for i in self.mine:
+            gf.gram(i, inputs[i][0])
+        torch.cuda.synchronize()
+        t["gram"] = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        gf.inverses()
+        torch.cuda.synchronize()
+        t["inverse"] = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        jobs = [(i, [inputs[i][1][p] for p, _, _ in units[i][1]], units[i][2]) for i in self.mine]
+        runs = gf.tails(jobs) if gf.grouped else [gf.tail(i, Ws, N) for i, Ws, N in jobs]
+        for r in runs:
+            r.finish()
+        torch.cuda.synchronize()
+        t["tails"] = time.perf_counter() - t2
+        gf.check()
+        return t
+
+
+# ------------------------------------------------------------------ stage rooflines
+
+TAIL_STAGE = (("ef_gemm", "ef"), ("ssr_", "ssr"), ("atq_", "atq"))
+
+
+def model_work(units, bs):
+    """Algorithmic work of one model step per stage: flops and HBM bytes."""
+    w = {k: 0.0 for k in ("gram_fl_2nm2", "gram_fl_done", "gram_bytes", "chol_fl", "ef_fl", "ef_bytes",
+                          "ssr_bytes", "atq_bytes")}
+    for _, lins, N in units:
+        m = lins[0][2]
+        w["gram_fl_2nm2"] += 2.0 * N * m * m          # §8(d) basis: the full product
+        w["gram_fl_done"] += float(N) * m * (m + 1)    # the symmetric half actually formed
+        w["gram_bytes"] += 2.0 * N * m                 # X read once (fp16)
+        w["chol_fl"] += float(m) ** 3                  # potrf + trtri + lauum, m^3/3 each
+        nblk = -(-m // bs) if bs < m else 1
+        rsum = sum(max(m - (k + 1) * bs, 0) for k in range(nblk))
+        for _, n, _ in lins:
+            w["ef_fl"] += 2.0 * n * bs * rsum          # W[:, rem] -= E C, K = b
+            w["ef_bytes"] += 8.0 * n * rsum            # read + write of W[:, rem] (fp32)
+            w["ssr_bytes"] += 8.0 * n * rsum           # w-bar pass + similarity pass over W[:, rem]
+            w["atq_bytes"] += 9.0 * n * m              # W block read, codes + error term written
+    return w
+
+
+def stage_roofline(work, phase_s, kern, ms_per_step, world):
+    """roofline.stages: every stage's algorithmic work per step against its peak.  gram /
+    cholesky / tails: live phase walls (bench.py phase_step); ef / ssr / atq: their kernel-busy
+    time in the tail phase of the committed rocprof trace (profiles/stage_kernels.json,
+    tools/phase_trace.sh), which the lanes overlap."""
+    F32, F16, HBM = MI355X_F32_MFMA_PEAK_TFLOPS * 1e12, MI355X_F16_MFMA_PEAK_TFLOPS * 1e12, MI355X_HBM_PEAK_GBS * 1e9
+    st = {}
+    g = phase_s["gram"]
+    st["gram"] = {"bound": "mfma", "seconds": g, "source": "live phase wall",
+                  "flops_2nm2": work["gram_fl_2nm2"], "frac_2nm2": work["gram_fl_2nm2"] / g / F16,
+                  "flops_done": work["gram_fl_done"], "frac_done": work["gram_fl_done"] / g / F16,
+                  "hbm_frac": work["gram_bytes"] / g / HBM}
+    c = phase_s["inverse"]
+    st["cholesky_inverse"] = {"bound": "mfma", "seconds": c, "source": "live phase wall (batched per width)",
+                              "flops": work["chol_fl"], "frac": work["chol_fl"] / c / F32}
+    st["tails"] = {"seconds": phase_s["tails"], "source": "live phase wall (grouped block loops on the lanes)"}
+    if kern and "tails" in kern:
+        busy = {"ef": 0.0, "ssr": 0.0, "atq": 0.0}
+        for name, (ms, _) in kern["tails"]["kernels"].items():
+            for pre, stage in TAIL_STAGE:
+                if name.startswith(pre):
+                    busy[stage] += ms / 1e3
+        if busy["ef"] > 0:
+            st["ef"] = {"bound": "mfma+hbm", "kernel_busy_s": busy["ef"], "flops": work["ef_fl"],
+                        "frac_mfma": work["ef_fl"] / busy["ef"] / F32, "bytes": work["ef_bytes"],
+                        "frac_hbm": work["ef_bytes"] / busy["ef"] / HBM, "source": kern.get("source")}
+        if busy["ssr"] > 0:
+            st["ssr"] = {"bound": "hbm", "kernel_busy_s": busy["ssr"], "bytes": work["ssr_bytes"],
+                         "frac_hbm": work["ssr_bytes"] / busy["ssr"] / HBM, "source": kern.get("source")}
+        if busy["atq"] > 0:
+            st["atq"] = {"bound": "hbm/latency", "kernel_busy_s": busy["atq"], "bytes": work["atq_bytes"],
+                         "frac_hbm": work["atq_bytes"] / busy["atq"] / HBM, "source": kern.get("source")}
+    floor = (work["gram_fl_done"] / F16 + work["chol_fl"] / F32 + work["ef_fl"] / F32 +
+             (work["ef_bytes"] + work["ssr_bytes"] + work["atq_bytes"]) / HBM) / max(world, 1)
+    st["step"] = {"floor_s": floor, "frac": floor / (ms_per_step * 1e-3),
+                  "floor": "Gram work done at the 16-bit MFMA peak + Cholesky inverse and EF flops at the "
+                           "f32 MFMA peak + EF/SSR/ATQ bytes at HBM peak, stages back to back, / ranks"}
+    return st
+
 
 class LayerStep:
     """One n x m layer per rank (weak scaling), a hipGraph replay; results gathered at N > 1."""
@@ -530,11 +623,25 @@ def main(argv=None):
                  "gram16x_kernel (m=4096: 128x256 tiles) / gram16w_kernel (m=11008: 256x256 tiles): "
                  "symmetric Gram XᵀX, LDS-DMA ring, ds_read_b64_tr_b16, hand-interleaved 16-bit MFMA "
                  "32x32x16, f32 accumulate")
+        fl_2nm2 = sum(cnt * 2.0 * N * m * m for m, cnt in mix.items()) / launches
         roof = {"bound": "mfma", "kernel": kname, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": None, "avg_launch_ms": avg_ms,
-                "flops_per_launch": avg_fl, "per_width": per_m,
+                "frac": achieved / peak, "frac_basis": "work done: N*m*(m+1) flops per launch (the symmetric "
+                                                      "half the kernel forms)",
+                "frac_2nm2": fl_2nm2 / (avg_ms * 1e-3) / 1e12 / peak,
+                "traffic": None, "avg_launch_ms": avg_ms,
+                "flops_per_launch": avg_fl, "flops_per_launch_2nm2": fl_2nm2, "per_width": per_m,
                 "gram_share_of_step": tot_ms / (ms_per_step * max(world, 1)) if a.workload == "model" else
                 avg_ms / ms_per_step}
+        if a.workload == "model" and work.gf is not None and a.schedule == "grams-first" and world == 1:
+            work.phase_step()
+            ph = work.phase_step()
+            kern = None
+            kp = os.path.join(ROOT, "profiles", "stage_kernels.json")
+            if os.path.exists(kp):
+                with open(kp) as f:
+                    kern = json.load(f)
+            roof["phase_s"] = ph
+            roof["stages"] = stage_roofline(model_work(work.units, bs), ph, kern, ms_per_step, world)
         tr = load_traffic()
         if tr and "per_width" in tr and all(str(m) in tr["per_width"] for m in mix):
             # PMC fabric bytes per launch of each width, averaged over the step's launch mix

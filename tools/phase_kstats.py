@@ -15,6 +15,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--top", type=int, default=15)
+    ap.add_argument("--json", default=None, help="also write {phase: {span_ms, busy_ms, kernels: {name: "
+                                                 "[ms, launches]}}} here (bench.py's stage roofline reads it)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -35,6 +37,7 @@ def main():
     lastg = max(i for i, r in enumerate(rows) if isg(r))
     firstl = min(i for i, r in enumerate(rows) if i > lastg and any(k in r["Kernel_Name"] for k in LOOP))
     phases = {"gram": rows[:lastg + 1], "inverse": rows[lastg + 1:firstl], "tails": rows[firstl:]}
+    out = {"source": a.csv}
     for ph, rs in phases.items():
         if not rs:
             continue
@@ -47,8 +50,14 @@ def main():
             busy += d
         span = (max(int(r["End_Timestamp"]) for r in rs) - int(rs[0]["Start_Timestamp"])) / 1e3
         print(f"== {ph}: launches {len(rs)}  span {span / 1e3:.2f} ms  kernel-busy {busy / 1e3:.2f} ms")
+        out[ph] = {"span_ms": span / 1e3, "busy_ms": busy / 1e3, "launches": len(rs),
+                   "kernels": {k: [v / 1e3, cnt[k]] for k, v in tot.items()}}
         for k, v in sorted(tot.items(), key=lambda x: -x[1])[:a.top]:
             print(f"{v / 1e3:10.3f} ms {cnt[k]:7d}x avg {v / cnt[k]:9.2f} us  {k}")
+    if a.json:
+        import json
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -10,5 +10,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output
   python3 $R/tools/phase_times.py "$@" > $OUT/phase.txt 2> $OUT/err || exit 1
 cat $OUT/phase.txt
 f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
-python3 $R/tools/phase_kstats.py $f > $OUT/phase_kstats.txt && cat $OUT/phase_kstats.txt
+python3 $R/tools/phase_kstats.py $f --json $OUT/stage_kernels.json > $OUT/phase_kstats.txt && cat $OUT/phase_kstats.txt
 gzip -f $f
