@@ -82,6 +82,9 @@ def parse(argv=None):
     p.add_argument("--no-batched-inverse", action="store_true",
                    help="model workload, grams-first: each unit's Cholesky inverse on its lane instead of "
                         "batched per width (engine.hessian_inverse_batched)")
+    p.add_argument("--inverse-overlap", action="store_true",
+                   help="model workload: each width's block loops start once its own batched inverses "
+                        "are done, beside the other widths' inverses (default: all inverses first)")
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
@@ -272,7 +275,8 @@ class ModelStep:
         self.bs, self.ssr = a.block_size, not a.no_ssr
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.schedule = a.schedule
-        self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group)
+        self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group,
+                                       overlap=a.inverse_overlap)
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.index = {u[0]: i for i, u in enumerate(self.units)}

@@ -311,7 +311,7 @@ class GramsFirst:
     per-step device word; check() reads that word once and clears it."""
 
     def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01,
-                 group: int = 16):
+                 group: int = 16, overlap: bool = False):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         self.batched, self.chunk, self.percdamp = batched, chunk, percdamp
@@ -320,6 +320,13 @@ class GramsFirst:
         self.group = group if batched else 0
         self.grouped = self.group > 1
         self.gws = {}
+        # overlap=True: the batched inverses run on a stream of their own, one event per (m, N)
+        # group, and a unit's block loops wait only for its own width's inverses, so the narrow
+        # units' loops overlap the wide units' inverses (measured slower on the 7B step, 2.816
+        # vs 2.771 s: both phases fill the CUs)
+        self.inv_stream = (torch.cuda.Stream(self.dev, priority=-1) if batched and overlap and self.dev.type == "cuda"
+                           else None)
+        self.inv_done = {}
         self.G, self.ws = {}, {}
         self.slot = {}       # key -> (group, index)
         self.groups = {}     # (m, N) -> {"G", "Hinv", "info"} packed over the group's units
@@ -364,18 +371,41 @@ class GramsFirst:
         torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
 
     def inverses(self):
-        """Step 2: every group's Hessian inverses, batched (no-op with batched=False)."""
+        """Step 2: every group's Hessian inverses, batched (no-op with batched=False), narrowest
+        width first, on the inverse stream; each group records its event."""
         if not self.batched:
             return
-        for (m, N), grp in self.groups.items():
-            self.engine.hessian_inverse_batched(grp["G"], N, self.percdamp, Hinv=grp["Hinv"], info=grp["info"],
-                                                scratch=self.scratch, chunk=self.chunk)
+        caller = torch.cuda.current_stream(self.dev)
+        self.inv_done = {}
+        if self.inv_stream is None:  # no overlap: on the caller's stream, before any tail
+            for g in sorted(self.groups):
+                grp = self.groups[g]
+                self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
+                                                    info=grp["info"], scratch=self.scratch, chunk=self.chunk)
+            return
+        self.inv_stream.wait_stream(caller)  # the Grams
+        with torch.cuda.stream(self.inv_stream):
+            for g in sorted(self.groups):
+                grp = self.groups[g]
+                self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
+                                                    info=grp["info"], scratch=self.scratch, chunk=self.chunk)
+                ev = torch.cuda.Event()
+                ev.record(self.inv_stream)
+                self.inv_done[g] = ev
+
+    def _wait_inverse(self, stream, key):
+        """`stream` waits for the inverses of `key`'s group (batched schedule)."""
+        if self.batched and key in self.slot:
+            ev = self.inv_done.get(self.slot[key][0])
+            if ev is not None:
+                stream.wait_event(ev)
 
     def tail(self, key, Ws, nsamples):
         if key in self.slot:
             g, z = self.slot[key]
             grp = self.groups[g]
             if self.batched:
+                self._wait_inverse(torch.cuda.current_stream(self.dev), key)
                 return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples, Hinv=grp["Hinv"][z],
                                      info=grp["info"][z:z + 1])
             return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples)
@@ -422,6 +452,8 @@ class GramsFirst:
             load[li] += cost
             ln = lanes[li]
             ln.stream.wait_stream(caller)
+            for key in {c[0].key for c in chunk}:
+                self._wait_inverse(ln.stream, key)
             with torch.cuda.stream(ln.stream):
                 if ckey[0] == "one":
                     run, k, W, G, H = chunk[0]
@@ -441,7 +473,8 @@ class GramsFirst:
                 state.statuses.append(lib.status_view(ws).clone())
                 for (run, k, _, _, _), out in zip(chunk, outs):
                     run.outs[k] = out
-        state.join = lambda: [caller.wait_stream(ln.stream) for ln in lanes]
+        state.join = lambda: [caller.wait_stream(x) for x in [ln.stream for ln in lanes] +
+                              ([self.inv_stream] if self.inv_stream is not None else [])]
         return runs
 
     def check(self):

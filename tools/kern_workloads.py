@@ -1,0 +1,30 @@
+"""PMC workloads (dev tool): python tools/kern_workloads.py {inverse M BATCH | group N M COUNT} [reps]
+inverse: engine.hessian_inverse_batched on BATCH synthetic Grams of order M (N = 262144 scale);
+group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M)."""
+import os
+import sys
+import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pt2q_loader
+pt2q = pt2q_loader.load()
+kind = sys.argv[1]
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+if kind == "inverse":
+    m, batch = int(sys.argv[2]), int(sys.argv[3])
+    X = pt2q.fill_synthetic((4 * m, m), 77, outliers=True).half()
+    G1 = pt2q.gram(X)
+    G = G1.expand(batch, m, m).contiguous()
+    for _ in range(reps):
+        Hinv, info = pt2q.engine.hessian_inverse_batched(G, 4 * m, chunk=batch)
+    torch.cuda.synchronize()
+    print("inverse done", int(info.max()))
+else:
+    n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    X = pt2q.fill_synthetic((4 * m, m), 78, outliers=True).half()
+    G = pt2q.gram(X)
+    Hinv, spd = pt2q.hessian_inverse(G, 4 * m)
+    Ws = [pt2q.fill_synthetic((n, m), 900 + z, std=0.02).half() for z in range(count)]
+    for _ in range(reps):
+        outs = pt2q.engine.quantize_blocks_group(Ws, [G] * count, [Hinv] * count)
+    torch.cuda.synchronize()
+    print("group done", spd)
