@@ -366,8 +366,9 @@ def model_work(units, bs):
 def stage_roofline(work, phase_s, kern, ms_per_step, world):
     """roofline.stages: every stage's algorithmic work per step against its peak.  gram /
     cholesky / tails: live phase walls (bench.py phase_step); ef / ssr / atq: their kernel-busy
-    time in the tail phase of the committed rocprof trace (profiles/stage_kernels.json,
-    tools/phase_trace.sh), which the lanes overlap."""
+    time in the tail phase of the committed rocprof trace of one step with the block loops on ONE
+    lane (profiles/stage_kernels.json, tools/round_r03.sh -> tools/phase_trace.sh --lanes 1), so
+    each kernel's time is its own, not stretched by co-running lanes."""
     F32, F16, HBM = MI355X_F32_MFMA_PEAK_TFLOPS * 1e12, MI355X_F16_MFMA_PEAK_TFLOPS * 1e12, MI355X_HBM_PEAK_GBS * 1e9
     st = {}
     g = phase_s["gram"]

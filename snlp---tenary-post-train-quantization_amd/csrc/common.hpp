@@ -109,7 +109,8 @@ struct Pt2qTuning {
   bool chol_lookahead = true;  // PT2Q_CHOL_LOOKAHEAD=0: the trailing updates on the main stream only
   int chol_panel = 0;          // PT2Q_CHOL_PANEL: rows per rank-P Cholesky update (0: by m)
   bool wbar_fused = true;      // PT2Q_WBAR_FUSED=0: three SSR-mean launches
-  int gemmx_stages = 3;        // PT2Q_GEMMX_STAGES: LDS stages of the f32 chain GEMM (2: 2 WGs per CU)
+  int gemmx_stages = 2;        // PT2Q_GEMMX_STAGES: LDS stages of the f32 chain GEMM (2: 64 KiB, 2 WGs per CU;
+                               // batched inverse 596 -> 534 ms per 7B step vs 3)
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
   bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM
   // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
