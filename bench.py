@@ -82,6 +82,9 @@ def parse(argv=None):
     p.add_argument("--no-batched-inverse", action="store_true",
                    help="model workload, grams-first: each unit's Cholesky inverse on its lane instead of "
                         "batched per width (engine.hessian_inverse_batched)")
+    p.add_argument("--no-batched-grams", action="store_true",
+                   help="model workload, grams-first: one stream-K Gram launch per unit instead of one "
+                        "data-parallel launch per width (pt2q_gram_batched)")
     p.add_argument("--inverse-overlap", action="store_true",
                    help="model workload: each width's block loops start once its own batched inverses "
                         "are done, beside the other widths' inverses (default: all inverses first)")
@@ -276,7 +279,7 @@ class ModelStep:
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.schedule = a.schedule
         self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group,
-                                       overlap=a.inverse_overlap)
+                                       overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams)
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.index = {u[0]: i for i, u in enumerate(self.units)}
@@ -321,6 +324,7 @@ class ModelStep:
         gf.begin([(i, units[i][1][0][2], units[i][2]) for i in self.mine])
         for i in self.mine:
             gf.gram(i, inputs[i][0])
+        gf.flush()
         torch.cuda.synchronize()
         t["gram"] = time.perf_counter() - t0
         t1 = time.perf_counter()

@@ -93,6 +93,16 @@ size_t pt2q_gram_workspace_bytes(int m);
 int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G, int64_t ldg,
               int accumulate, void* workspace, size_t workspace_bytes, void* stream);
 
+/* A batch of Grams of one shape in ONE data-parallel launch: G[z] = X[z]ᵀX[z] for z < batch
+ * (STORE), X: host array of `batch` device pointers to N x m fp16 / bf16 matrices (ld ldx), G:
+ * batch x m x m fp32 packed.  256 x 256 tiles, every tile one chain over all N rows (no
+ * stream-K pieces, no hand-offs, no workspace), so each G[z] is bit-identical to pt2q_gram on
+ * X[z] alone.  Needs m % 256 == 0, ldx % 8 == 0, 16-byte aligned X[z] and batch <= 128, else
+ * PT2Q_E_UNSUPPORTED (use pt2q_gram per item).  Replaces main.py:128 for every unit of a model
+ * step whose activations are at hand (the q/k/v, o, gate/up inputs of all decoder layers). */
+int pt2q_gram_batched(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
+                      float* G, void* stream);
+
 /* H = G / nsamples; H_ii += percdamp * mean(diag H).  Replaces main.py:129-133 and
  * gptq.py:94-98.  damp_dev (nullable) receives the damping value. */
 int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples, float percdamp,

@@ -49,6 +49,7 @@ _SIGS = {
     "pt2q_ssr_workspace_bytes": (SZ, [I, I]),
     "pt2q_gram_workspace_bytes": (SZ, [I]),
     "pt2q_gram": (I, [P, I, I64, I, I64, P, I64, I, P, SZ, P]),
+    "pt2q_gram_batched": (I, [I, P, I, I64, I, I64, P, P]),
     "pt2q_prepare_hessian": (I, [P, I64, I, I64, F, P, I64, P, P]),
     "pt2q_cholesky_inverse": (I, [P, I64, I, P, I64, P, SZ, P, P]),
     "pt2q_hessian_inverse_batched_workspace_bytes": (SZ, [I, I]),

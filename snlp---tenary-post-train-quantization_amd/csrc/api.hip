@@ -427,6 +427,12 @@ extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ld
   return pt2q_launch_gram(g, flags, (hipStream_t)stream, status);
 }
 
+extern "C" int pt2q_gram_batched(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
+                                 float* G, void* stream) {
+  if (batch <= 0 || !X || !G || N < 0 || N > INT_MAX || m <= 0 || ldx < m) return PT2Q_E_ARG;
+  return pt2q_launch_gram16_batched(X, xdtype, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream);
+}
+
 extern "C" int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples,
                                     float percdamp, float* H, int64_t ldh, float* damp_dev,
                                     void* stream) {

@@ -825,7 +825,116 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// ---- a batch of Grams in one data-parallel launch (pt2q_gram_batched) ------------------------
+// `batch` Grams of the same shape (N x m, m % 256 == 0), item z from X[z] into G + z*gstride.
+// The work line is every item's 256 x 256 upper tiles, item-major, in the super-block order of
+// gram16w_kernel; one workgroup per CU walks it in waves, workgroup w = x + NG r taking tile
+// v*grid + x*R + r (the R workgroups of an XCD run R neighbouring tiles of one item at the same
+// k, as the data-parallel waves of gram16w_kernel).  Every tile is ONE chain over all rows: no
+// stream-K pieces, no hand-offs, and the bits of pt2q_gram on each item alone.
+constexpr int GB_MAX = 128;
+struct GbArgs {
+  const uint16_t* X[GB_MAX];
+  float* G;
+  long gstride, ldx, ldc;
+  int T, SJ, K, M, batch, NG, R;
+  long ntile, total;
+};
+
+template <bool BF16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram16b_kernel(GbArgs b) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[GwGeo<GW_B>::LDS];
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x, x = w % b.NG, r = w / b.NG;
+  const long ldc = b.ldc;
+  for (long L = (long)x * b.R + r; L < b.total; L += gridDim.x) {
+    const int z = (int)(L / b.ntile);
+    const int a = (int)(L - (long)z * b.ntile);
+    int ti, tj;
+    gx_tile<1>(a, b.T, b.T, b.SJ, ti, tj);
+    const int i0 = ti * GW_B, j0 = tj * GW_B;
+    float* const C = b.G + (long)z * b.gstride;
+    const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wu >> 1, wc = wu & 1;
+    const int iw = i0 + wr * 128, jw = j0 + wc * 128;
+    const uint32_t lo = (uint32_t)(4 * (lane >> 5)) * (uint32_t)ldc + (lane & 31);
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[mt][nt][q] = 0.0f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counts its own DMAs
+    gw_chain<GW_B, BF16>(acc, b.X[z], b.ldx, b.M, i0, j0, 0, b.K, true, smem);
+    // upper tile and its mirror, as gram16w_kernel's final store
+    const bool diag = ti == tj;
+    const int dl = (wc * 128 + (lane & 31)) - (wr * 128 + 4 * (lane >> 5));
+    const uint32_t lm = (uint32_t)(lane & 31) * (uint32_t)ldc + 4 * (lane >> 5);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int rl = mt * 32 + 8 * g4;
+          const f32x16& A = acc[mt][nt];
+          const int dc = dl + nt * 32 - rl;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float* rp = C + (long)(iw + rl + u) * ldc + jw;
+            if (!diag || dc >= u) rp[lo + nt * 32] = A[4 * g4 + u];
+          }
+          float* mp = C + (long)(jw + nt * 32) * ldc + iw + rl;
+          if (!diag || dc > 3) {
+            *(float4*)(mp + lm) = make_float4(A[4 * g4], A[4 * g4 + 1], A[4 * g4 + 2], A[4 * g4 + 3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (dc > u) mp[lm + u] = A[4 * g4 + u];
+          }
+        }
+  }
+}
+
 }  // namespace
+
+// batch Grams G[z] = X[z]ᵀX[z] (STORE), X[z] N x m 16-bit (ld ldx), G packed (gstride floats apart,
+// ld m).  E_UNSUPPORTED unless m % 256 == 0 and the LDS-DMA staging conditions hold.
+int pt2q_launch_gram16_batched(const void* const* X, int dtype, long N, int m, long ldx, float* G, long gstride,
+                               int batch, hipStream_t st) {
+  if ((dtype != PT2Q_F16 && dtype != PT2Q_BF16) || batch <= 0 || m <= 0 || N < 0 || !G) return PT2Q_E_ARG;
+  if (batch > GB_MAX || m % GW_B || ldx % 8 || ldx >= (1l << 25) || (uintptr_t)G % 16 || gstride % 4)
+    return PT2Q_E_UNSUPPORTED;
+  GbArgs b{};
+  for (int z = 0; z < batch; ++z) {
+    if (!X[z] && N > 0) return PT2Q_E_ARG;
+    if ((uintptr_t)X[z] % 16) return PT2Q_E_UNSUPPORTED;
+    b.X[z] = (const uint16_t*)X[z];
+  }
+  const Pt2qTuning& tu = pt2q_tuning();
+  b.G = G; b.gstride = gstride; b.ldx = ldx; b.ldc = m;
+  b.T = m / GW_B;
+  b.SJ = tu.gram_super > 0 ? tu.gram_super : 8;
+  b.K = (int)N;
+  b.M = m;
+  b.batch = batch;
+  b.ntile = (long)b.T * (b.T + 1) / 2;
+  b.total = b.ntile * batch;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  b.NG = std::max(1, tu.gram_groups);
+  b.R = std::max(1, cus / b.NG);
+  const long grid = std::min<long>(b.total, (long)b.NG * b.R);
+  if (grid < (long)b.NG * b.R) {  // fewer tiles than workgroups: one tile each, no team order
+    b.NG = 1;
+    b.R = (int)grid;
+  }
+  hipLaunchKernelGGL(dtype == PT2Q_BF16 ? gram16b_kernel<true> : gram16b_kernel<false>, dim3((unsigned)grid),
+                     dim3(256), 0, st, b);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
 
 size_t pt2q_gram16_flags_ints(int m) { return (size_t)gx_ntile(m) + 2; }
 

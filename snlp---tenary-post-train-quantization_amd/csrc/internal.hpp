@@ -98,6 +98,8 @@ size_t pt2q_gram_flags_ints(int m);
 // 16-bit-input Gram on the 16-bit MFMA (gram16.hip): every shape, STORE / ADD / CHAIN_POS
 int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);
 size_t pt2q_gram16_flags_ints(int m);
+int pt2q_launch_gram16_batched(const void* const* X, int dtype, long N, int m, long ldx, float* G, long gstride,
+                               int batch, hipStream_t st);
 
 // ---- misc (misc.hip)
 int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,

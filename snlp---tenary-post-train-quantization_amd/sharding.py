@@ -202,6 +202,8 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
             grams_first.begin([(i, units[i][1][0][2], units[i][2]) for i in mine])
         for i in mine:
             grams_first.gram(i, inputs[i][0])
+        if hasattr(grams_first, "flush"):
+            grams_first.flush()  # batched Grams issued here
         if hasattr(grams_first, "inverses"):
             grams_first.inverses()
         jobs = [(i, [inputs[i][1][p] for p, _, _ in units[i][1]], units[i][2]) for i in mine]
@@ -311,9 +313,12 @@ class GramsFirst:
     per-step device word; check() reads that word once and clears it."""
 
     def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01,
-                 group: int = 16, overlap: bool = False):
+                 group: int = 16, overlap: bool = False, batch_grams: bool = True):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
+        # step 1 batched: the Grams of each (m, N) group in data-parallel launches
+        # (pt2q_gram_batched) instead of one stream-K launch per unit
+        self.batch_grams, self.pending = batch_grams, {}
         self.batched, self.chunk, self.percdamp = batched, chunk, percdamp
         # step 3 grouped: the block loops of up to `group` same-shape linears (across units) per
         # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
@@ -365,10 +370,32 @@ class GramsFirst:
     def gram(self, key, X):
         X2 = X.reshape(-1, X.shape[-1])
         m = X2.shape[1]
+        if self.batch_grams and key in self.slot and self.engine.gram_batched_supported(X2):
+            g, z = self.slot[key]
+            self.pending.setdefault(g, []).append((z, X2))  # issued by flush()
+            return
         if m not in self.ws:
             self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
         self.engine.gram(X2, G=self._gbuf(key, m), workspace=self.ws[m], check=False)
         torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
+
+    def flush(self):
+        """Issue the batched Grams gram() collected: one pt2q_gram_batched sequence per group
+        whose every slot is pending (else per item)."""
+        for g, items in self.pending.items():
+            items.sort(key=lambda t: t[0])
+            grp = self.groups[g]
+            if [z for z, _ in items] == list(range(grp["G"].shape[0])) and \
+                    len({(X.shape, X.dtype) for _, X in items}) == 1:
+                self.engine.gram_batched([X for _, X in items], grp["G"])
+            else:
+                m = grp["G"].shape[1]
+                if m not in self.ws:
+                    self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
+                for z, X in items:
+                    self.engine.gram(X, G=grp["G"][z], workspace=self.ws[m], check=False)
+                    torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
+        self.pending = {}
 
     def inverses(self):
         """Step 2: every group's Hessian inverses, batched (no-op with batched=False), narrowest

@@ -580,3 +580,16 @@ def test_blocks_group_equals_per_linear(pt2q, n, m, count, ssr, dt):
         for a, b in ((got[z].perm, want.perm), (got[z].T, want.T), (got[z].alpha, want.alpha),
                      (got[z].mu, want.mu), (got[z].iters, want.iters)):
             assert bits_equal(host(a), host(b)), z
+
+
+@pytest.mark.parametrize("m,N,batch,dt", [(256, 1000, 3, torch.float16), (512, 2048, 5, torch.bfloat16),
+                                          (4096, 8192, 3, torch.float16), (768, 64, 130, torch.float16)])
+def test_gram_batched_equals_per_item(pt2q, m, N, batch, dt):
+    """pt2q_gram_batched (one data-parallel launch for every item, 256 x 256 tiles, each tile one
+    chain over all rows) == pt2q_gram on each item alone, bit for bit; ragged N, bf16, and more
+    items than one launch takes (130 > 128)."""
+    Xs = [pt2q.fill_synthetic((N, m), 40 + z, outliers=True, device="cuda").to(dt) for z in range(batch)]
+    G = torch.empty((batch, m, m), dtype=torch.float32, device="cuda")
+    pt2q.engine.gram_batched(Xs, G)
+    for z in (0, batch // 2, batch - 1):
+        assert bits_equal(host(G[z]), host(pt2q.gram(Xs[z]))), z

@@ -27,6 +27,7 @@ def step(timed):
     gf.begin([(i, units[i][1][0][2], units[i][2]) for i in mine])
     for i in mine:
         gf.gram(i, inputs[i][0])
+    gf.flush()
     torch.cuda.synchronize()
     t["gram"] = time.perf_counter() - t0
     t1 = time.perf_counter()
