@@ -27,7 +27,6 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_GRAM_PAIR", t.gram_pair);
   getb("PT2Q_GRAM_DP", t.gram_dp);
   getb("PT2Q_GRAM_WIDE", t.gram_wide);
-  getb("PT2Q_GRAM_DMA", t.gram_dma);
   geti("PT2Q_GRAM_SEGLEN", t.gram_seglen);
   geti("PT2Q_GEMM_TILE", t.gemm_tile);
   getb("PT2Q_RANK_UPDATE", t.rank_update);

@@ -102,7 +102,6 @@ struct Pt2qTuning {
   bool gram_pair = true;       // PT2Q_GRAM_PAIR=0: no tile-pair teams
   bool gram_dp = true;         // PT2Q_GRAM_DP=0: no data-parallel waves
   bool gram_wide = true;       // PT2Q_GRAM_WIDE=0: no 256 x 256 tiles
-  bool gram_dma = true;        // PT2Q_GRAM_DMA=0: f32-kernel family without LDS-DMA
   int gram_seglen = 0;         // PT2Q_GRAM_SEGLEN: f32 stream-K segment override
   int gemm_tile = 0;           // PT2Q_GEMM_TILE: 1 = 128x128, 6 = 64x64
   bool rank_update = true;     // PT2Q_RANK_UPDATE=0: generic grouped GEMM for Cholesky updates

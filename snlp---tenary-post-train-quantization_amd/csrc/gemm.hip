@@ -478,259 +478,6 @@ __global__ __launch_bounds__(256) void gram_streamk_kernel(GemmDesc g, int T, in
   }
 }
 
-// ------------------------------------------------------------------ 16-bit Gram, LDS-DMA staged
-//
-// fp16/bf16 X (m % 8 == 0): operand tiles go global -> LDS directly (global_load_lds_dwordx4,
-// no VGPR staging) in their 16-bit form, double-buffered with BK = 64, and are widened to fp32
-// as each lane reads its MFMA operand.  The MFMA row of lane li in sub-tile rm is output row
-// 2*li + rm (a relabeling of the 64 rows a wave owns), so one ds_read_b32 yields both rm (or rn)
-// operands.  LDS image: row k = 256 B = 16 chunks of 8 elements, chunk c stored at c ^ 8*(k&1)
-// so the two k-rows of a k-pair land in different bank halves.  Accumulation is the same f32
-// MFMA k-ascending chain as every other path (bit-identical results).
-constexpr int G16_BK = 64;
-constexpr int G16_ROWB = 256;                 // bytes per k-row (128 elements)
-constexpr int G16_TILEB = G16_BK * G16_ROWB;  // 16 KiB per operand per stage
-#ifndef G16_SB
-#define G16_SB 8
-#endif
-
-template <bool BF16>
-PT2Q_DEV float h2f(uint32_t h) {
-  if constexpr (BF16) {
-    return __uint_as_float(h << 16);
-  } else {
-    _Float16 v;
-    uint16_t u = (uint16_t)h;
-    __builtin_memcpy(&v, &u, 2);
-    return (float)v;
-  }
-}
-
-// Stage one operand tile (k rows [k0, k0+64) x columns [d0, d0+128)) into lds (16 KiB).
-// Each wave issues 4 wave-instructions of 1 KiB; out-of-range chunks read 16 zero bytes.
-PT2Q_DEV void g16_stage(const uint16_t* X, long ld, int d0, int k0, int kend, int M,
-                        uint8_t* lds, const uint16_t* zeros) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = wave * 4 + j;               // wave-instruction index 0..15
-    const int p = q * 64 + lane;              // LDS chunk index 0..1023
-    const int k = p >> 4, phys = p & 15;
-    const int c = phys ^ ((k & 1) << 3);      // logical chunk held at this position
-    const int gk = k0 + k, gd = d0 + c * 8;
-    const uint16_t* src = (gk < kend && gd < M) ? X + (long)gk * ld + gd : zeros;
-    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(lds + q * 1024), 16, 0, 0);
-  }
-}
-
-template <bool BF16>
-struct G16Tile {
-  f32x16 acc[2][2];
-  // output coordinates of accumulator element r of sub-tile (rm, rn)
-  PT2Q_DEV static int row(int i0, int rm, int r) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wr = wave >> 1, lk = lane >> 5;
-    return i0 + wr * 64 + 2 * ((r & 3) + 8 * (r >> 2) + 4 * lk) + rm;
-  }
-  PT2Q_DEV static int col(int j0, int rn) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wc = wave & 1, li = lane & 31;
-    return j0 + wc * 64 + 2 * li + rn;
-  }
-  template <typename F>
-  PT2Q_DEV void for_each(int i0, int j0, F&& f) {
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < 2; ++rn)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = acc[rm][rn][r];
-          f(v, row(i0, rm, r), col(j0, rn));
-          acc[rm][rn][r] = v;
-        }
-  }
-
-  // chains over k in [kbeg, kend); As/Bs: 2 stages of 16 KiB each
-  PT2Q_DEV void mma(const GemmDesc& g, int i0, int j0, int kbeg, int kend, uint8_t* As,
-                    uint8_t* Bs, const uint16_t* zeros) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
-    const uint16_t* X = (const uint16_t*)g.A;
-    const bool same = (i0 == j0);  // diagonal tile: one panel serves both operands
-    // byte offsets of this lane's operand pairs within a stage (k-row 2s+lk added per step)
-    const int offA = ((wr * 8 + (li >> 2)) ^ (lk << 3)) * 16 + (li & 3) * 4 + lk * G16_ROWB;
-    const int offB = ((wc * 8 + (li >> 2)) ^ (lk << 3)) * 16 + (li & 3) * 4 + lk * G16_ROWB;
-    const int ntile = (kend - kbeg + G16_BK - 1) / G16_BK;
-    if (ntile <= 0) return;
-    g16_stage(X, g.lda, i0, kbeg, kend, g.M, As, zeros);
-    if (!same) g16_stage(X, g.lda, j0, kbeg, kend, g.M, Bs, zeros);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < ntile; ++t) {
-      const int cur = t & 1;
-      if (t + 1 < ntile) {
-        const int nb = (t + 1) & 1;
-        g16_stage(X, g.lda, i0, kbeg + (t + 1) * G16_BK, kend, g.M, As + nb * G16_TILEB, zeros);
-        if (!same)
-          g16_stage(X, g.lda, j0, kbeg + (t + 1) * G16_BK, kend, g.M, Bs + nb * G16_TILEB, zeros);
-      }
-      const uint8_t* a = As + cur * G16_TILEB + offA;
-      const uint8_t* b = (same ? As : Bs) + cur * G16_TILEB + offB;
-      // operand pairs are read a batch ahead of the MFMAs that consume them
-      constexpr int SB = G16_SB;
-      uint32_t pa[SB], pb[SB];
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        pa[u] = *(const uint32_t*)(a + u * 2 * G16_ROWB);
-        pb[u] = *(const uint32_t*)(b + u * 2 * G16_ROWB);
-      }
-#pragma unroll
-      for (int s0 = 0; s0 < G16_BK / 2; s0 += SB) {
-        uint32_t qa[SB], qb[SB];
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-          qa[u] = pa[u];
-          qb[u] = pb[u];
-        }
-        if (s0 + SB < G16_BK / 2) {
-#pragma unroll
-          for (int u = 0; u < SB; ++u) {
-            pa[u] = *(const uint32_t*)(a + (s0 + SB + u) * 2 * G16_ROWB);
-            pb[u] = *(const uint32_t*)(b + (s0 + SB + u) * 2 * G16_ROWB);
-          }
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int u = 0; u < SB; ++u) {
-          const float a0 = h2f<BF16>(qa[u] & 0xffffu), a1 = h2f<BF16>(qa[u] >> 16);
-          const float b0 = h2f<BF16>(qb[u] & 0xffffu), b1 = h2f<BF16>(qb[u] >> 16);
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-        }
-        __builtin_amdgcn_s_setprio(0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
-};
-
-#ifdef PT2Q_GRAM_PROFILE
-// dev-only (tools/gram_probe.hip): summed per-workgroup cycles [reload+wait, mma, total, wgs]
-__device__ unsigned long long g16_prof[4];
-#endif
-
-// Persistent Gram over 16-bit X with a STATIC balanced split ("stream-K"): the upper tiles, in
-// supertile order, laid end to end along K form one line of ntile*Kp rows of work; workgroup w
-// takes the contiguous range [w*L, (w+1)*L), L >= Kp.  A range is [head: end of tile a0]
-// [full tiles] [tail: start of tile a1].  The workgroup does its tail FIRST (chains from zero,
-// partial tile published in C + flag), then its full tiles, then its head, which continues the
-// chains of tile a0 from the partial workgroup w-1 published at its start: the wait is normally
-// already satisfied, every fp32 chain stays k-ascending and unsplit, and each tile is split at
-// most once.  (Replaces a dynamic unit queue whose flag waits cost ~4 % of the kernel.)
-// The only dependency is on workgroup w-1, which the in-order dispatcher starts first.
-template <bool BF16>
-__global__ __launch_bounds__(256) void gram16_streamk_kernel(GemmDesc g, int T, int Kp, long L,
-                                                             int* flags, int* status, long cap,
-                                                             const uint16_t* zeros) {
-  constexpr int BM = 128, BN = 128;
-  // ONE __shared__ object: a second one beside the DMA staging makes hipcc wait vmcnt(0)
-  // before every k-step's first ds_read (cdna_hip_programming.md §5, trap 4a)
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[4 * G16_TILEB];
-  uint8_t* As = smem;
-  uint8_t* Bs = smem + 2 * G16_TILEB;
-  const int ntile = T * (T + 1) / 2;
-  const long W = (long)ntile * Kp;
-  // no XCD remap here: w-1 must have a lower dispatch index than w (in-order dispatch) so that
-  // the one dependency can never wait on a workgroup that has not been started
-  const int w = blockIdx.x;
-  const long s = (long)w * L, e = min(s + L, W);
-  if (s >= e) return;
-  const int a0 = (int)(s / Kp), k0 = (int)(s % Kp);
-  const int a1 = (int)((e - 1) / Kp), k1 = (int)(e - (long)a1 * Kp);
-#ifdef PT2Q_GRAM_PROFILE
-  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-  unsigned long long t_wait = 0, t_mma = 0;
-#endif
-  const bool head = k0 > 0;                          // tile a0 rows [k0, ...) after w-1's part
-  const bool tail = k1 < Kp && !(head && a1 == a0);  // tile a1 rows [0, k1), continued by w+1
-  const int f0 = head ? a0 + 1 : a0, f1 = tail ? a1 - 1 : a1;  // full tiles [f0, f1]
-  const int nfull = f1 >= f0 ? f1 - f0 + 1 : 0;
-  const int npieces = (tail ? 1 : 0) + nfull + (head ? 1 : 0);
-  // one loop body (a lambda called three times was inlined three times: 1 wave/SIMD)
-  for (int q = 0; q < npieces; ++q) {
-    int a, kb, ke;
-    bool from_partial = false;
-    if (tail && q == 0) {
-      a = a1; kb = 0; ke = k1;
-    } else if (head && q == npieces - 1) {
-      a = a0; kb = k0; ke = (a0 == a1) ? k1 : Kp; from_partial = true;
-    } else {
-      a = f0 + q - (tail ? 1 : 0); kb = 0; ke = Kp;
-    }
-    int ti, tj;
-    upper_tile(a, T, ti, tj);
-    const int i0 = ti * BM, j0 = tj * BN;
-    G16Tile<BF16> F;
-#ifdef PT2Q_GRAM_PROFILE
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-    if (!from_partial && g.mode != GEMM_CHAIN_POS) {
-      F.for_each(i0, j0, [&](float& v, int, int) { v = 0.0f; });
-    } else {
-      if (from_partial && threadIdx.x == 0) {
-        wait_flag_ge<2>(&flags[a], 1, cap, status, STALL_GRAM);  // gives up loudly
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      F.for_each(i0, j0, [&](float& v, int row, int col) {
-        bool in = row < g.M && col < g.N;
-        v = g.C[in ? (long)row * g.ldc + col : 0];
-      });
-      F.for_each(i0, j0, [&](float& v, int row, int col) {
-        if (!(row < g.M && col < g.N)) v = 0.0f;
-      });
-    }
-#ifdef PT2Q_GRAM_PROFILE
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-#endif
-    F.mma(g, i0, j0, kb, min(ke, g.K), As, Bs, zeros);
-#ifdef PT2Q_GRAM_PROFILE
-    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-    t_wait += t1 - t0;
-    t_mma += t2 - t1;
-#endif
-    const bool final = (ke >= Kp);
-    const bool mirror = final && (ti != tj);
-    F.for_each(i0, j0, [&](float& v, int row, int col) {
-      if (row >= g.M || col >= g.N) return;
-      g.C[(long)row * g.ldc + col] = v;
-      if (mirror) g.C[(long)col * g.ldc + row] = v;
-    });
-    if (!final) {  // publish the partial for workgroup w+1
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&flags[a], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-#ifdef PT2Q_GRAM_PROFILE
-  if (threadIdx.x == 0) {
-    atomicAdd(&g16_prof[0], t_wait);
-    atomicAdd(&g16_prof[1], t_mma);
-    atomicAdd(&g16_prof[2], __builtin_amdgcn_s_memtime() - t_start);
-    atomicAdd(&g16_prof[3], 1ull);
-  }
-#endif
-}
-
 template <int BM, int BN, typename TIn>
 bool vec_ok(const GemmDesc& g) {
   const int vw = 16 / (int)sizeof(TIn);
@@ -792,17 +539,8 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st, in
   int dev = 0, cus = 256, per_cu = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   auto kern = vec_ok<128, 128, TIn>(g) ? gram_streamk_kernel<TIn, true> : gram_streamk_kernel<TIn, false>;
-  // 16-bit inputs with 16-byte rows: the LDS-DMA kernel (PT2Q_GRAM_DMA=0 disables)
-  const bool dma = sizeof(TIn) == 2 && vec_ok<128, 128, TIn>(g) && tu.gram_dma;
-  void (*kern16)(GemmDesc, int, int, long, int*, int*, long, const uint16_t*) =
-      std::is_same<TIn, uint16_t>::value ? gram16_streamk_kernel<true> : gram16_streamk_kernel<false>;
-  if (dma) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern16, 256, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-  } else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
-             per_cu < 1) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  }
   const int P = cus * per_cu;  // one resident wave of workgroups (correctness does not need it)
   // segment length (>= 2048 rows, multiple of 2*BK): minimise the makespan estimate
   // rounds(units / P) * (seglen + per-unit overhead of ~256 rows: partial reload/store, wait)
@@ -819,27 +557,16 @@ int launch_streamk(const GemmDesc& g, int* flags, int nflags, hipStream_t st, in
       seglen = len;
     }
   }
-  // flags: ntile tile flags, status, unit counter, then 16 zero bytes (aligned) for the DMA
+  // flags: ntile tile flags, status, unit counter
   if (tu.gram_seglen >= 64) {
     seglen = tu.gram_seglen / (2 * BK) * (2 * BK);
     nseg = ceil_div(g.K, seglen);
   }
-  if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2 + 8), st) != hipSuccess) return PT2Q_E_HIP;
+  if (hipMemsetAsync(flags, 0, sizeof(int) * (ntile + 2), st) != hipSuccess) return PT2Q_E_HIP;
   if (!status) status = flags + ntile;
   int* counter = flags + ntile + 1;
-  if (dma) {
-    const uint16_t* zeros = (const uint16_t*)(((uintptr_t)(flags + ntile + 2) + 15) & ~(uintptr_t)15);
-    // static split: P16 workgroups, each L >= Kp rows of the tile-major work line
-    const int Kp = ceil_div(g.K, G16_BK) * G16_BK;
-    const int P16 = P < ntile ? P : ntile;
-    const long Wt = (long)ntile * Kp;
-    const long L = ((Wt + P16 - 1) / P16 + G16_BK - 1) / G16_BK * G16_BK;
-    hipLaunchKernelGGL(kern16, dim3((unsigned)ceil_div(Wt, L)), dim3(256), 0, st, g, T, Kp, L, flags,
-                       status, tu.spin_cap_long, zeros);
-  } else {
-    hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, counter, status,
-                       tu.spin_cap_long);
-  }
+  hipLaunchKernelGGL(kern, dim3(P), dim3(256), 0, st, g, T, nseg, seglen, flags, counter, status,
+                     tu.spin_cap_long);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
@@ -1148,14 +875,7 @@ int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st, int* status)
   const bool allow = pt2q_tuning().gram_split;
   if (flags && allow && (g.mode == GEMM_STORE || g.mode == GEMM_CHAIN_POS) && g.upper && g.mirror && g.M == g.N &&
       ntile >= 128 && g.K >= 16384) {
-    switch (g.in_dtype) {
-      case PT2Q_F32:
-        return launch_streamk<float>(g, flags, (int)ntile, st, status);
-      case PT2Q_F16:
-        return launch_streamk<_Float16>(g, flags, (int)ntile, st, status);
-      case PT2Q_BF16:
-        return launch_streamk<uint16_t>(g, flags, (int)ntile, st, status);
-    }
+    if (g.in_dtype == PT2Q_F32) return launch_streamk<float>(g, flags, (int)ntile, st, status);
   }
   return pt2q_launch_gemm(g, st);
 }

@@ -17,6 +17,7 @@
 // per CU (each tile split at most once; the continuing piece waits on the previous workgroup).
 #include "common.hpp"
 #include "internal.hpp"
+#include "probe.hpp"
 
 namespace {
 
@@ -91,6 +92,16 @@ long gx_ntile(int m) { return gx_ntile(ceil_div(m, GX_BM), ceil_div(m, GX_BN), G
 // (units of P tiles): tail piece first (chains from the start of its last unit), full units,
 // then the head piece of its first unit, continuing the partial that the same member of the
 // previous team (w - P*NG, dispatched earlier) published.  L >= Kp.  NG = 1 and L = Kp: no split.
+// Forward progress of that wait: a workgroup only ever waits on a LOWER blockIdx (w - P*NG),
+// the dispatcher hands workgroups out in blockIdx order (round-robin over the XCDs, in order
+// within each XCD), and P*NG is a multiple of the 8 XCDs, so the producer sits on the waiter's
+// own XCD, earlier in that XCD's queue: it was resident before the waiter took a slot and it
+// waits, in turn, only on still lower indices -- induction from w < P*NG, which waits on nobody.
+// The argument needs no co-residency of the grid.  Should the order ever be violated, the wait
+// gives up after the spin cap, sets STALL_GRAM in the status word and the host raises
+// Pt2qError (no hang, no silent result); a consumer-side recompute is not possible since the
+// producer's partial lives only in C.  The batched Gram of a step (gram16b_kernel, the bench
+// and GramsFirst default) is purely data parallel and has no such wait at all.
 // P = 2: the line is cut into tile pairs (2j, 2j+1), which share their column block tj, and
 // workgroups r = 2i, 2i+1 (a team) walk the same stretch of pairs in step, one tile of each
 // pair apiece, so the X panel of tj is fetched into L2 once for both.
@@ -200,9 +211,7 @@ PT2Q_DEV void gx_voff(long ld, int i0, int j0, uint32_t (&vo)[12]) {
 
 // Quarter qq of a fast stage: A chunk j = qq, B chunks j = 2qq, 2qq + 1.
 PT2Q_DEV void gx_stage_q(const uint16_t* Xk0, const uint32_t (&vo)[12], uint8_t* stg, int qq) {
-#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
-  return;
-#endif
+  if constexpr (probe::gram_no_dma) return;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const char* sb = (const char*)Xk0;
   typedef __attribute__((address_space(3))) void* lptr;
@@ -279,9 +288,7 @@ struct GxTile {
 
   template <bool BF16>
   PT2Q_DEV void mma(const GxFrags& f) {
-#ifdef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
-    return;
-#endif
+    if constexpr (probe::gram_no_mfma) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -407,9 +414,7 @@ PT2Q_DEV void gw_chunk(int q, int& row, int& c) {
 // whole stage with per-lane sources: rows past kend and columns past M read the zero chunk
 template <int BM>
 PT2Q_DEV void gw_stage(const uint16_t* X, long ld, int M, int i0, int j0, int k0, int kend, uint8_t* stg) {
-#ifdef GX_PROBE_NO_DMA  // tools/gram16_probe.hip: compute-only timing (stale LDS)
-  return;
-#endif
+  if constexpr (probe::gram_no_dma) return;
   using G = GwGeo<BM>;
   const int wave = threadIdx.x >> 6;
   typedef __attribute__((address_space(3))) void* lptr;
@@ -492,17 +497,13 @@ PT2Q_DEV void gw_vmwait_y(int y) {
 
 template <bool BF16>
 PT2Q_DEV void gw_mfma1(f32x16& acc, const s16x4& alo, const s16x4& ahi, const s16x4& blo, const s16x4& bhi) {
-#ifndef GX_PROBE_NO_MFMA  // tools/gram16_probe.hip: fetch-only timing
-  acc = gx_mfma<BF16>(gx_cat(alo, ahi), gx_cat(blo, bhi), acc);
-#endif
+  if constexpr (!probe::gram_no_mfma) acc = gx_mfma<BF16>(gx_cat(alo, ahi), gx_cat(blo, bhi), acc);
   __builtin_amdgcn_sched_barrier(0);  // nothing moves across: the step's interleaving stays
 }
 
 // one 16-B LDS-DMA: global (sbase + voff) -> LDS m0 + 16 lane
 PT2Q_DEV void gw_dma_asm(const char* sbase, uint32_t voff, uint32_t m0) {
-#ifdef GX_PROBE_NO_DMA
-  return;
-#endif
+  if constexpr (probe::gram_no_dma) return;
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0)
                : "memory");  // (m0 is reserved: the compiler sets it afresh before its own DMAs)
 }

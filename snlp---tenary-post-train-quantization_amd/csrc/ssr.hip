@@ -8,6 +8,7 @@
 // "column" gather of the reference is a gather of whole contiguous rows here.
 #include "common.hpp"
 #include "internal.hpp"
+#include "probe.hpp"
 
 namespace {
 
@@ -375,13 +376,6 @@ constexpr int S1_ROWS = TOPK_THREADS / 128;  // S1 rows per helper workgroup
 // rows of G[blk][blk] in parallel and sum each in l order; the last one to finish forms d in j
 // order (the s1_block order).  Workgroup 0 is dispatched first and waits on nobody, so the
 // spin cannot deadlock.  sync[0]: pick published; sync[1]: helpers done.
-#ifdef TOPK_STAMPS  // tools/topk_probe.hip: phase timestamps (thread 0 of each workgroup)
-__device__ long long topk_stamps[64][16];
-#define TOPK_STAMP(i) \
-  if (threadIdx.x == 0 && blockIdx.x < 64) topk_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
-#else
-#define TOPK_STAMP(i)
-#endif
 
 PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* S1, float* d,
                         int* sync, float* gb, int* status, long cap) {
@@ -390,7 +384,7 @@ PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* 
   // before the flag / counter, sc1 loads on the consuming side, no fences
   if (tid == 0) wait_flag_ge<1>(&sync[0], 1, cap, status, STALL_TOPK);
   __syncthreads();
-  TOPK_STAMP(8);
+  PT2Q_TOPK_STAMP(8);
   const int jj = tid >> 7, l = tid & 127;
   const int j = (blockIdx.x - 1) * S1_ROWS + jj;
   if (j < b && l < b) {
@@ -416,7 +410,7 @@ PT2Q_DEV void s1_helper(const float* G, long ldg, const int* blk, int b, float* 
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  TOPK_STAMP(9);
+  PT2Q_TOPK_STAMP(9);
   if (tid == 0) last = atomicAdd(&sync[1], 1) == nh - 1;
   __syncthreads();
   if (!last) return;
@@ -453,7 +447,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
   int* bl = (int*)(pv + b);             // b block indices (selection order)
   float* s1 = (float*)(bl + b);
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6;
-  TOPK_STAMP(0);
+  PT2Q_TOPK_STAMP(0);
   for (int e = tid; e < r; e += nt) vals[e] = orderable(sim[e]);
   uint32_t prefix = 0, pmask = 0;
   int kk = b;  // rank (1-based) of v* among the values matching prefix
@@ -462,7 +456,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
   // alternating slots (read after the pass's second barrier, rewritten two passes later).
   for (int i = tid; i < 32 * TOPK_HPAD; i += nt) hist[i] = 0;
   __syncthreads();
-  TOPK_STAMP(4);
+  PT2Q_TOPK_STAMP(4);
   int* res = sc + 70;
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
@@ -514,12 +508,12 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
       }
     }
     __syncthreads();
-    if (p == 0) TOPK_STAMP(5);
+    if (p == 0) PT2Q_TOPK_STAMP(5);
     prefix |= (uint32_t)res[2 * (p & 1)] << shift;
     pmask |= 255u << shift;
     kk = res[2 * (p & 1) + 1];
   }
-  TOPK_STAMP(1);
+  PT2Q_TOPK_STAMP(1);
   // prefix = v*; the first kk positions holding v* are picked, with every value above it
   const int per = (r + nt - 1) / nt;
   const int e0 = min(r, tid * per), e1 = min(r, e0 + per);
@@ -534,7 +528,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
     cs += s;
     cu += !s;
   }
-  TOPK_STAMP(2);
+  PT2Q_TOPK_STAMP(2);
   // one scan for both compactions (r < 2^16): picks and the unselected remainder, ascending
   const int both = block_excl_scan((cs << 16) | cu, sc, &tot);
   int os = both >> 16, ou = both & 0xFFFF;
@@ -547,7 +541,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
     }
   }
   __syncthreads();
-  TOPK_STAMP(3);
+  PT2Q_TOPK_STAMP(3);
   // rank of pick t: picks above it in (value desc, position asc); picks are position-ascending.
   // Eight threads per pick, each over every eighth other pick, then summed across the eight.
   for (int t0 = 0; t0 < b; t0 += nt / 8) {
@@ -572,13 +566,13 @@ __global__ __launch_bounds__(TOPK_THREADS) void ssr_topk_kernel(const float* sim
   (void)lane;
   (void)bl;
   (void)s1;
-  TOPK_STAMP(6);
+  PT2Q_TOPK_STAMP(6);
   if (G) {  // publish the pick to the S1 helpers (every storing wave drained first)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_store(&sync[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  TOPK_STAMP(7);
+  PT2Q_TOPK_STAMP(7);
 }
 
 // Sequential block (use_ssr=False: main.py:167-169, gptq.py:135-137) or "take the rest"

@@ -1,10 +1,16 @@
-// Dev tool: phase timestamps of the SSR top-k launch (ssr.hip built with -DTOPK_STAMPS).
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DTOPK_STAMPS -I include \
+// Dev tool: phase timestamps of the SSR top-k launch (ssr.hip built with -DPT2Q_PROBE=4, csrc/probe.hpp).
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DPT2Q_PROBE=4 -I include \
 //   -I snlp---tenary-post-train-quantization_amd/csrc tools/topk_probe.hip -o tools/topk_probe.bin
 #include "../snlp---tenary-post-train-quantization_amd/csrc/ssr.hip"
 
 #include <cstdio>
 #include <vector>
+
+// the library's tuning (api.hip) at its defaults
+const Pt2qTuning& pt2q_tuning() {
+  static Pt2qTuning t;
+  return t;
+}
 
 int main() {
   const int r = 3968, b = 128, m = 4096;
