@@ -33,6 +33,7 @@ WORLD_SIZE, else the run is refused; `n_gpus` in the line is `dist.get_world_siz
 `--dry-run` exercises the same multi-rank plumbing on CPU (gloo, stub units, no libpt2q) for tests.
 """
 import argparse
+import gc
 import json
 import os
 import socket
@@ -63,14 +64,18 @@ def parse(argv=None):
     p.add_argument("--workload", choices=["model", "layer", "split"], default="model",
                    help="model: LPT-sharded 7B step; layer: one layer per rank (weak); split: one n x m "
                         "layer, its Gram data-parallel over the ranks (strong)")
-    p.add_argument("--layers", type=int, default=32, help="decoder layers of the model workload")
-    p.add_argument("--hidden", type=int, default=4096)
-    p.add_argument("--inter", type=int, default=11008)
+    p.add_argument("--model", choices=["llama-2-7b", "gpt2", "opt-1.3b", "llama-2-13b"], default="llama-2-7b",
+                   help="model workload: the BASELINE config whose linears one step quantises (C4 default; "
+                        "C2 gpt2, C3 opt-1.3b, C5 llama-2-13b) -- sets the defaults of --layers, --tokens, "
+                        "--block-size and --io-dtype (sharding.MODELS)")
+    p.add_argument("--layers", type=int, default=None, help="decoder layers of the model workload")
+    p.add_argument("--hidden", type=int, default=None, help="llama models: override the hidden width")
+    p.add_argument("--inter", type=int, default=None, help="llama models: override the MLP width")
     p.add_argument("--n", type=int, default=4096, help="layer workload: d_out")
     p.add_argument("--m", type=int, default=4096, help="layer workload: d_in")
-    p.add_argument("--tokens", type=int, default=262144)
-    p.add_argument("--block-size", type=int, default=128)
-    p.add_argument("--io-dtype", choices=["fp16", "fp32", "bf16"], default="fp16")
+    p.add_argument("--tokens", type=int, default=None, help="calibration rows N (default: the model's)")
+    p.add_argument("--block-size", type=int, default=None)
+    p.add_argument("--io-dtype", choices=["fp16", "fp32", "bf16"], default=None)
     p.add_argument("--no-ssr", action="store_true")
     p.add_argument("--lanes", type=int, default=3, help="model workload: UnitPipeline lanes")
     p.add_argument("--schedule", choices=["grams-first", "interleaved"], default="grams-first",
@@ -93,8 +98,80 @@ def parse(argv=None):
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true",
-                   help="skip the single-layer / Gram extras (profiling: keeps only the step's launches)")
+                   help="skip the single-layer / Gram / per-config extras (profiling: keeps only the "
+                        "step's launches)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip extra.configs (one short run of each other BASELINE config)")
     return p.parse_args(argv)
+
+
+def resolve(a):
+    """Fill the model-dependent defaults from sharding.MODELS (after _load_runtime)."""
+    c = sharding.MODELS[a.model]
+    hidden = c["units"](1, 1)[0][1][0][2]  # the first unit's input width
+    a.layers = c["layers"] if a.layers is None else a.layers
+    a.tokens = c["tokens"] if a.tokens is None else a.tokens
+    a.block_size = c["block_size"] if a.block_size is None else a.block_size
+    a.io_dtype = c["io"] if a.io_dtype is None else a.io_dtype
+    a.hidden_given = a.hidden is not None or a.inter is not None
+    a.hidden = hidden if a.hidden is None else a.hidden
+    a.inter = 11008 if a.inter is None else a.inter
+    return a
+
+
+def describe_units(units, layers):
+    """'L layers x (q_proj,k_proj,v_proj,o_proj 4096x4096; ...) = K linears in U shared-input units'."""
+    per = units[:len(units) // max(layers, 1)]
+    shapes = {}
+    for _, lins, _ in per:
+        for p, n, m in lins:
+            shapes.setdefault((n, m), []).append(p)
+    body = "; ".join(f"{','.join(ps)} {n}x{m}" for (n, m), ps in shapes.items())
+    return (f"{layers} layers x ({body}) = {sum(len(l) for _, l, _ in units)} linears in {len(units)} "
+            f"shared-input units")
+
+
+def config_runs(a, dev):
+    """extra.configs: one short grams-first run (1 warmup + 2 timed steps, same flags) of every
+    other BASELINE config's model workload on this GPU (C2 gpt2, C3 opt-1.3b, C5 llama-2-13b, or
+    C4 when another model is the headline)."""
+    out = {}
+    for name in sharding.MODELS:
+        if name == a.model:
+            continue
+        b = resolve(parse(["--model", name, "--steps", "2", "--warmup", "1", "--group", str(a.group),
+                           "--lanes", str(a.lanes)]))
+        io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[b.io_dtype]
+        try:
+            w = ModelStep(b, 0, 1, dev, io)
+            for _ in range(b.warmup):
+                w.step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(b.steps):
+                w.step()
+            torch.cuda.synchronize()
+            s = (time.perf_counter() - t0) / b.steps
+            cols = sharding.units_cols(w.units)
+            out[name] = {"config": sharding.MODELS[name]["config"], "workload": describe_units(w.units, b.layers),
+                         "tokens": b.tokens, "block_size": b.block_size if b.block_size < (1 << 14) else "m (per-channel)",
+                         "io_dtype": b.io_dtype, "weight_columns_per_step": cols, "ms_per_step": s * 1e3,
+                         "cols_per_s": cols / s, "s_per_decoder_layer": s / b.layers,
+                         "steps": b.steps, "warmup": b.warmup}
+            del w
+            gc.collect()
+        except Exception as e:  # a config that fails is reported, not allowed to drop the line
+            out[name] = {"config": sharding.MODELS[name]["config"], "error": f"{type(e).__name__}: {e}"}
+        gc.collect()
+        torch.cuda.empty_cache()
+    return out
+
+
+def model_units(a):
+    """The model workload's units: sharding.MODELS[a.model], or llama shapes with --hidden/--inter."""
+    if a.hidden_given and a.model.startswith("llama"):
+        return sharding.llama_units(a.layers, a.hidden, a.inter, a.tokens)
+    return sharding.model_units(a.model, a.layers, a.tokens)
 
 
 def _free_port():
@@ -260,6 +337,22 @@ def gram_time_ms(X, m, reps=3):
     return ev0.elapsed_time(ev1) / reps
 
 
+def gram_batched_time_ms(X, m, count, reps=2):
+    """Average time of ONE batched Gram launch over `count` Grams of X (pt2q_gram_batched, as the
+    step issues it), HIP events on torch's current stream (the launch stream)."""
+    G = torch.empty((count, m, m), dtype=torch.float32, device=X.device)
+    Xs = [X] * count
+    pt2q.engine.gram_batched(Xs, G)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        pt2q.engine.gram_batched(Xs, G)
+    ev1.record()
+    torch.cuda.synchronize()
+    del G
+    return ev0.elapsed_time(ev1) / reps
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "gram_pmc.json")
     if os.path.exists(path):
@@ -272,8 +365,8 @@ class ModelStep:
     """This rank's share of the model: resident inputs, per-width workspaces, one step."""
 
     def __init__(self, a, rank, world, dev, io):
-        self.units = sharding.llama_units(a.layers, a.hidden, a.inter, a.tokens)
-        self.shards = sharding.assign_lpt([sharding.unit_cost(u) for u in self.units], world)
+        self.units = model_units(a)
+        self.shards = sharding.assign_lpt([sharding.unit_cost(u, a.block_size) for u in self.units], world)
         self.mine = self.shards[rank]
         self.bs, self.ssr = a.block_size, not a.no_ssr
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
@@ -452,8 +545,8 @@ class DryStep:
     returns small deterministic outputs instead of launching kernels."""
 
     def __init__(self, a, rank, world, dev, io):
-        self.units = sharding.llama_units(a.layers, a.hidden, a.inter, a.tokens)
-        self.shards = sharding.assign_lpt([sharding.unit_cost(u) for u in self.units], world)
+        self.units = model_units(a)
+        self.shards = sharding.assign_lpt([sharding.unit_cost(u, a.block_size) for u in self.units], world)
         self.mine = self.shards[rank]
         self.bs = a.block_size
         self.ran = []
@@ -489,6 +582,7 @@ def main(argv=None):
     if rc is not None:
         return rc
     _load_runtime(a.dry_run)
+    resolve(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -613,29 +707,39 @@ def main(argv=None):
         mix = {}
         for _, lins, Nu in work.units:
             mix[lins[0][2]] = mix.get(lins[0][2], 0) + 1
-        launches = sum(mix.values())
+        # the step's Gram launches: one pt2q_gram_batched launch per input width (<= 128 Grams
+        # each) with batched Grams, else one pt2q_gram launch per unit
+        gb = (a.workload == "model" and work.gf is not None and work.gf.batch_grams and a.io_dtype != "fp32"
+              and all(m % 256 == 0 for m in mix))
+        per_launch = {m: (min(cnt, pt2q.engine.GRAM_BATCH_MAX) if gb else 1) for m, cnt in mix.items()}
+        nl = {m: -(-cnt // per_launch[m]) for m, cnt in mix.items()}
+        launches = sum(nl.values())
         tot_ms = tot_fl = 0.0
         per_m = {}
         for m, cnt in sorted(mix.items()):
             Xm = work.X.get(m) if a.workload == "model" else work.Xl
             if Xm is None:
                 Xm = pt2q.fill_synthetic((N, m), 2000 + m, std=1.0, outliers=True, device=dev).to(io)
-            ms = gram_time_ms(Xm, m)
-            fl = float(N) * m * (m + 1)   # unique entries of the symmetric product, 2 flop each
-            per_m[str(m)] = {"launches_per_step": cnt, "avg_launch_ms": ms, "tflops": fl / ms / 1e9}
-            tot_ms += cnt * ms
-            tot_fl += cnt * fl
+            ms = gram_batched_time_ms(Xm, m, per_launch[m]) if gb else gram_time_ms(Xm, m)
+            fl = float(N) * m * (m + 1) * per_launch[m]  # unique entries of each symmetric product, 2 flop each
+            per_m[str(m)] = {"launches_per_step": nl[m], "grams_per_launch": per_launch[m], "avg_launch_ms": ms,
+                             "ms_per_gram": ms / per_launch[m], "tflops": fl / ms / 1e9}
+            tot_ms += nl[m] * ms
+            tot_fl += nl[m] * fl
         avg_ms, avg_fl = tot_ms / launches, tot_fl / launches
         achieved = avg_fl / (avg_ms * 1e-3) / 1e12
         peak = MI355X_F32_MFMA_PEAK_TFLOPS if a.io_dtype == "fp32" else MI355X_F16_MFMA_PEAK_TFLOPS
         kname = ("gram_streamk_kernel (symmetric Gram XᵀX, f32 MFMA 32x32x2)" if a.io_dtype == "fp32" else
+                 "gram16b_kernel: every Gram of one input width in one data-parallel launch (256x256 tiles, "
+                 "LDS-DMA ring, ds_read_b64_tr_b16, hand-interleaved 16-bit MFMA 32x32x16, f32 accumulate)"
+                 if gb else
                  "gram16x_kernel (m=4096: 128x256 tiles) / gram16w_kernel (m=11008: 256x256 tiles): "
                  "symmetric Gram XᵀX, LDS-DMA ring, ds_read_b64_tr_b16, hand-interleaved 16-bit MFMA "
                  "32x32x16, f32 accumulate")
-        fl_2nm2 = sum(cnt * 2.0 * N * m * m for m, cnt in mix.items()) / launches
+        fl_2nm2 = sum(nl[m] * per_launch[m] * 2.0 * N * m * m for m in mix) / launches
         roof = {"bound": "mfma", "kernel": kname, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "frac_basis": "work done: N*m*(m+1) flops per launch (the symmetric "
-                                                      "half the kernel forms)",
+                "frac": achieved / peak, "frac_basis": "work done: N*m*(m+1) flops per Gram (the symmetric "
+                                                      "half the kernel forms) x Grams per launch",
                 "frac_2nm2": fl_2nm2 / (avg_ms * 1e-3) / 1e12 / peak,
                 "traffic": None, "avg_launch_ms": avg_ms,
                 "flops_per_launch": avg_fl, "flops_per_launch_2nm2": fl_2nm2, "per_width": per_m,
@@ -652,16 +756,17 @@ def main(argv=None):
             roof["phase_s"] = ph
             roof["stages"] = stage_roofline(model_work(work.units, bs), ph, kern, ms_per_step, world)
         tr = load_traffic()
-        if tr and "per_width" in tr and all(str(m) in tr["per_width"] for m in mix):
-            # PMC fabric bytes per launch of each width, averaged over the step's launch mix
-            pw = tr["per_width"]
-            roof["traffic"] = sum(cnt * pw[str(m)]["fabric_bytes_per_launch"] for m, cnt in mix.items()) / launches
-            roof["traffic_source"] = tr.get("source")
+        key = "batched" if gb else "per_item"
+        if tr and key in tr and all(str(m) in tr[key]["per_width"] for m in mix):
+            # PMC fabric bytes per Gram of each width (same kernel, same launch shape), times the
+            # Grams of the step, over its launches
+            pw = tr[key]["per_width"]
+            roof["traffic"] = sum(cnt * pw[str(m)]["fabric_bytes_per_gram"] for m, cnt in mix.items()) / launches
+            roof["traffic_algorithmic"] = sum(cnt * 2.0 * N * m for m, cnt in mix.items()) / launches
+            roof["traffic_source"] = tr[key].get("source")
 
     if rank == 0:
-        model_desc = (f"llama-2-7b shapes: {a.layers} layers x (q,k,v,o {d}x{d}; gate,up {a.inter}x{d}; "
-                      f"down {d}x{a.inter}) = {sum(len(l) for _, l, _ in work.units)} linears in "
-                      f"{len(work.units)} shared-input units" if a.workload == "model" else
+        model_desc = (f"{a.model} shapes: {describe_units(work.units, a.layers)}" if a.workload == "model" else
                       f"one {a.n}x{a.m} linear per rank" if a.workload == "layer" else
                       f"one {a.n}x{a.m} linear, its Gram split over {world} ranks' calibration rows")
         res = {
@@ -675,10 +780,10 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak" if a.workload == "layer" else "strong",
             "vs_baseline": None,
-            "dtype": "fp16->f32" if a.io_dtype != "fp32" else "f32",
-            "data": ("synthetic (counter-hash fp16 weights std 0.02; fp16 activations, unit variance, "
-                     "1% x20 outlier channels; one resident activation tensor per input width per rank)"),
-            "config": {"workload": f"{model_desc}, N={N} calibration rows (CLI 128x2048), variant M, "
+            "dtype": f"{a.io_dtype}->f32" if a.io_dtype != "fp32" else "f32",
+            "data": (f"synthetic (counter-hash {a.io_dtype} weights std 0.02; {a.io_dtype} activations, unit "
+                     "variance, 1% x20 outlier channels; one resident activation tensor per input width per rank)"),
+            "config": {"workload": f"{model_desc}, N={N} calibration rows, variant M, "
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
                        "weight_columns_per_step": cols, "tokens": N, "io_dtype": a.io_dtype,
                        "block_size": bs,
@@ -695,6 +800,15 @@ def main(argv=None):
             res["ranks"] = ranks
         if roof is not None:
             res["roofline"] = roof
+        if (a.workload == "model" and world == 1 and not a.no_extra and not a.no_configs
+                and not a.hidden_given and a.layers == sharding.MODELS[a.model]["layers"]):
+            log(rank, "per-config runs ...")
+            units_main = work.units
+            del work  # the headline model's resident inputs and buffers (~150 GB) make room
+            gc.collect()
+            torch.cuda.empty_cache()
+            extra["configs"] = config_runs(a, dev)
+            work = argparse.Namespace(units=units_main)
         res["extra"] = extra
         if world == 1 and not a.no_cpu_baseline and a.workload != "split":
             log(rank, "cpu baseline (oracle) ...")

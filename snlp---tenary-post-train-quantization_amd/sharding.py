@@ -45,6 +45,52 @@ def llama_units(num_layers: int, hidden: int = 4096, inter: int = 11008, tokens:
     return units
 
 
+def gpt2_units(num_layers: int = 12, hidden: int = 768, inter: int = 3072, tokens: int = 2048):
+    """GPT-2 decoder stack (HF Conv1D weights taken transposed): c_attn is already
+    the fused q/k/v projection, so every linear is its own unit."""
+    units = []
+    for l in range(num_layers):
+        units.append((f"h_{l}.c_attn", [("c_attn", 3 * hidden, hidden)], tokens))
+        units.append((f"h_{l}.attn_c_proj", [("attn.c_proj", hidden, hidden)], tokens))
+        units.append((f"h_{l}.c_fc", [("c_fc", inter, hidden)], tokens))
+        units.append((f"h_{l}.mlp_c_proj", [("mlp.c_proj", hidden, inter)], tokens))
+    return units
+
+
+def opt_units(num_layers: int = 24, hidden: int = 2048, ffn: int = 8192, tokens: int = 2048):
+    """OPT decoder stack (model.py:139-171 finds q/k/v/out_proj, fc1, fc2): q/k/v share one input."""
+    units = []
+    for l in range(num_layers):
+        units.append((f"layer_{l}.qkv", [("q_proj", hidden, hidden), ("k_proj", hidden, hidden),
+                                         ("v_proj", hidden, hidden)], tokens))
+        units.append((f"layer_{l}.out", [("out_proj", hidden, hidden)], tokens))
+        units.append((f"layer_{l}.fc1", [("fc1", ffn, hidden)], tokens))
+        units.append((f"layer_{l}.fc2", [("fc2", hidden, ffn)], tokens))
+    return units
+
+
+# The BASELINE.json configs C2-C5 as model workloads (SURVEY §8 config table): unit list, calibration
+# rows N, block size (C5 per-channel: one block per linear, b >= every m) and activation dtype.
+MODELS = {
+    "gpt2": dict(config="C2 GPT-2-small all linears, ITF + SSR", layers=12,
+                 units=lambda L, N: gpt2_units(L, 768, 3072, N), tokens=2048, block_size=128, io="fp32"),
+    "opt-1.3b": dict(config="C3 OPT-1.3B fp16, AGA + GPTQ error feedback", layers=24,
+                     units=lambda L, N: opt_units(L, 2048, 8192, N), tokens=2048, block_size=128, io="fp16"),
+    "llama-2-7b": dict(config="C4 Llama-2-7B fp16, full ATQ + SSR", layers=32,
+                       units=lambda L, N: llama_units(L, 4096, 11008, N), tokens=262144, block_size=128,
+                       io="fp16"),
+    "llama-2-13b": dict(config="C5 Llama-2-13B bf16, per-channel, 4096-row Hessian", layers=40,
+                        units=lambda L, N: llama_units(L, 5120, 13824, N), tokens=4096, block_size=1 << 14,
+                        io="bf16"),
+}
+
+
+def model_units(model: str, layers: Optional[int] = None, tokens: Optional[int] = None):
+    """Work units of one of MODELS (layers / tokens override the config's)."""
+    c = MODELS[model]
+    return c["units"](c["layers"] if layers is None else layers, c["tokens"] if tokens is None else tokens)
+
+
 # Measured single-MI355X rates behind unit_cost (profiles/r02f_summary.md, DESIGN.md §4): the
 # 16-bit Gram moves ~1.05e15 N·m² per second; the Cholesky inverse costs m³ at ~1e14/s plus a
 # ~25 µs critical-path step per 64 columns; a block of the block loop costs ~30 µs of launch

@@ -1,6 +1,8 @@
-"""PMC workloads (dev tool): python tools/kern_workloads.py {inverse M BATCH | group N M COUNT} [reps]
+"""PMC workloads (dev tool):
+python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT} [reps]
 inverse: engine.hessian_inverse_batched on BATCH synthetic Grams of order M (N = 262144 scale);
-group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M)."""
+group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M);
+grams:   engine.gram_batched over COUNT Grams of one resident fp16 N x M activation (as the bench)."""
 import os
 import sys
 import torch
@@ -18,6 +20,14 @@ if kind == "inverse":
         Hinv, info = pt2q.engine.hessian_inverse_batched(G, 4 * m, chunk=batch)
     torch.cuda.synchronize()
     print("inverse done", int(info.max()))
+elif kind == "grams":
+    n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    X = pt2q.fill_synthetic((n, m), 79, outliers=True).half()
+    G = torch.empty(count, m, m, device=X.device)
+    for _ in range(reps):
+        pt2q.engine.gram_batched([X] * count, G)
+    torch.cuda.synchronize()
+    print("grams done", float(G[0, 0, 0]))
 else:
     n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     X = pt2q.fill_synthetic((4 * m, m), 78, outliers=True).half()

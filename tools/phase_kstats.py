@@ -2,6 +2,7 @@
 python tools/phase_kstats.py <kernel_trace.csv> [--top 20]
 Phases: gram (gram16* launches), inverse (after the last Gram up to the first block-loop kernel),
 tails (the rest).  Prints the span, busy time and per-kernel totals of each phase."""
+import os
 import argparse
 import csv
 from collections import defaultdict
@@ -37,7 +38,8 @@ def main():
     lastg = max(i for i, r in enumerate(rows) if isg(r))
     firstl = min(i for i, r in enumerate(rows) if i > lastg and any(k in r["Kernel_Name"] for k in LOOP))
     phases = {"gram": rows[:lastg + 1], "inverse": rows[lastg + 1:firstl], "tails": rows[firstl:]}
-    out = {"source": a.csv}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {"source": os.path.relpath(os.path.abspath(a.csv), root) + " (kernel trace of tools/phase_times.py)"}
     for ph, rs in phases.items():
         if not rs:
             continue

@@ -10,6 +10,7 @@ import bench  # noqa: E402
 
 a = bench.parse(sys.argv[1:] + ["--no-cpu-baseline"])
 bench._load_runtime(False)
+bench.resolve(a)
 torch, sharding = bench.torch, bench.sharding
 dev = torch.device("cuda", 0)
 io = torch.float16

@@ -1,14 +1,22 @@
 #!/bin/bash
-# PMC passes of the 16-bit Gram alone (GPU box, repo root, via gpurun), one counter per run:
-#   bash tools/pmc_gram.sh TAG M [N]      -> gpurun_out/pmc_<TAG>/<CTR>/  (tools/pmc_table.py reads it)
+# PMC passes (one counter set per run) on the batched Gram: bash tools/pmc_gram.sh TAG (GPU box)
 set -o pipefail
-TAG=$1; M=${2:-11008}; N=${3:-262144}
+TAG=${1:-pmc_gram}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/pmc_$TAG
+OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-for ctr in FETCH_SIZE WRITE_SIZE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE; do
-  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/$ctr -o run --output-format csv -- \
-    python3 $R/tools/bench_gram.py $N $M fp16 > $OUT/$ctr.log 2>&1 || exit 1
+run() {  # name, counters, workload args...
+  local name=$1 ctr=$2; shift 2
+  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/$name -o run --output-format csv -- \
+    python3 $R/tools/kern_workloads.py "$@" > $OUT/$name.log 2>&1 || { echo "FAIL $name"; tail -3 $OUT/$name.log; exit 1; }
+  echo "ok $name"
+}
+for w in "4096 24" "11008 8"; do
+  set -- $w
+  run g$1_mfma "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES" grams 262144 $1 $2 2
+  run g$1_fetch "FETCH_SIZE" grams 262144 $1 $2 2
+  run g$1_write "WRITE_SIZE" grams 262144 $1 $2 2
+  run g$1_hit "TCC_HIT_sum TCC_MISS_sum" grams 262144 $1 $2 2
 done
-echo "pmc $TAG done"
+python3 $R/tools/pmc_multi.py $OUT/g4096_* $OUT/g11008_* > $OUT/summary.txt && cat $OUT/summary.txt
