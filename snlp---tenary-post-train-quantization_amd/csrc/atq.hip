@@ -568,23 +568,17 @@ __global__ void count_zero_rows_kernel(const float* T, long ldt, int n, int b, i
 // ----------------------------------------------------------------- wide blocks (b > 512)
 //
 // Per-channel quantisation (block_size = m, BASELINE config 5) makes a block as wide as the
-// layer (5120 .. 13824 columns): a row no longer fits in registers.  Here ONE LANE OWNS ONE ROW
-// (64 rows per wave) and streams the row's columns from HBM/L2 on every pass, keeping only the
-// 16 residue-class partials of the canonical SUM16 in registers; fold16() applies the same
-// xor-8/4/2/1 butterfly to them, so every value is bit-identical to the 16-lane kernels and to
-// the oracle.  The codes live in the output array T itself between passes.  Each round pass
-// also accumulates the next grid's partials from the codes it just wrote (same values, same
-// order), so an ITF iteration costs one pass over W and T.
-
-PT2Q_DEV float fold16(const float (&p)[16]) {
-  float q[8], r[4];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) q[j] = p[j] + p[j + 8];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) r[j] = q[j] + q[j + 4];
-  float s0 = r[0] + r[2], s1 = r[1] + r[3];
-  return s0 + s1;
-}
+// layer (5120 .. 13824 columns): a row no longer fits in registers.  The lane mapping stays the
+// narrow kernels' -- 4 rows per wave, the 16 lanes of a row own the columns k = l + 16 s -- so the
+// SUM16 partials are one register per lane and bfly16 folds them: every value is bit-identical
+// to the register-resident kernels and to the oracle.  Instead of holding the row, each pass
+// STREAMS it: batches of 16 columns per lane (16 index loads, then 16 weight and 16 code loads
+// in flight, then the 16 sequential updates).  Lane groups of a wave read 4 adjacent rows of one
+// column (feature-major: 16 B of a line per row group, the rest of the line by the neighbouring
+// waves of the workgroup through L1) or 64 B of one row (row-major).  The codes live in the
+// output array T between passes.  Passes: sum(w); sum|w - mu|; init (writes T, also the first
+// grid's partials); one pass per ITF iteration (round + the next grid's partials); AGA; E.
+constexpr int WIDE_WAVES = 4;  // 16 rows per workgroup
 
 struct WideArgs {
   int mode;          // PT2Q_STAGE_* ; BLOCK = fused init+ITF+AGA+E of the block loop
@@ -610,243 +604,246 @@ constexpr int MODE_BLOCK = 100;
 template <bool FM>
 struct WideRow {
   const WideArgs& A;
-  int i;
+  int i, l;  // row (clamped to 0 when invalid: reads stay in range), residue class
   bool valid;
-  PT2Q_DEV long col(int k) const { return FM ? (long)A.blk[k] : (long)k; }
-  PT2Q_DEV float w(int k) const {
-    if (!valid) return 0.0f;
-    return FM ? A.W[col(k) * A.ldw + i] : A.W[(long)i * A.ldw + k];
+  PT2Q_DEV long woff(long c) const { return FM ? c * A.ldw + i : (long)i * A.ldw + c; }
+  PT2Q_DEV long toff(long c) const { return FM ? c * A.ldt + i : (long)i * A.ldt + c; }
+  PT2Q_DEV float t(long c) const {
+    return FM ? (float)((const int8_t*)A.T)[toff(c)] : ((const float*)A.T)[toff(c)];
   }
-  PT2Q_DEV float t(int k) const {
-    if (!valid) return 0.0f;
-    return FM ? (float)((const int8_t*)A.T)[col(k) * A.ldt + i] : ((const float*)A.T)[(long)i * A.ldt + k];
-  }
-  PT2Q_DEV void set_t(int k, float v) const {
+  PT2Q_DEV void set_t(long c, float v) const {
     if (!valid) return;
-    if (FM) ((int8_t*)A.T)[col(k) * A.ldt + i] = (int8_t)v;
-    else ((float*)A.T)[(long)i * A.ldt + k] = v;
+    if (FM) ((int8_t*)A.T)[toff(c)] = (int8_t)v;
+    else ((float*)A.T)[toff(c)] = v;
   }
-};
 
-// SUM16 over the row of one lane: f(k) gives the k-th term.
-template <typename F>
-PT2Q_DEV float wide_sum(int b, F&& f) {
-  float p[16];
+  // One streamed pass: f(k, c, w, t) for this lane's columns k = l + 16 s in s order (c = the
+  // storage column of k, w / t = 0 on an invalid row; t only with TC).
+  template <bool TC, typename F>
+  PT2Q_DEV void pass(F&& f) const {
+    const int b = A.b;
+    for (int k0 = 0; k0 < b; k0 += 256) {
+      long c[16];
+      float w[16], tv[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) p[j] = 0.0f;
-  int k0 = 0;
-  for (; k0 + 16 <= b; k0 += 16) {
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + 16 * u + l;
+        const int kc = k < b ? k : 0;
+        c[u] = FM ? (long)A.blk[kc] : (long)kc;
+      }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) p[j] = p[j] + f(k0 + j);
-  }
-  for (int j = 0; k0 + j < b; ++j) p[j] = p[j] + f(k0 + j);
-  return fold16(p);
-}
-
-struct Grid3 {
-  float wt[16], t[16], t2[16];
-  PT2Q_DEV void zero() {
+      for (int u = 0; u < 16; ++u) w[u] = A.W[woff(c[u])];
+      if constexpr (TC) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) wt[j] = t[j] = t2[j] = 0.0f;
-  }
-  PT2Q_DEV void add(int j, float w, float tv) {
-    wt[j] = wt[j] + w * tv;
-    t[j] = t[j] + tv;
-    t2[j] = t2[j] + tv * tv;
-  }
-};
-
-PT2Q_DEV void grid_from(const Grid3& G, float fb, float wsum, float* a, float* m) {
-  float swt = fold16(G.wt), ts = fold16(G.t), t2 = fold16(G.t2);
-  float den = clampmin(fb * t2 - ts * ts);
-  *a = (fb * swt - ts * wsum) / den;
-  *m = (t2 * wsum - ts * swt) / den;
-}
-
-template <bool FM>
-PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, int b, Grid3& G) {
-  G.zero();
-  int k0 = 0;
-  for (; k0 + 16 <= b; k0 += 16) {
+        for (int u = 0; u < 16; ++u) tv[u] = t(c[u]);
+      }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) G.add(j, R.w(k0 + j), R.t(k0 + j));
-  }
-  for (int j = 0; k0 + j < b; ++j) G.add(j, R.w(k0 + j), R.t(k0 + j));
-}
-
-// flexible_round over the row, writing T; accumulates the next grid's partials. Returns changed.
-template <bool FM>
-PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, int b, float a, float m, Grid3& G) {
-  const float as = clampmin(a);
-  const float ras = rcp_approx(as);
-  const bool rok = rcp_ok(as);
-  bool changed = false;
-  G.zero();
-  auto one = [&](int k, int j) {
-    float w = R.w(k), old = R.t(k);
-    float nt = round_code(w - m, as, ras, rok);
-    if (nt != old) {
-      changed = true;
-      R.set_t(k, nt);
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + 16 * u + l;
+        if (k < b) f(k, c[u], valid ? w[u] : 0.0f, TC && valid ? tv[u] : 0.0f);
+      }
     }
-    G.add(j, w, nt);
-  };
-  int k0 = 0;
-  for (; k0 + 16 <= b; k0 += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) one(k0 + j, j);
   }
-  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
-  return changed;
+};
+
+template <bool FM>
+PT2Q_DEV float wide_sum_w(const WideRow<FM>& R) {
+  float p = 0.0f;
+  R.template pass<false>([&](int, long, float w, float) { p = p + w; });
+  return bfly16(p);
 }
 
-// ternary_init; writes T. Returns whether the row's codes are all zero.
+// ternary_init (quantizer.py:32-69): writes T; also returns the first grid's sums (row_grid's
+// partials over the codes just written -- same values, same order).  Returns all-zero.
 template <bool FM>
-PT2Q_DEV bool wide_init(const WideRow<FM>& R, int b, float wsum, float* a, float* m) {
-  const float fb = (float)b;
+PT2Q_DEV bool wide_init(const WideRow<FM>& R, float wsum, float* a, float* m, float* g) {
+  const float fb = (float)R.A.b;
   const float mu = wsum / fb;
-  float delta = 0.75f * (wide_sum(b, [&](int k) { return fabsf(R.w(k) - mu); }) / fb);
-  float pn[16], pd[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) pn[j] = pd[j] = 0.0f;
-  auto one = [&](int k, int j) {
-    float wc = R.w(k) - mu;
-    float t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
-    R.set_t(k, t);
-    pn[j] = pn[j] + t * wc;
-    pd[j] = pd[j] + fabsf(t);
-  };
-  int k0 = 0;
-  for (; k0 + 16 <= b; k0 += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) one(k0 + j, j);
-  }
-  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
-  float num = fold16(pn), cnt = fold16(pd);
+  float p = 0.0f;
+  R.template pass<false>([&](int, long, float w, float) { p = p + fabsf(w - mu); });
+  const float delta = 0.75f * (bfly16(p) / fb);
+  float pn = 0.0f, pd = 0.0f, pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
+  R.template pass<false>([&](int, long c, float w, float) {
+    const float wc = w - mu;
+    const float t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
+    R.set_t(c, t);
+    pn = pn + t * wc;
+    pd = pd + fabsf(t);
+    pwt = pwt + w * t;
+    pt = pt + t;
+    pt2 = pt2 + t * t;
+  });
+  const float num = bfly16(pn), cnt = bfly16(pd);
+  g[0] = bfly16(pwt);
+  g[1] = bfly16(pt);
+  g[2] = bfly16(pt2);
   *a = num / clampmin(cnt);
   *m = mu;
   return cnt == 0.0f;
 }
 
+// build_optimal_grid (quantizer.py:71-108) from the folded sums
+PT2Q_DEV void wide_grid(const float* g, float fb, float wsum, float* a, float* m) {
+  const float den = clampmin(fb * g[2] - g[1] * g[1]);
+  *a = (fb * g[0] - g[1] * wsum) / den;
+  *m = (g[2] * wsum - g[1] * g[0]) / den;
+}
+
+// grid partials over the codes in T (the ITF stage entry without a preceding init pass)
 template <bool FM>
-PT2Q_DEV int wide_itf(const WideRow<FM>& R, int b, float wsum, int max_iter, float* a, float* m) {
-  Grid3 G;
-  wide_grid_pass(R, b, G);
+PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, float* g) {
+  float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
+  R.template pass<true>([&](int, long, float w, float t) {
+    pwt = pwt + w * t;
+    pt = pt + t;
+    pt2 = pt2 + t * t;
+  });
+  g[0] = bfly16(pwt);
+  g[1] = bfly16(pt);
+  g[2] = bfly16(pt2);
+}
+
+// flexible_round (quantizer.py:110-134) over the row, writing changed codes; accumulates the
+// next grid's sums into g.  Returns whether this lane changed a code.
+template <bool FM>
+PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, float a, float m, float* g) {
+  const float as = clampmin(a);
+  const float ras = rcp_approx(as);
+  const bool rok = rcp_ok(as);
+  bool changed = false;
+  float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
+  R.template pass<true>([&](int, long c, float w, float old) {
+    const float nt = round_code(w - m, as, ras, rok);
+    if (nt != old) {
+      changed = true;
+      R.set_t(c, nt);
+    }
+    pwt = pwt + w * nt;
+    pt = pt + nt;
+    pt2 = pt2 + nt * nt;
+  });
+  g[0] = bfly16(pwt);
+  g[1] = bfly16(pt);
+  g[2] = bfly16(pt2);
+  return changed;
+}
+
+// iterative_ternary_fitting (quantizer.py:136-175), wave-level stop as row_itf; g holds the
+// grid sums of the codes in T on entry.
+template <bool FM>
+PT2Q_DEV int wide_itf(const WideRow<FM>& R, float wsum, int max_iter, float* a, float* m, float* g) {
   int it = 0;
   bool any = true;
   for (; it < max_iter; ++it) {
     if (!any) break;
-    grid_from(G, (float)b, wsum, a, m);
-    bool ch = wide_round_pass(R, b, *a, *m, G);
+    wide_grid(g, (float)R.A.b, wsum, a, m);
+    const bool ch = wide_round_pass(R, *a, *m, g);
     any = __any(ch);
   }
   return it;
 }
 
+// activation_aware_grid_alignment (quantizer.py:177-248) given S1 and d
 template <bool FM>
-PT2Q_DEV void wide_aga(const WideRow<FM>& R, int b, const float* S1, float d, float* a, float* m) {
-  float pv[16], pws[16], pwts[16], pt2s[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) pv[j] = pws[j] = pwts[j] = pt2s[j] = 0.0f;
-  auto one = [&](int k, int j) {
-    float t = R.t(k), w = R.w(k), c = S1[k];
-    pv[j] = fmaf(t, c, pv[j]);
-    pws[j] = fmaf(w, c, pws[j]);
-    pwts[j] = fmaf(w * t, c, pwts[j]);
-    pt2s[j] = fmaf(t * t, c, pt2s[j]);
-  };
-  int k0 = 0;
-  for (; k0 + 16 <= b; k0 += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) one(k0 + j, j);
-  }
-  for (int j = 0; k0 + j < b; ++j) one(k0 + j, j);
-  float v = fold16(pv), ws1 = fold16(pws), wts1 = fold16(pwts), t2s1 = fold16(pt2s);
-  float v2 = v * v;
-  float den = clampmin(d * t2s1 - v2);
+PT2Q_DEV void wide_aga(const WideRow<FM>& R, const float* S1, float d, float* a, float* m) {
+  float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
+  R.template pass<true>([&](int k, long, float w, float t) {
+    const float c = S1[k];
+    pv = fmaf(t, c, pv);
+    pws = fmaf(w, c, pws);
+    pwts = fmaf(w * t, c, pwts);
+    pt2s = fmaf(t * t, c, pt2s);
+  });
+  const float v = bfly16(pv), ws1 = bfly16(pws), wts1 = bfly16(pwts), t2s1 = bfly16(pt2s);
+  const float v2 = v * v;
+  const float den = clampmin(d * t2s1 - v2);
   *a = (d * wts1 - v * ws1) / den;
   *m = (t2s1 * ws1 - v * wts1) / den;
 }
 
-// Block-loop mode for rows [row0, row0 + 64): init -> ITF -> AGA -> E.
 template <bool FM>
-PT2Q_DEV void wide_block_rows(const WideArgs& A, int row0, bool skip_itf, bool count_zero) {
+PT2Q_DEV WideRow<FM> wide_row(const WideArgs& A) {
   const int lane = threadIdx.x & 63;
-  WideRow<FM> R{A, row0 + lane, row0 + lane < A.n};
-  const int b = A.b;
-  float wsum = wide_sum(b, [&](int k) { return R.w(k); });
-  float a, m;
-  bool zero = wide_init(R, b, wsum, &a, &m);
-  if (count_zero && R.valid && zero) atomicAdd(&A.counters[0], 1);
-  int it = 0;
-  if (!skip_itf) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
-  if (A.S1) wide_aga(R, b, A.S1, *A.d, &a, &m);
-  if (A.iters && lane == 0 && !skip_itf) atomicMax(A.iters, it);
-  if (!R.valid) return;
-  A.alpha[R.i] = a;
-  A.mu[R.i] = m;
-  if (A.Et)
-    for (int k = 0; k < b; ++k) A.Et[(long)k * A.lde + R.i] = R.w(k) - (a * R.t(k) + m);
+  const int i = ((int)blockIdx.x * WIDE_WAVES + (int)(threadIdx.x >> 6)) * 4 + (lane >> 4);
+  const bool valid = i < A.n;
+  return WideRow<FM>{A, valid ? i : 0, lane & 15, valid};
 }
 
-// One wave (64 rows) per workgroup: few rows per layer, so spread them over CUs.
+// Block-loop mode for this wave's 4 rows: init -> ITF -> AGA -> E.
 template <bool FM>
-__global__ __launch_bounds__(64) void atq_wide_block_kernel(WideArgs A) {
-  wide_block_rows<FM>(A, blockIdx.x * 64, false, true);
+PT2Q_DEV void wide_block_rows(const WideArgs& A, bool skip_itf, bool count_zero) {
+  const WideRow<FM> R = wide_row<FM>(A);
+  const float wsum = wide_sum_w(R);
+  float a, m, g[3];
+  const bool zero = wide_init(R, wsum, &a, &m, g);
+  if (count_zero && R.valid && R.l == 0 && zero) atomicAdd(&A.counters[0], 1);
+  int it = 0;
+  if (!skip_itf) it = wide_itf(R, wsum, A.max_iter, &a, &m, g);
+  if (A.S1) wide_aga(R, A.S1, *A.d, &a, &m);
+  if (A.iters && (threadIdx.x & 63) == 0 && !skip_itf) atomicMax(A.iters, it);
+  if (!R.valid) return;
+  if (R.l == 0) {
+    A.alpha[R.i] = a;
+    A.mu[R.i] = m;
+  }
+  if (A.Et)
+    R.template pass<true>([&](int k, long, float w, float t) { A.Et[(long)k * A.lde + R.i] = w - (a * t + m); });
+}
+
+template <bool FM>
+__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_block_kernel(WideArgs A) {
+  wide_block_rows<FM>(A, false, true);
 }
 
 // whole-block T_init == 0 repair after the kernel boundary (see atq_zero_fixup_kernel)
 template <bool FM>
-__global__ __launch_bounds__(64) void atq_wide_zero_fixup_kernel(WideArgs A) {
+__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_zero_fixup_kernel(WideArgs A) {
   if (A.counters[0] != A.n) return;
   if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
-  wide_block_rows<FM>(A, blockIdx.x * 64, true, false);
+  wide_block_rows<FM>(A, true, false);
 }
 
 // Per-method stages on row-major W / float T (quantizer.py surface) for b > 512.
-__global__ __launch_bounds__(64) void atq_wide_stage_kernel(WideArgs A) {
-  const int lane = threadIdx.x & 63;
-  WideRow<false> R{A, (int)blockIdx.x * 64 + lane, (int)blockIdx.x * 64 + lane < A.n};
-  const int b = A.b;
-  float wsum = wide_sum(b, [&](int k) { return R.w(k); });
-  float a = R.valid ? A.alpha[R.i] : 0.0f, m = R.valid ? A.mu[R.i] : 0.0f;
+__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_stage_kernel(WideArgs A) {
+  const WideRow<false> R = wide_row<false>(A);
+  const float wsum = wide_sum_w(R);
+  float a = R.valid ? A.alpha[R.i] : 0.0f, m = R.valid ? A.mu[R.i] : 0.0f, g[3];
   int it = 0;
   bool write_am = true;
   switch (A.mode) {
     case PT2Q_STAGE_INIT:
-      wide_init(R, b, wsum, &a, &m);
+      wide_init(R, wsum, &a, &m, g);
       break;
-    case PT2Q_STAGE_GRID: {
-      Grid3 G;
-      wide_grid_pass(R, b, G);
-      grid_from(G, (float)b, wsum, &a, &m);
+    case PT2Q_STAGE_GRID:
+      wide_grid_pass(R, g);
+      wide_grid(g, (float)A.b, wsum, &a, &m);
       break;
-    }
-    case PT2Q_STAGE_ROUND: {
-      Grid3 G;
-      wide_round_pass(R, b, a, m, G);
+    case PT2Q_STAGE_ROUND:
+      wide_round_pass(R, a, m, g);
       write_am = false;
       break;
-    }
     case PT2Q_STAGE_ITF:
-      if (*A.counters != A.n) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
+      if (*A.counters != A.n) {
+        wide_grid_pass(R, g);
+        it = wide_itf(R, wsum, A.max_iter, &a, &m, g);
+      }
       break;
     case PT2Q_STAGE_AGA:
-      wide_aga(R, b, A.S1, *A.d, &a, &m);
+      wide_aga(R, A.S1, *A.d, &a, &m);
       break;
     case PT2Q_STAGE_FULL: {
-      bool zero = wide_init(R, b, wsum, &a, &m);
+      const bool zero = wide_init(R, wsum, &a, &m, g);
       if (A.pass == 0) {
-        if (R.valid && zero) atomicAdd(A.counters, 1);
+        if (R.valid && R.l == 0 && zero) atomicAdd(A.counters, 1);
         return;
       }
-      if (*A.counters != A.n) it = wide_itf(R, b, wsum, A.max_iter, &a, &m);
-      if (A.S1) wide_aga(R, b, A.S1, *A.d, &a, &m);
+      if (*A.counters != A.n) it = wide_itf(R, wsum, A.max_iter, &a, &m, g);
+      if (A.S1) wide_aga(R, A.S1, *A.d, &a, &m);
       break;
     }
   }
-  if (A.iters && lane == 0) atomicMax(A.iters, it);
-  if (R.valid && write_am) {
+  if (A.iters && (threadIdx.x & 63) == 0) atomicMax(A.iters, it);
+  if (R.valid && R.l == 0 && write_am) {
     A.alpha[R.i] = a;
     A.mu[R.i] = m;
   }
@@ -876,9 +873,10 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
-    hipLaunchKernelGGL(atq_wide_block_kernel<true>, dim3(ceil_div(n, 64)), dim3(64), 0, st, WA);
+    const int wgrid = ceil_div(n, 4 * WIDE_WAVES);
+    hipLaunchKernelGGL(atq_wide_block_kernel<true>, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<true>, dim3(ceil_div(n, 64)), dim3(64), 0, st, WA);
+    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<true>, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
     if (Hinv && nr > 0) return pt2q_launch_ef_coeffs(Hinv, ldh, blk, b, rem, nr, C, ldc, st);
     return PT2Q_OK;
@@ -932,14 +930,14 @@ extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int 
   if (b > 512) {
     WideArgs WA{mode, Wp, ldw, n, b, nullptr, S1, d_dev, max_iter, alpha, mu, T,
                 ldt, nullptr, 0, iters_dev, zero_rows, 0};
-    const int wgrid = ceil_div(n, 64);
+    const int wgrid = ceil_div(n, 4 * WIDE_WAVES);
     if (mode == PT2Q_STAGE_FULL) {
       if (hipMemsetAsync(zero_rows, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
-      hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64), 0, st, WA);
+      hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
       PT2Q_LAUNCH_CHECK();
       WA.pass = 1;
     }
-    hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64), 0, st, WA);
+    hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }
