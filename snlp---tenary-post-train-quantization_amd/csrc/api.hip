@@ -33,6 +33,7 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_CHOL_PANEL", t.chol_panel);
   getb("PT2Q_CHOL_LOOKAHEAD", t.chol_lookahead);
   getb("PT2Q_WBAR_FUSED", t.wbar_fused);
+  getb("PT2Q_SIM_SPLIT", t.sim_split);
   geti("PT2Q_GEMMX_STAGES", t.gemmx_stages);
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);

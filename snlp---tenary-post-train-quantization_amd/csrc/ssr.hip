@@ -279,6 +279,80 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
   if (t == 0) sim[e] = p;
 }
 
+// Columns of 4096 < n <= 16384 rows (n % 4 == 0): S = ceil(n / 4096) waves per column, wave s
+// holding the float4s u in [16 s, 16 s + 16) of lane t (elements {256u + 4t + q}) in registers,
+// so the whole column is loaded at once with 16 float4 per lane (~110 VGPRs: 4 waves per SIMD,
+// where one wave holding all 48 needs 256 VGPRs and runs alone on its SIMD).  Each lane's chain
+// continues across the waves in s order through LDS -- the per-lane order of ssr_sim_kernel<48>
+// -- and wave S-1 folds it (bfly64): the same bits.
+template <int S>
+__global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, long ldw, int n, const int* rem,
+                                                               int r, const float* wn, float* sim, long zs) {
+  __shared__ float part[64];
+  __shared__ float njs;
+  Wt = zws(Wt, zs);
+  rem = zws(rem, zs);
+  wn = zws(wn, zs);
+  sim = zws(sim, zs);
+  const int e = blockIdx.x;
+  const int s = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const float* x = Wt + (long)rem[e] * ldw;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 v[16], w[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const long base = 4 * t + 256 * (16 * s + u);
+    if (base < n) v[u] = *(const f4*)(x + base);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const long base = 4 * t + 256 * (16 * s + u);
+    if (base < n) w[u] = *(const f4*)(wn + base);
+  }
+  float ss = 0.0f;
+  for (int q = 0; q < S; ++q) {
+    if (s == q) {
+      if (q > 0) ss = part[t];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (4 * t + 256 * (16 * s + u) < n) {
+          ss = fmaf(v[u][0], v[u][0], ss);
+          ss = fmaf(v[u][1], v[u][1], ss);
+          ss = fmaf(v[u][2], v[u][2], ss);
+          ss = fmaf(v[u][3], v[u][3], ss);
+        }
+      if (q < S - 1) part[t] = ss;
+    }
+    __syncthreads();
+  }
+  if (s == S - 1) {
+    const float tot = bfly64(ss);
+    if (t == 0) njs = clampmin(sqrtf(tot));
+  }
+  __syncthreads();
+  const float nj = njs;
+  float p = 0.0f;
+  for (int q = 0; q < S; ++q) {
+    if (s == q) {
+      if (q > 0) p = part[t];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (4 * t + 256 * (16 * s + u) < n) {
+          p = fmaf(v[u][0] / nj, w[u][0], p);
+          p = fmaf(v[u][1] / nj, w[u][1], p);
+          p = fmaf(v[u][2] / nj, w[u][2], p);
+          p = fmaf(v[u][3] / nj, w[u][3], p);
+        }
+      if (q < S - 1) part[t] = p;
+    }
+    __syncthreads();
+  }
+  if (s == S - 1) {
+    p = bfly64(p);
+    if (t == 0) sim[e] = p;
+  }
+}
+
 PT2Q_DEV uint32_t orderable(float f) {
   uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -799,10 +873,16 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
       PT2Q_LAUNCH_CHECK();
     }
   }
-  const bool v4 = (n & 3) == 0 && (ldw & 3) == 0;
-  auto sim_k = !v4 ? ssr_sim_kernel<0> : n <= 4096 ? ssr_sim_kernel<16> : n <= 12288 ? ssr_sim_kernel<48>
-                                                                                   : ssr_sim_kernel<0>;
-  hipLaunchKernelGGL(sim_k, dim3(ceil_div(r, 4), 1, nz), dim3(256), 0, st, Wt, ldw, n, rem, r, wn, sim, zs);
+  const bool v4 = (n & 3) == 0 && (ldw & 3) == 0 && (uintptr_t)Wt % 16 == 0;
+  const int S = ceil_div(n, 4096);
+  if (v4 && n > 4096 && n <= 16384 && pt2q_tuning().sim_split) {
+    auto k = S == 2 ? ssr_sim_split_kernel<2> : S == 3 ? ssr_sim_split_kernel<3> : ssr_sim_split_kernel<4>;
+    hipLaunchKernelGGL(k, dim3(r, 1, nz), dim3(64 * S), 0, st, Wt, ldw, n, rem, r, wn, sim, zs);
+  } else {
+    auto sim_k = !v4 ? ssr_sim_kernel<0> : n <= 4096 ? ssr_sim_kernel<16> : n <= 12288 ? ssr_sim_kernel<48>
+                                                                                     : ssr_sim_kernel<0>;
+    hipLaunchKernelGGL(sim_k, dim3(ceil_div(r, 4), 1, nz), dim3(256), 0, st, Wt, ldw, n, rem, r, wn, sim, zs);
+  }
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
