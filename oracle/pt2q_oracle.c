@@ -265,8 +265,21 @@ int orc_atq_quantize(const float* W, long ldw, int n, int b, int aga, const floa
 
 /* ---------------------------------------------------------------- SSR (reorder.py) */
 
+/* The w-bar partial of one chunk of 128 rem entries v[0..128) (+0 past r): the order the
+ * error-feedback tile that wrote them forms it in (DESIGN.md §3 CHUNK128):
+ * x_l = v[l] + v[l+32], y_l = v[64+l] + v[96+l] (l < 32), X = butterfly32(x), Y = butterfly32(y),
+ * partial = X + Y. */
+float orc_wbar_chunk(const float* v) {
+  float x[32], y[32];
+  for (int l = 0; l < 32; ++l) {
+    x[l] = v[l] + v[l + 32];
+    y[l] = v[64 + l] + v[96 + l];
+  }
+  return butterfly(x, 32) + butterfly(y, 32);
+}
+
 /* compute_column_similarity_to_mean reorder.py:36-61 on Wt (feature-major, m x ldw).
- * wbar = chunked sum (chunks of 128 rem entries, each k-ascending; chunks summed ascending)
+ * wbar = chunked sum (chunks of 128 rem entries, each orc_wbar_chunk; chunks summed ascending)
  * / r; nw = sqrt(SUMN fma w²); wn = wbar / clamp(nw); per column: nj = sqrt(SUMN fma x²),
  * s = SUMN fma (x / clamp(nj)) * wn. */
 void orc_ssr_similarity(const float* Wt, long ldw, int n, const int64_t* rem, int r,
@@ -277,10 +290,9 @@ void orc_ssr_similarity(const float* Wt, long ldw, int n, const int64_t* rem, in
   for (int i = 0; i < n; ++i) {
     float t = 0.0f;
     for (int c0 = 0; c0 < r; c0 += 128) {
-      float p = 0.0f;
-      int c1 = (c0 + 128 < r) ? c0 + 128 : r;
-      for (int e = c0; e < c1; ++e) p = p + Wt[rem[e] * ldw + i];
-      t = t + p;
+      float v[128];
+      for (int j = 0; j < 128; ++j) v[j] = (c0 + j < r) ? Wt[rem[c0 + j] * ldw + i] : 0.0f;
+      t = t + orc_wbar_chunk(v);
     }
     tot[i] = t / (float)r;
   }

@@ -34,6 +34,7 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_CHOL_LOOKAHEAD", t.chol_lookahead);
   getb("PT2Q_WBAR_FUSED", t.wbar_fused);
   getb("PT2Q_SIM_SPLIT", t.sim_split);
+  getb("PT2Q_EF_WBAR", t.ef_wbar);
   geti("PT2Q_GEMMX_STAGES", t.gemmx_stages);
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);
@@ -99,6 +100,14 @@ struct BlockWs {
   float* hS;
   long ldw;
 };
+
+// Whether the error feedback may hand the next block's SSR its w-bar partials (ef.hip / ssr.hip
+// pre path: the fused w-bar launch's conditions; PT2Q_EF_WBAR=0 keeps the separate pass).
+inline bool ef_wbar_ok(int n, long ldw, const float* Wt) {
+  const Pt2qTuning& t = pt2q_tuning();
+  return t.ef_wbar && t.wbar_fused && t.ef_kernel && n <= 16384 && n % 4 == 0 && ldw % 4 == 0 &&
+         (uintptr_t)Wt % 16 == 0;
+}
 
 // variant G's AGA matrix for blocks wider than one workgroup's LDS holds (> 128 columns)
 inline bool hess_wide(int flags, int bb) { return (flags & PT2Q_AGA_MASK) == PT2Q_AGA_HESS && bb > 128; }
@@ -196,6 +205,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   float* wn = part + (size_t)ceil_div(m, 128) * n;
   float* sim = wn + n;
   int processed = 0, r = m, cur = 0;
+  bool pre = false;  // part holds rem's w-bar partials (from the previous block's error feedback)
   for (int k = 0; k < B; ++k) {
     const int bs = r < b ? r : b;
     const int nr = r - bs;
@@ -207,8 +217,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     const bool s1_in_topk = !s1_in_atq && ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
     if (ssr) {
       if (r > b) {
-        if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B)) !=
-            PT2Q_OK)
+        if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B,
+                                             nullptr, pre)) != PT2Q_OK)
           return rc;
         if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm + processed, st,
                                        s1_in_topk ? A : nullptr, lda, w.S1, w.d,
@@ -239,10 +249,12 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
                                     s1_in_atq ? A : nullptr, lda,
                                     s1_in_atq ? w.counters + 2 * B + 2 * k : nullptr, w.status)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
+    const bool want = ssr && nr > b && ef_wbar_ok(n, w.ldw, w.Wt);  // the next block runs SSR over nrem
     rc = (nr > 0 && pt2q_tuning().ef_kernel)
-             ? pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st)
+             ? pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, nullptr, want ? part : nullptr, n)
              : PT2Q_E_UNSUPPORTED;
     if (rc != PT2Q_OK && rc != PT2Q_E_UNSUPPORTED) return rc;
+    pre = want && rc == PT2Q_OK;
     if (nr > 0 && rc == PT2Q_E_UNSUPPORTED) {
       GemmDesc g{};
       g.M = nr; g.N = n; g.K = bs;
@@ -311,14 +323,15 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
   float* wn = part + (size_t)ceil_div(m, 128) * n;
   float* sim = wn + n;
   int processed = 0, r = m, cur = 0;
+  bool pre = false;  // part holds rem's w-bar partials (from the previous block's error feedback)
   for (int k = 0; k < B; ++k) {
     const int bs = r < b ? r : b;
     const int nr = r - bs;
     int* rem = w.rem[cur];
     int* nrem = w.rem[cur ^ 1];
     if (ssr && r > b) {
-      if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B, &g)) !=
-          PT2Q_OK)
+      if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B, &g,
+                                           pre)) != PT2Q_OK)
         return rc;
       if ((rc = pt2q_launch_ssr_topk(sim, rem, r, b, w.blk, nrem, perm64 + processed, st, nullptr, 0, nullptr,
                                      nullptr, nullptr, w.status, &g)) != PT2Q_OK)
@@ -334,8 +347,11 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
                                     Hinv[0], ldhi, nrem, nr, w.Ck, m, w.iters_part, act ? A[0] : nullptr, lda,
                                     act ? w.counters + 2 * B + 2 * k : nullptr, w.status, &g)) != PT2Q_OK)
       return rc;
-    if (nr > 0 && (rc = pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, &g)) != PT2Q_OK)
+    const bool want = ssr && nr > b && ef_wbar_ok(n, w.ldw, w.Wt);  // the next block runs SSR over nrem
+    if (nr > 0 && (rc = pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, &g,
+                                       want ? part : nullptr, n)) != PT2Q_OK)
       return rc;
+    pre = want && nr > 0;
     processed += bs;
     r = nr;
     cur ^= 1;

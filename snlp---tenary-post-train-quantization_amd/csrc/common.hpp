@@ -108,6 +108,7 @@ struct Pt2qTuning {
   bool chol_lookahead = true;  // PT2Q_CHOL_LOOKAHEAD=0: the trailing updates on the main stream only
   int chol_panel = 0;          // PT2Q_CHOL_PANEL: rows per rank-P Cholesky update (0: by m)
   bool wbar_fused = true;      // PT2Q_WBAR_FUSED=0: three SSR-mean launches
+  bool ef_wbar = true;         // PT2Q_EF_WBAR=0: the SSR mean pass reads W again (no EF partials)
   bool sim_split = true;       // PT2Q_SIM_SPLIT=0: one wave per column for n > 4096 (256 VGPRs)
   int gemmx_stages = 2;        // PT2Q_GEMMX_STAGES: LDS stages of the f32 chain GEMM (2: 64 KiB, 2 WGs per CU;
                                // batched inverse 596 -> 534 ms per 7B step vs 3)

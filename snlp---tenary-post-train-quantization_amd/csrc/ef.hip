@@ -12,6 +12,13 @@
 // Every wave issues the same number of memory instructions per tile (out-of-range rows and
 // columns go through buffer ops with offsets past the end, which the hardware drops), so the
 // hand-counted s_waitcnt vmcnt values below are exact.
+//
+// With a partial buffer the epilogue also forms the NEXT block's SSR mean partials (the w-bar of
+// ssr.hip over the rows just written, crow = the next block's rem): a tile's 128 rows e are
+// exactly one w-bar chunk, so per column i its new values are folded in registers -- rows e and
+// e + 32 of a lane added, a butterfly over the 32 lanes (xor 16 by ds_swizzle, then bfly16), the
+// two waves of a column half combined through LDS -- the CHUNK128 order of DESIGN.md §3.  That
+// removes the separate w-bar pass over W[:, rem] (one full read per block).
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -40,8 +47,10 @@ struct EfArgs {
   long ldw;
   const int* crow;  // rem (nr entries)
   int nr, bs, te, ti, ntile, nh;
-  long zs;          // grouped: bytes between the linears' workspace slices (Ck, Et, Wt, crow)
+  long zs;          // grouped: bytes between the linears' workspace slices (Ck, Et, Wt, crow, part)
   int nz;           // linears; the work line is nz * ntile tiles, linear-major
+  float* part;      // nullable: w-bar chunk partials part[c][i] of the updated rows, i < n
+  int n;
 };
 
 // The arguments of linear z (its workspace slice).
@@ -52,6 +61,7 @@ PT2Q_DEV EfArgs ef_linear(const EfArgs& a0, int z) {
   a.Et = (const float*)((const char*)a0.Et + o);
   a.Wt = (float*)((char*)a0.Wt + o);
   a.crow = (const int*)((const char*)a0.crow + o);
+  if (a0.part) a.part = (float*)((char*)a0.part + o);
   return a;
 }
 
@@ -205,14 +215,70 @@ struct EfIO {
 PT2Q_DEV void ef_vmcnt(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
     case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
   }
 }
 
-__global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) {
+constexpr int EF_PS = 8;  // w-bar partial stores per wave per tile (float4; dropped where unused)
+
+// xor-16 lane exchange inside each 32-lane half (ds_swizzle bitmask mode: and 0x1f, xor 0x10)
+PT2Q_DEV float ef_xor16(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+}
+
+// The w-bar partials of tile (e0, i0) from its new values (see the file header): every wave
+// issues exactly EF_PS buffer stores (real ones: lanes 0 and 32 of the row-half-0 waves, i < n).
+PT2Q_DEV void ef_wbar(const EfArgs& a, __amdgpu_buffer_rsrc_t rp, int e0, int i0, const int (&wrow)[2],
+                      const u32x4 (&pend)[EF_CV], float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const int h = lane >> 5;
+  float x[2][4][4];
+#pragma unroll
+  for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float v0 = wrow[0] >= 0 ? __uint_as_float(pend[rn * 4 + q][u]) : 0.0f;
+        const float v1 = wrow[1] >= 0 ? __uint_as_float(pend[(2 + rn) * 4 + q][u]) : 0.0f;
+        float v = v0 + v1;
+        v = v + ef_xor16(v);
+        x[rn][q][u] = bfly16(v);
+      }
+  if (wr == 1 && (lane & 31) == 0) {
+#pragma unroll
+    for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) red[wc * 64 + rn * 32 + 8 * q + 4 * h + u] = x[rn][q][u];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const bool mine = wr == 0 && (lane & 31) == 0;
+  const int c = e0 / EF_T;
+#pragma unroll
+  for (int rn = 0; rn < 2; ++rn)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int il = wc * 64 + rn * 32 + 8 * q + 4 * h;
+      const int i = i0 + il;
+      f32x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = mine ? x[rn][q][u] + red[il + u] : 0.0f;
+      const unsigned off = (mine && i < a.n) ? (unsigned)(((long)c * a.n + i) * 4) : EF_DROP;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rp, off, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, long part_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
+  __shared__ float red[128];  // w-bar partials of the row-half-1 waves (ef_wbar)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   const int total = a0.ntile * a0.nz;
   int t = blockIdx.x;
@@ -225,6 +291,8 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
     i0 = (tl % a0.ti) * EF_T;
   };
   auto rsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000); };
+  auto prsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)part_bytes, 0x00020000); };
+  const int P = a0.part ? EF_PS : 0;  // part stores per tile, younger than the tile's stages
   EfArgs a;
   int e0, i0, wrow[2];
   corner(t, a, e0, i0);
@@ -234,6 +302,8 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
   ef_rows(a, e0, wrow);
   ef_stage(a, e0, i0, 0, smem);
   if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
+  // P dropped stores: every tile's first wait then sees the same count of younger operations
+  for (int j = 0; j < P; ++j) __builtin_amdgcn_raw_buffer_store_b128(u32x4{}, rc, EF_DROP, 0, 0);
   int prow[2] = {-1, -1}, pi0 = 0;
   u32x4 c[EF_CV], pend[EF_CV];
 #pragma unroll
@@ -252,7 +322,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
       for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
-    ef_vmcnt(S1);  // stage 0 landed (younger: stage 1)
+    ef_vmcnt(S1 + P);  // stage 0 landed (younger: stage 1, the previous tile's part stores)
     asm volatile("s_barrier" ::: "memory");
     if (more) ef_rows(an, en, nrow);
     {
@@ -262,7 +332,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
     if (more) ef_stage(an, en, in, 0, smem);
     if (a.nh == 2) {
-      ef_vmcnt(2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
+      ef_vmcnt(P + 2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
       asm volatile("s_barrier" ::: "memory");
       EfNoIO nio;
       F.half(lds0 + EF_STAGE, nio);
@@ -281,6 +351,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
           for (int u = 0; u < 4; ++u)
             pend[j][u] = __float_as_uint(__uint_as_float(c[j][u]) - F.acc[rm][rn][4 * q + u]);
         }
+    if (P) ef_wbar(a, prsrc(a), e0, i0, wrow, pend, red);
     prow[0] = wrow[0];
     prow[1] = wrow[1];
     pi0 = i0;
@@ -304,19 +375,22 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes) 
 // Wt[crow[e]][i] -= sum_k Ck[k][e] * Et[k][i] for e < nr, i < ldw (the padding columns of Wt
 // beyond n are scratch), k < bs <= 128.  Wt has wt_rows rows of ldw floats.
 int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
-                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp) {
+                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp, float* part, int n) {
   if (nr <= 0) return PT2Q_OK;
   const long wt_bytes = wt_rows * ldw * 4;
+  const long part_bytes = part ? (long)ceil_div(nr, EF_T) * n * 4 : 0;
   if (bs <= 0 || bs > 2 * EF_KH || ldw % 4 || ldk % 4 || (uintptr_t)Ck % 16 || (uintptr_t)Et % 16 ||
       (uintptr_t)Wt % 16 || wt_bytes >= (long)EF_DROP || wt_rows > 65536)
     return PT2Q_E_UNSUPPORTED;
+  if (part && (n <= 0 || n % 4 || n > ldw || (uintptr_t)part % 16 || part_bytes >= (long)EF_DROP))
+    return PT2Q_E_UNSUPPORTED;
   EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1,
-           grp ? grp->ws : 0l, (int)grp_z(grp)};
+           grp ? grp->ws : 0l, (int)grp_z(grp), part, n};
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::min(a.ntile * a.nz, cus);
-  hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes);
+  hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes, part_bytes);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

@@ -40,9 +40,11 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
 
 // ---- SSR / selection (ssr.hip)
 // cnt (nullable): pt2q_ssr_counter_ints(n) zeroed ints -> one fused wbar launch (self-resetting)
+// pre: part already holds the chunk partials of rem (written by the error feedback of the previous
+// block, pt2q_launch_ef with part); only their sum and the norm remain (needs the fused path)
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
                                float* part, float* wn, float* sim, hipStream_t st, int* cnt = nullptr,
-                               const Grp* grp = nullptr);
+                               const Grp* grp = nullptr, bool pre = false);
 inline int pt2q_ssr_counter_ints(int n) { return (n + 255) / 256 + 1; }
 int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* blk, int* newrem,
                          int64_t* perm_out, hipStream_t st, const float* G = nullptr, long ldg = 0,
@@ -80,8 +82,11 @@ struct GemmDesc {
 };
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
 // block error feedback Wt[crow[e]][i] -= sum_k Ck[k][e] Et[k][i] (ef.hip); E_UNSUPPORTED if bs > 128
+// part (nullable): also the w-bar chunk partials of the updated rows, part[c][i] for i < n (the
+// next block's SSR mean over crow, ssr.hip wbar_chunk order)
 int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long ldw, long wt_rows,
-                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp = nullptr);
+                   const int* crow, int nr, int bs, hipStream_t st, const Grp* grp = nullptr,
+                   float* part = nullptr, int n = 0);
 // two independent f32 GEMMs in one launch (either may be empty)
 // dA != nullptr: also factor the diagonal block (dp0, dp0) of dA (nb dnb) in the same launch if
 // g0's first tile is that block; *fused reports whether it did (else launch the factor).

@@ -16,7 +16,46 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int CHUNK = 128;  // canonical wbar chunk (rem entries per partial sum)
 
-// part[c][i] = sum over rem[c*128 .. c*128+127] (ascending) of Wt[rem[e]][i]
+PT2Q_DEV constexpr int brev5(int k) {
+  return ((k & 1) << 4) | ((k & 2) << 2) | (k & 4) | ((k & 8) >> 2) | ((k & 16) >> 4);
+}
+
+// Half of a chunk's w-bar partial (DESIGN.md §3 CHUNK128): butterfly32 over x_l = v[o+l] + v[o+l+32],
+// evaluated as a pairwise stack over the leaves in bit-reversed order (the butterfly's tree),
+// 8 leaves' loads in flight at a time.  ld(j) = v[j] (zero past the chunk's end).
+template <typename V, typename LD>
+PT2Q_DEV V wbar_half(LD&& ld, int o) {
+  V acc[6];
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 8) {
+    V a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = ld(o + brev5(k0 + u));
+      b[u] = ld(o + brev5(k0 + u) + 32);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      V v = a[u] + b[u];
+      int lvl = 0;
+#pragma unroll
+      for (; lvl < 5 && ((k >> lvl) & 1); ++lvl) v = acc[lvl] + v;
+      acc[lvl] = v;
+    }
+  }
+  return acc[5];
+}
+
+// The w-bar partial of one chunk: X + Y (X over entries 0..63, Y over 64..127) -- the order the
+// error-feedback tile that last wrote these columns forms it in (ef.hip), oracle orc_wbar_chunk.
+template <typename V, typename LD>
+PT2Q_DEV V wbar_chunk(LD&& ld) {
+  const V x = wbar_half<V>(ld, 0);
+  return x + wbar_half<V>(ld, 64);
+}
+
+// part[c][i] = wbar_chunk over rem[c*128 .. c*128+127] of Wt[rem[e]][i]
 __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, long ldw, int n,
                                                                const int* rem, int r,
                                                                float* part) {
@@ -27,17 +66,7 @@ __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, 
   __syncthreads();
   const int i = blockIdx.y * 256 + threadIdx.x;
   if (i >= n) return;
-  float p = 0.0f;
-  int e = 0;
-  for (; e + 8 <= cnt; e += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = Wt[rows[e + u] + i];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) p = p + v[u];
-  }
-  for (; e < cnt; ++e) p = p + Wt[rows[e] + i];
-  part[(long)c * n + i] = p;
+  part[(long)c * n + i] = wbar_chunk<float>([&](int j) { return j < cnt ? Wt[rows[j] + i] : 0.0f; });
 }
 
 // The three wbar steps in one launch (n <= 16384, n % 4 == 0): every workgroup (one wave: 256
@@ -50,7 +79,7 @@ __global__ __launch_bounds__(256) void ssr_wbar_partial_kernel(const float* Wt, 
 // last arrivers put them back to zero.
 __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, long ldw, int n,
                                                              const int* rem, int r, float* part,
-                                                             float* wn, int* cnt, long zs) {
+                                                             float* wn, int* cnt, long zs, int pre) {
   __shared__ long rows[CHUNK];
   Wt = zws(Wt, zs);  // grouped launch: linear blockIdx.z's slice
   rem = zws(rem, zs);
@@ -58,33 +87,29 @@ __global__ __launch_bounds__(256) void ssr_wbar_fused_kernel(const float* Wt, lo
   wn = zws(wn, zs);
   cnt = zws(cnt, zs);
   __shared__ int last;
-  const int c = blockIdx.x, nchunks = gridDim.x, nsl = gridDim.y;
+  const int c = blockIdx.x, nchunks = (r + CHUNK - 1) / CHUNK, nsl = gridDim.y;
   const int e0 = c * CHUNK, ce = min(r, e0 + CHUNK) - e0;
-  for (int e = threadIdx.x; e < ce; e += blockDim.x) rows[e] = (long)rem[e0 + e] * ldw;
-  __syncthreads();
+  if (!pre) {
+    for (int e = threadIdx.x; e < ce; e += blockDim.x) rows[e] = (long)rem[e0 + e] * ldw;
+    __syncthreads();
+  }
   // four consecutive rows i per thread (float4; n % 4 == 0), each its own chain over e
   typedef float f4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(part, 0, nchunks * n * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(wn, 0, n * 4, 0x00020000);
   const int i = (blockIdx.y * blockDim.x + threadIdx.x) * 4;
-  if (i < n) {
-    f4 p = {0.0f, 0.0f, 0.0f, 0.0f};
-    int e = 0;
-    for (; e + 16 <= ce; e += 16) {  // 16 loads in flight per lane
-      f4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = *(const f4*)(Wt + rows[e + u] + i);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) p = p + v[u];
+  if (!pre) {  // (pre: the partials came from the error feedback that wrote these columns)
+    if (i < n) {
+      const f4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+      const f4 p = wbar_chunk<f4>([&](int j) { return j < ce ? *(const f4*)(Wt + rows[j] + i) : z; });
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, p), rp, (c * n + i) * 4, 0, 16);  // sc1
     }
-    for (; e < ce; ++e) p = p + *(const f4*)(Wt + rows[e] + i);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, p), rp, (c * n + i) * 4, 0, 16);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(cnt + blockIdx.y, 1) == nchunks - 1;
+    __syncthreads();
+    if (!last) return;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(cnt + blockIdx.y, 1) == nchunks - 1;
-  __syncthreads();
-  if (!last) return;
   if (i < n) {
     f4 t = {0.0f, 0.0f, 0.0f, 0.0f};
     int k = 0;
@@ -845,7 +870,7 @@ size_t pt2q_ssr_scratch_floats(int n, int m) {
 
 int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem, int r,
                                float* part, float* wn, float* sim, hipStream_t st, int* cnt,
-                               const Grp* grp) {
+                               const Grp* grp, bool pre) {
   if (r <= 0 || n <= 0) return PT2Q_E_ARG;
   if ((size_t)(n + 1) * sizeof(float) > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   int nchunks = ceil_div(r, CHUNK);
@@ -853,10 +878,10 @@ int pt2q_launch_ssr_similarity(const float* Wt, long ldw, int n, const int* rem,
   const long zs = grp ? grp->ws : 0;
   const bool fused = cnt && n <= 16384 && n % 4 == 0 && ldw % 4 == 0 && (uintptr_t)Wt % 16 == 0 &&
                      pt2q_tuning().wbar_fused;
-  if (nz > 1 && !fused) return PT2Q_E_UNSUPPORTED;  // grouped launches use the fused w-bar only
+  if ((nz > 1 || pre) && !fused) return PT2Q_E_UNSUPPORTED;  // grouped launches use the fused w-bar only
   if (fused) {
-    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(nchunks, ceil_div(n, 256), nz), dim3(64), 0, st, Wt, ldw,
-                       n, rem, r, part, wn, cnt, zs);
+    hipLaunchKernelGGL(ssr_wbar_fused_kernel, dim3(pre ? 1 : nchunks, ceil_div(n, 256), nz), dim3(64), 0, st, Wt,
+                       ldw, n, rem, r, part, wn, cnt, zs, pre ? 1 : 0);
     PT2Q_LAUNCH_CHECK();
   } else {
     hipLaunchKernelGGL(ssr_wbar_partial_kernel, dim3(nchunks, ceil_div(n, 256)), dim3(256), 0, st,
