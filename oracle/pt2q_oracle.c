@@ -267,15 +267,17 @@ int orc_atq_quantize(const float* W, long ldw, int n, int b, int aga, const floa
 
 /* The w-bar partial of one chunk of 128 rem entries v[0..128) (+0 past r): the order the
  * error-feedback tile that wrote them forms it in (DESIGN.md §3 CHUNK128):
- * x_l = v[l] + v[l+32], y_l = v[64+l] + v[96+l] (l < 32), X = butterfly32(x), Y = butterfly32(y),
- * partial = X + Y. */
+ * x_l = v[l] + v[l+32], y_l = v[64+l] + v[96+l] (l < 32); X = butterfly16(x[0..16)) +
+ * butterfly16(x[16..32)), Y likewise; partial = X + Y. */
 float orc_wbar_chunk(const float* v) {
   float x[32], y[32];
   for (int l = 0; l < 32; ++l) {
     x[l] = v[l] + v[l + 32];
     y[l] = v[64 + l] + v[96 + l];
   }
-  return butterfly(x, 32) + butterfly(y, 32);
+  const float X = butterfly(x, 16) + butterfly(x + 16, 16);
+  const float Y = butterfly(y, 16) + butterfly(y + 16, 16);
+  return X + Y;
 }
 
 /* compute_column_similarity_to_mean reorder.py:36-61 on Wt (feature-major, m x ldw).

@@ -31,6 +31,7 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_GEMM_TILE", t.gemm_tile);
   getb("PT2Q_RANK_UPDATE", t.rank_update);
   geti("PT2Q_CHOL_PANEL", t.chol_panel);
+  geti("PT2Q_CHOL_SUBPANEL", t.chol_subpanel);
   getb("PT2Q_CHOL_LOOKAHEAD", t.chol_lookahead);
   getb("PT2Q_WBAR_FUSED", t.wbar_fused);
   getb("PT2Q_SIM_SPLIT", t.sim_split);

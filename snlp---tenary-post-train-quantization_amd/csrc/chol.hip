@@ -247,7 +247,7 @@ GemmDesc trtri_desc(const float* U, float* UiT, long ld, int j0, int K, int c1, 
 
 // Large chain GEMMs (panel-wide updates, lauum): the LDS-DMA kernel where it applies and pays.
 int launch_big(const GemmDesc& g, hipStream_t st) {
-  const long tiles = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128) / (g.upper ? 2 : 1);
+  const long tiles = (long)ceil_div(g.M, 128) * ceil_div(g.N, 128) / (g.upper ? 2 : 1) * (g.batch > 1 ? g.batch : 1);
   if (tiles >= 64 && g.K >= 128) {
     const int rc = pt2q_launch_gemmx(g, st);
     if (rc != PT2Q_E_UNSUPPORTED) return rc;
@@ -343,20 +343,38 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     pending = false;
     return PT2Q_OK;
   };
+  // sub-panels of SP rows (a multiple of NB dividing CP): a block's rank-64 strip update reaches
+  // only the rows of its sub-panel; the rest of the panel takes the sub-panel's terms as one
+  // rank-SP chain GEMM once the sub-panel is done -- the same terms in the same ascending order
+  // (inverse columns of later sub-panels get the zero terms of rows below their diagonal, exact
+  // no-ops), with a quarter of the strip updates' read-modify-write traffic at SP = CP / 4.
+  const int SPt = tu.chol_subpanel >= NB ? tu.chol_subpanel / NB * NB : CP;
+  const int SP = (SPt < CP && CP % SPt == 0) ? SPt : CP;
   for (int P0 = 0; P0 < m; P0 += CP) {
     const int Pend = (m - P0 < CP) ? m : P0 + CP;
-    for (int p0 = P0; p0 < Pend; p0 += NB) {
-      const int nb = (Pend - p0 < NB) ? Pend - p0 : NB;
-      if ((rc = factor(p0, nb, factored)) != PT2Q_OK) return rc;
-      factored = false;
-      const int p1 = p0 + nb;
-      if (p1 >= Pend) break;
-      const int nb1 = (Pend - p1 < NB) ? Pend - p1 : NB;
-      // U rows [p1, Pend) x columns [p1, m) and inverse columns [p1, Pend) x rows [0, p1)
-      if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, Pend - p1, p1, m - p1, false, batch),
-                                  trtri_desc(U, Ui, ld, p0, nb, p1, Pend - p1, p1, batch), st, U, ld, p1,
-                                  nb1, info, &factored)) != PT2Q_OK)
+    for (int Q0 = P0; Q0 < Pend; Q0 += SP) {
+      const int Qend = (Pend - Q0 < SP) ? Pend : Q0 + SP;
+      for (int p0 = Q0; p0 < Qend; p0 += NB) {
+        const int nb = (Qend - p0 < NB) ? Qend - p0 : NB;
+        if ((rc = factor(p0, nb, factored)) != PT2Q_OK) return rc;
+        factored = false;
+        const int p1 = p0 + nb;
+        if (p1 >= Qend) break;
+        const int nb1 = (Qend - p1 < NB) ? Qend - p1 : NB;
+        // U rows [p1, Qend) x columns [p1, m) and inverse columns [p1, Qend) x rows [0, p1)
+        if ((rc = pt2q_launch_gemm2(trailing_desc(U, ld, p0, nb, p1, Qend - p1, p1, m - p1, false, batch),
+                                    trtri_desc(U, Ui, ld, p0, nb, p1, Qend - p1, p1, batch), st, U, ld, p1,
+                                    nb1, info, &factored)) != PT2Q_OK)
+          return rc;
+      }
+      if (Qend >= Pend) break;
+      // the sub-panel's terms: U rows [Qend, Pend) x columns [Qend, m), inverse columns
+      // [Qend, Pend) x rows [0, Qend)
+      const int K = Qend - Q0;
+      if ((rc = launch_big(trailing_desc(U, ld, Q0, K, Qend, Pend - Qend, Qend, m - Qend, false, batch), st)) !=
+          PT2Q_OK)
         return rc;
+      if ((rc = launch_big(trtri_desc(U, Ui, ld, Q0, K, Qend, Pend - Qend, Qend, batch), st)) != PT2Q_OK) return rc;
     }
     if (Pend >= m) break;
     const int K = Pend - P0, rest = m - Pend;

@@ -107,6 +107,8 @@ struct Pt2qTuning {
   bool rank_update = true;     // PT2Q_RANK_UPDATE=0: generic grouped GEMM for Cholesky updates
   bool chol_lookahead = true;  // PT2Q_CHOL_LOOKAHEAD=0: the trailing updates on the main stream only
   int chol_panel = 0;          // PT2Q_CHOL_PANEL: rows per rank-P Cholesky update (0: by m)
+  int chol_subpanel = 256;     // PT2Q_CHOL_SUBPANEL: rank-64 strip updates only inside sub-panels of
+                               // this many rows, rank-SP updates (gemmx) to the rest of the panel (0: off)
   bool wbar_fused = true;      // PT2Q_WBAR_FUSED=0: three SSR-mean launches
   bool ef_wbar = true;         // PT2Q_EF_WBAR=0: the SSR mean pass reads W again (no EF partials)
   bool sim_split = true;       // PT2Q_SIM_SPLIT=0: one wave per column for n > 4096 (256 VGPRs)

@@ -126,11 +126,13 @@ struct EfAcc {
         asm volatile("" ::"v"(a[p][0]), "v"(a[p][1]), "v"(b[p][0]), "v"(b[p][1]));
       }
       __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-        for (int rn = 0; rn < 2; ++rn)
-          acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][rn], a[c][rm], acc[rm][rn], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      io.template mid<S>();  // VALU work that issues in the shadow of that MFMA
+      __builtin_amdgcn_sched_barrier(0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (S + 1 < EF_KH / 2) ef_wait(a[n], b[n]);
       run<S + 1>(bA, bB, a, b, io);
@@ -184,7 +186,29 @@ PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
 struct EfNoIO {
   template <int S>
   PT2Q_DEV void at() {}
+  template <int S>
+  PT2Q_DEV void mid() {}
 };
+
+// ---- the next block's w-bar partials (see the file header), one column j per k-pair of the
+// next tile's first K half.  Column j = (rn, q, u) of the tile's results pend; the lane sum over
+// rows e and e + 32 (its two row blocks rm), bfly16 inside each 16-lane row, then row_bcast:15
+// adds row 0's sum into row 1 (row 2's into row 3): lanes 16 and 48 hold the wave's 64-row sum
+// for column halves h = 0, 1 and store it to LDS (the other lanes to a per-lane spare slot).
+constexpr int EF_PS = 8;    // w-bar partial stores per wave per tile (float4; dropped where unused)
+constexpr int EF_RED = 512; // LDS floats: [wave][64] sums + [wave][64] spare slots
+
+template <int J>
+PT2Q_DEV void ef_wbar_step(const int (&prow)[2], const u32x4 (&pend)[EF_CV], float* red) {
+  constexpr int rn = J >> 4, q = (J >> 2) & 3, u = J & 3;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float v0 = prow[0] >= 0 ? __uint_as_float(pend[rn * 4 + q][u]) : 0.0f;
+  const float v1 = prow[1] >= 0 ? __uint_as_float(pend[(2 + rn) * 4 + q][u]) : 0.0f;
+  float x = bfly16(v0 + v1);
+  x = x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
+  const bool sel = (lane & 31) == 16;
+  red[sel ? wave * 64 + (lane >> 5) * 32 + J : 256 + wave * 64 + lane] = x;
+}
 
 // The Wt traffic of a tile, spread over the first K half of the next one instead of bursting
 // at tile ends (every CU would burst at once): at every even k-pair one store of the previous
@@ -200,6 +224,8 @@ struct EfIO {
   int i0;
   const u32x4 (&pend)[EF_CV];
   u32x4 (&c)[EF_CV];
+  bool wb;     // form the previous tile's w-bar partials in this half
+  float* red;
 
   template <int S>
   PT2Q_DEV void at() {
@@ -208,6 +234,10 @@ struct EfIO {
       __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
       c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
     }
+  }
+  template <int S>
+  PT2Q_DEV void mid() {
+    if (wb) ef_wbar_step<S>(prow, pend, red);
   }
 };
 
@@ -225,60 +255,46 @@ PT2Q_DEV void ef_vmcnt(int n) {
   }
 }
 
-constexpr int EF_PS = 8;  // w-bar partial stores per wave per tile (float4; dropped where unused)
-
-// xor-16 lane exchange inside each 32-lane half (ds_swizzle bitmask mode: and 0x1f, xor 0x10)
-PT2Q_DEV float ef_xor16(float v) {
-  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
-}
-
-// The w-bar partials of tile (e0, i0) from its new values (see the file header): every wave
-// issues exactly EF_PS buffer stores (real ones: lanes 0 and 32 of the row-half-0 waves, i < n).
-PT2Q_DEV void ef_wbar(const EfArgs& a, __amdgpu_buffer_rsrc_t rp, int e0, int i0, const int (&wrow)[2],
-                      const u32x4 (&pend)[EF_CV], float* red) {
+// The w-bar partials of a finished tile (e0, i0) from the wave sums in LDS: part[c][i] = X + Y,
+// X from the row-half-0 wave of the column half, Y from the row-half-1 wave.  Branch-free: every
+// lane reads (b128, all in flight) and every wave issues exactly EF_PS buffer stores (real ones:
+// lanes 0 and 32 of the row-half-0 waves, i < n; the rest dropped).
+PT2Q_DEV void ef_wbar_store(int n, __amdgpu_buffer_rsrc_t rp, bool valid, int e0, int i0, const float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
   const int h = lane >> 5;
-  float x[2][4][4];
+  const bool mine = valid && wr == 0 && (lane & 31) == 0;
+  const long cb = (long)(e0 / EF_T) * n;
+  const f32x4* X = (const f32x4*)(red + wc * 64 + h * 32);
+  const f32x4* Y = (const f32x4*)(red + (wc + 2) * 64 + h * 32);
 #pragma unroll
-  for (int rn = 0; rn < 2; ++rn)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float v0 = wrow[0] >= 0 ? __uint_as_float(pend[rn * 4 + q][u]) : 0.0f;
-        const float v1 = wrow[1] >= 0 ? __uint_as_float(pend[(2 + rn) * 4 + q][u]) : 0.0f;
-        float v = v0 + v1;
-        v = v + ef_xor16(v);
-        x[rn][q][u] = bfly16(v);
-      }
-  if (wr == 1 && (lane & 31) == 0) {
-#pragma unroll
-    for (int rn = 0; rn < 2; ++rn)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) red[wc * 64 + rn * 32 + 8 * q + 4 * h + u] = x[rn][q][u];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  const bool mine = wr == 0 && (lane & 31) == 0;
-  const int c = e0 / EF_T;
-#pragma unroll
-  for (int rn = 0; rn < 2; ++rn)
+  for (int rn = 0; rn < 2; ++rn) {
+    f32x4 x[4], y[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int il = wc * 64 + rn * 32 + 8 * q + 4 * h;
-      const int i = i0 + il;
-      f32x4 o;
+      x[q] = X[rn * 4 + q];
+      y[q] = Y[rn * 4 + q];
+    }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) o[u] = mine ? x[rn][q][u] + red[il + u] : 0.0f;
-      const unsigned off = (mine && i < a.n) ? (unsigned)(((long)c * a.n + i) * 4) : EF_DROP;
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + wc * 64 + rn * 32 + 8 * q + 4 * h;
+      const f32x4 o = x[q] + y[q];
+      const unsigned off = (mine && i < n) ? (unsigned)((cb + i) * 4) : EF_DROP;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rp, off, 0, 0);
     }
+  }
+}
+
+template <int J>
+PT2Q_DEV void ef_wbar_all(const int (&prow)[2], const u32x4 (&pend)[EF_CV], float* red) {
+  if constexpr (J < 32) {
+    ef_wbar_step<J>(prow, pend, red);
+    ef_wbar_all<J + 1>(prow, pend, red);
+  }
 }
 
 __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, long part_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * EF_STAGE];
-  __shared__ float red[128];  // w-bar partials of the row-half-1 waves (ef_wbar)
+  __shared__ __attribute__((aligned(16))) float red[EF_RED];  // w-bar wave sums (ef_wbar_step)
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   const int total = a0.ntile * a0.nz;
   int t = blockIdx.x;
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     i0 = (tl % a0.ti) * EF_T;
   };
   auto rsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000); };
-  auto prsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)part_bytes, 0x00020000); };
+  auto prsrc = [&](const EfArgs& x) { return __builtin_amdgcn_make_buffer_rsrc(x.part, 0, (int)part_bytes, 0x00020000); };
   const int P = a0.part ? EF_PS : 0;  // part stores per tile, younger than the tile's stages
   EfArgs a;
   int e0, i0, wrow[2];
@@ -304,7 +320,8 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
   if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
   // P dropped stores: every tile's first wait then sees the same count of younger operations
   for (int j = 0; j < P; ++j) __builtin_amdgcn_raw_buffer_store_b128(u32x4{}, rc, EF_DROP, 0, 0);
-  int prow[2] = {-1, -1}, pi0 = 0;
+  int prow[2] = {-1, -1}, pi0 = 0, pe0 = -1;
+  __amdgpu_buffer_rsrc_t prp = rc;  // the previous tile's part buffer (its linear's)
   u32x4 c[EF_CV], pend[EF_CV];
 #pragma unroll
   for (int j = 0; j < EF_CV; ++j) pend[j] = u32x4{};
@@ -326,11 +343,12 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     asm volatile("s_barrier" ::: "memory");
     if (more) ef_rows(an, en, nrow);
     {
-      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c};
+      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, P > 0, red};
       F.half(lds0, io);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
     if (more) ef_stage(an, en, in, 0, smem);
+    if (P) ef_wbar_store(a0.n, prp, pe0 >= 0, pe0, pi0, red);  // the previous tile's partials
     if (a.nh == 2) {
       ef_vmcnt(P + 2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
       asm volatile("s_barrier" ::: "memory");
@@ -339,7 +357,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (more) ef_stage(an, en, in, 1, smem + EF_STAGE);
     }
-    ef_vmcnt(more ? EF_DMA + S1 : 0);  // the old values landed (younger: the next tile's stages)
+    ef_vmcnt(more ? EF_DMA + P + S1 : 0);  // the old values landed (younger: next stages, part stores)
 #pragma unroll
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
@@ -351,10 +369,11 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
           for (int u = 0; u < 4; ++u)
             pend[j][u] = __float_as_uint(__uint_as_float(c[j][u]) - F.acc[rm][rn][4 * q + u]);
         }
-    if (P) ef_wbar(a, prsrc(a), e0, i0, wrow, pend, red);
     prow[0] = wrow[0];
     prow[1] = wrow[1];
     pi0 = i0;
+    pe0 = e0;
+    if (P) prp = prsrc(a);
     prc = rc;
     if (!more) break;
     t = tn;
@@ -368,6 +387,12 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
 #pragma unroll
   for (int j = 0; j < EF_CV; ++j)
     __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, j >> 3, (j >> 2) & 1, j & 3), 0, 0);
+  if (P) {  // the last tile's partials (the earlier ones were formed in the next tile's first half)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red free (last readers done)
+    ef_wbar_all<0>(prow, pend, red);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    ef_wbar_store(a0.n, prp, true, pe0, pi0, red);
+  }
 }
 
 }  // namespace

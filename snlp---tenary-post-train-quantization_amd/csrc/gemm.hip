@@ -388,6 +388,12 @@ template <int BM, int BN, typename TIn, bool VEC>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  if (gridDim.y > 1) {  // batch item blockIdx.y (f32, no row index)
+    const long o = (long)blockIdx.y * g.bstride;
+    g.A = (const TIn*)g.A + o;
+    g.B = (const TIn*)g.B + o;
+    g.C += o;
+  }
   gemm_tile<BM, BN, TIn, VEC>(g, tiles_m, tiles_n, blockIdx.x, gridDim.x, As, Bs);
 }
 
@@ -485,7 +491,8 @@ bool vec_ok(const GemmDesc& g) {
     int vdim = (layout == LAY_KMAJOR) ? dim : g.K;
     return ((uintptr_t)p % 16 == 0) && (ld % vw == 0) && (vdim % vw == 0);
   };
-  return ok_vec(g.A, g.lda, g.a_layout, g.M) && ok_vec(g.B, g.ldb, g.b_layout, g.N);
+  return ok_vec(g.A, g.lda, g.a_layout, g.M) && ok_vec(g.B, g.ldb, g.b_layout, g.N) &&
+         (g.batch <= 1 || g.bstride % vw == 0);  // every batch item aligned like item 0
 }
 
 template <int BM, int BN, typename TIn>
@@ -499,11 +506,12 @@ int launch_t(const GemmDesc& g, hipStream_t st) {
     ntiles = (long)tm * tn;
   }
   if (ntiles <= 0) return PT2Q_OK;
+  const unsigned nb = g.batch > 1 ? (unsigned)g.batch : 1u;  // grid.y = batch item
   if (vec_ok<BM, BN, TIn>(g))
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, true>), dim3((unsigned)ntiles), dim3(256), 0, st, g,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, true>), dim3((unsigned)ntiles, nb), dim3(256), 0, st, g,
                        tm, tn);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, false>), dim3((unsigned)ntiles), dim3(256), 0, st,
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, TIn, false>), dim3((unsigned)ntiles, nb), dim3(256), 0, st,
                        g, tm, tn);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
@@ -516,7 +524,7 @@ template <typename TIn>
 int launch_dt(const GemmDesc& g, hipStream_t st) {
   auto count = [&](int t) -> long {
     long tm = ceil_div(g.M, t), tn = ceil_div(g.N, t);
-    return g.upper ? tm * (tm + 1) / 2 : tm * tn;
+    return (g.upper ? tm * (tm + 1) / 2 : tm * tn) * (g.batch > 1 ? g.batch : 1);
   };
   const double slots = 256.0;
   long c128 = count(128), c64 = count(64);
@@ -838,16 +846,9 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
   if (g.M <= 0 || g.N <= 0) return PT2Q_OK;
   if (g.K < 0 || !g.A || !g.B || !g.C) return PT2Q_E_ARG;
-  if (g.batch > 1) {  // one item per launch
-    if (g.in_dtype != PT2Q_F32) return PT2Q_E_ARG;
-    for (int z = 0; z < g.batch; ++z) {
-      GemmDesc h = g;
-      const long o = (long)z * g.bstride;
-      h.A = (const float*)g.A + o; h.B = (const float*)g.B + o; h.C = g.C + o; h.batch = 1;
-      const int rc = pt2q_launch_gemm(h, st);
-      if (rc != PT2Q_OK) return rc;
-    }
-    return PT2Q_OK;
+  if (g.batch > 1) {  // every item in one launch (grid.y); f32 chains without a row index
+    if (g.in_dtype != PT2Q_F32 || g.crow) return PT2Q_E_ARG;
+    return launch_dt<float>(g, st);
   }
   switch (g.in_dtype) {
     case PT2Q_F32:

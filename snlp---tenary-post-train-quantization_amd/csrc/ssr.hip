@@ -16,13 +16,15 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int CHUNK = 128;  // canonical wbar chunk (rem entries per partial sum)
 
+// Leaf k of the CHUNK128 half tree: bfly16 over l in [0, 16) (leaves in 4-bit bit-reversed
+// order), then the same over [16, 32), the two sums added.
 PT2Q_DEV constexpr int brev5(int k) {
-  return ((k & 1) << 4) | ((k & 2) << 2) | (k & 4) | ((k & 8) >> 2) | ((k & 16) >> 4);
+  return (k & 16) | ((k & 1) << 3) | ((k & 2) << 1) | ((k & 4) >> 1) | ((k & 8) >> 3);
 }
 
-// Half of a chunk's w-bar partial (DESIGN.md §3 CHUNK128): butterfly32 over x_l = v[o+l] + v[o+l+32],
-// evaluated as a pairwise stack over the leaves in bit-reversed order (the butterfly's tree),
-// 8 leaves' loads in flight at a time.  ld(j) = v[j] (zero past the chunk's end).
+// Half of a chunk's w-bar partial (DESIGN.md §3 CHUNK128): x_l = v[o+l] + v[o+l+32] (l < 32),
+// bfly16(x[0..16)) + bfly16(x[16..32)), evaluated as a pairwise stack over the leaves in the
+// tree's order, 8 leaves' loads in flight at a time.  ld(j) = v[j] (zero past the chunk's end).
 template <typename V, typename LD>
 PT2Q_DEV V wbar_half(LD&& ld, int o) {
   V acc[6];
