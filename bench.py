@@ -455,7 +455,10 @@ def model_work(units, bs):
         for _, n, _ in lins:
             w["ef_fl"] += 2.0 * n * bs * rsum          # W[:, rem] -= E C, K = b
             w["ef_bytes"] += 8.0 * n * rsum            # read + write of W[:, rem] (fp32)
-            w["ssr_bytes"] += 8.0 * n * rsum           # w-bar pass + similarity pass over W[:, rem]
+            # similarity pass over W[:, rem] of every SSR block (r = m, m - b, ...: m + rsum columns)
+            # plus block 0's stand-alone w-bar pass (m columns); later blocks' w-bar partials come
+            # out of the error feedback (no pass over W, DESIGN.md §3 CHUNK128)
+            w["ssr_bytes"] += 4.0 * n * (2 * m + rsum)
             w["atq_bytes"] += 9.0 * n * m              # W block read, codes + error term written
     return w
 
