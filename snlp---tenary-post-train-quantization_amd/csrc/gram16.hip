@@ -514,11 +514,11 @@ struct GwDma {          // a future stage's LDS-DMAs
 };
 
 // one k16 step: MFMAs on cur, the reads of nxt (byte offsets ROFFA / ROFFB from ra) in the gaps.
-// SYNC: after the first MFMA wait for the stage the reads need (Y younger stages stay in flight;
-// Y < 0: y at run time) and meet the other waves.  HALF >= 0: issue that half of a stage's
-// DMAs.  No run-time branch between the MFMAs of a steady step (Y >= 0): a branch there makes
+// SYNC: after the first MFMA wait for the stage the reads need (VM younger DMAs stay in flight;
+// VM < 0: y younger whole stages, y at run time) and meet the other waves.  HALF >= 0: issue that half of a stage's
+// DMAs.  No run-time branch between the MFMAs of a steady step (VM >= 0): a branch there makes
 // the register allocator shuffle the accumulator registers.
-template <int BM, bool BF16, int ROFFA, int ROFFB, bool SYNC, int Y, int HALF>
+template <int BM, bool BF16, int ROFFA, int ROFFB, bool SYNC, int VM, int HALF>
 PT2Q_DEV void gw_step(f32x16 (&acc)[GwGeo<BM>::MT][4], const GwFrags<GwGeo<BM>::NF>& cur,
                       GwFrags<GwGeo<BM>::NF>& nxt, const uint32_t (&ra)[GwGeo<BM>::NF], int y, const GwDma& d,
                       const uint32_t (&vo)[GwGeo<BM>::DMA]) {
@@ -526,8 +526,8 @@ PT2Q_DEV void gw_step(f32x16 (&acc)[GwGeo<BM>::MT][4], const GwFrags<GwGeo<BM>::
   constexpr int NM = G::MT * 4, HD = G::DMA / 2;
   gw_mfma1<BF16>(acc[0][0], cur.lo[0], cur.hi[0], cur.lo[G::MT], cur.hi[G::MT]);
   if constexpr (SYNC) {
-    if constexpr (Y >= 0)
-      gw_vmwait<Y * G::DMA>();
+    if constexpr (VM >= 0)
+      gw_vmwait<VM>();
     else
       gw_vmwait_y<G::DMA>(y);
     asm volatile("s_barrier" ::: "memory");
@@ -622,7 +622,8 @@ PT2Q_DEV void gw_chain(f32x16 (&acc)[GwGeo<BM>::MT][4], const uint16_t* X, long 
     const uint32_t base = lds0 + (uint32_t)(((t + 1) % NS) * G::STG);
 #pragma unroll
     for (int u = 0; u < G::NF; ++u) ra[u] = base + off[u];
-    gw_step<BM, BF16, 0, 0, true, NS - 2, 1>(acc, Q, P, ra, 0, d, vo);  // stage t+1 published
+    // in flight past stage t+1: stages t+2 .. t+NS-2 and the first half of t+NS-1 (step A's DMAs)
+    gw_step<BM, BF16, 0, 0, true, (NS - 3) * G::DMA + G::DMA / 2, 1>(acc, Q, P, ra, 0, d, vo);
   }
   // the rest: per-lane sources (a ragged last stage, an edge tile) and a draining ring
   for (; t < nk; ++t) {

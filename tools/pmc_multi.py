@@ -49,6 +49,10 @@ def main():
                 for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                     if n in c:
                         out.append(f"{n[3:].lower()} {c[n] / w:.2f}")
+            if c.get("SQ_INSTS_LDS"):
+                out.append(f"lds_insts {c['SQ_INSTS_LDS']:.3g}")
+                if "SQ_LDS_BANK_CONFLICT" in c:
+                    out.append(f"lds_conflict_cyc {c['SQ_LDS_BANK_CONFLICT']:.3g}")
             print("  " + "  ".join(out))
 
 
