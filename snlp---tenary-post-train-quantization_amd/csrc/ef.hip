@@ -21,6 +21,7 @@
 // removes the separate w-bar pass over W[:, rem] (one full read per block).
 #include "common.hpp"
 #include "internal.hpp"
+#include "probe.hpp"
 
 namespace {
 
@@ -77,8 +78,8 @@ PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, i
   const int d = 4 * (lane & 31);
   const bool kin = k < a.bs;
   const int e = e0 + d, i = i0 + d;
-  const void* sa = kin ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
-  const void* sb = kin ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
+  const void* sa = kin && !probe::ef_zero_dma ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
+  const void* sb = kin && !probe::ef_zero_dma ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
   __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
@@ -126,13 +127,17 @@ struct EfAcc {
         asm volatile("" ::"v"(a[p][0]), "v"(a[p][1]), "v"(b[p][0]), "v"(b[p][1]));
       }
       __builtin_amdgcn_sched_barrier(0);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
+      if constexpr (!probe::ef_no_mfma) acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       io.template mid<S>();  // VALU work that issues in the shadow of that MFMA
       __builtin_amdgcn_sched_barrier(0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
+      if constexpr (!probe::ef_no_mfma) {
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
+      } else {  // keep the operands live
+        asm volatile("" ::"v"(a[c][0]), "v"(a[c][1]), "v"(b[c][0]), "v"(b[c][1]));
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (S + 1 < EF_KH / 2) ef_wait(a[n], b[n]);
       run<S + 1>(bA, bB, a, b, io);
@@ -166,7 +171,7 @@ PT2Q_DEV int ef_col(int i0, int rn, int q) {
 // of this lane's output row in row block rm (-1 past nr)
 PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm, int rn, int q) {
   const int i = ef_col(i0, rn, q);
-  if (wrow[rm] < 0 || i >= a.ldw) return EF_DROP;
+  if (wrow[rm] < 0 || i >= a.ldw || probe::ef_drop_wt) return EF_DROP;
   return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
 }
 

@@ -11,6 +11,9 @@ namespace probe {
 constexpr bool gram_no_dma = (PT2Q_PROBE & 1) != 0;   // tools/gram16_probe.hip: compute-only (stale LDS)
 constexpr bool gram_no_mfma = (PT2Q_PROBE & 2) != 0;  // tools/gram16_probe.hip: fetch-only
 constexpr bool topk_stamps = (PT2Q_PROBE & 4) != 0;   // tools/topk_probe.hip: phase timestamps
+constexpr bool ef_drop_wt = (PT2Q_PROBE & 8) != 0;    // tools/ef_probe.hip: Wt loads / stores dropped
+constexpr bool ef_no_mfma = (PT2Q_PROBE & 16) != 0;   // tools/ef_probe.hip: no MFMAs
+constexpr bool ef_zero_dma = (PT2Q_PROBE & 32) != 0;  // tools/ef_probe.hip: operand DMAs from one chunk
 }  // namespace probe
 
 #if (PT2Q_PROBE & 4) != 0

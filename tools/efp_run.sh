@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/efp
+for m in 0 8 16 32 56; do
+  timeout -k 10 60 tools/_probe/ef_probe_$m 16384 4096 128 20 1 || exit 1
+  timeout -k 10 60 tools/_probe/ef_probe_$m 4096 2048 128 50 1 || exit 1
+done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/efp/out.txt
