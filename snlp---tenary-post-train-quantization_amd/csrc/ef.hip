@@ -70,7 +70,7 @@ PT2Q_DEV EfArgs ef_linear(const EfArgs& a0, int z) {
 // k rows past bs come from a zero chunk (their MFMA steps are then exact no-ops); columns past
 // the data come from row 0 (garbage in rows / columns whose results are dropped), so every wave
 // issues exactly EF_DMA instructions.
-PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, int q) {
+PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, int q, bool withB) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   typedef __attribute__((address_space(3))) void* lptr;
   const int kr = (wave * 8 + q) * 2 + (lane >> 5);  // k row inside the stage
@@ -81,13 +81,17 @@ PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, i
   const void* sa = kin && !probe::ef_zero_dma ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
   const void* sb = kin && !probe::ef_zero_dma ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
+  if constexpr (probe::ef_no_dma) return;
   __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 8 + q) * 1024), 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
+  if (withB) __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + EF_PANEL + (wv * 8 + q) * 1024), 16, 0, 0);
 }
 
-PT2Q_DEV void ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg) {
+// withB = false: the B panel (E columns i0) already holds this K half -- the previous tile of the
+// workgroup had the same linear and i0 -- so only the A panel is fetched (8 DMAs instead of 16)
+PT2Q_DEV int ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, bool withB = true) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) ef_stage_q(a, e0, i0, h, stg, q);
+  for (int q = 0; q < 8; ++q) ef_stage_q(a, e0, i0, h, stg, q, withB);
+  return withB ? EF_DMA : EF_DMA / 2;
 }
 
 template <int OFF>
@@ -97,8 +101,10 @@ PT2Q_DEV float ef_ld(uint32_t addr) {
   return r;
 }
 
+// wait until at most N LDS operations are outstanding, tying the operand registers a, b
+template <int N>
 PT2Q_DEV void ef_wait(float (&a)[2], float (&b)[2]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]));
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(b[0]), "+v"(b[1]) : "n"(N));
 }
 
 // k-pair S of a stage: lane reads A rows e (2 MFMA row blocks) and B columns i (2 blocks).
@@ -113,48 +119,57 @@ PT2Q_DEV void ef_read(uint32_t baseA, uint32_t baseB, float (&a)[2], float (&b)[
 struct EfAcc {
   f32x16 acc[2][2];  // [rm][rn], transposed MFMA: lane <-> e row, registers <-> i columns
 
-  // k-pair S: its operands are in set S % 3; the reads of pair S+1 go to set (S+1) % 3, whose
-  // registers the MFMAs of pair S-2 read long ago (no overwrite of an operand in flight).  The
-  // order reads -> MFMAs -> wait is pinned (the scheduler would sink the reads below the MFMAs).
-  template <int S, class IO>
-  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[3][2], float (&b)[3][2], IO& io) {
-    if constexpr (S < EF_KH / 2) {
-      constexpr int c = S % 3, n = (S + 1) % 3;
-      if constexpr (S + 1 < EF_KH / 2) ef_read<S + 1>(bA, bB, a[n], b[n]);
-      io.template at<S>();
+  // k-pair S: its operands are in set S % 4; the reads of pair S+2 go to set (S+2) % 4, whose
+  // registers the MFMAs of pair S-2 read long ago (no overwrite of an operand in flight), so an
+  // LDS read has two pairs (~500 cycles) to land instead of one.  The IO work of the pair sits in
+  // the shadows of its MFMAs (one piece after each of the first three): a VMEM issue before the
+  // first MFMA would leave the MFMA pipe idle.  WB: LDS writes the IO issues per pair (the w-bar
+  // step), counted in the lgkmcnt waits.  The order reads -> MFMAs -> wait is pinned.
+  template <int S, int WB, class IO>
+  PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[4][2], float (&b)[4][2], IO& io) {
+    constexpr int NP = EF_KH / 2;
+    if constexpr (S < NP) {
+      constexpr int c = S % 4;
+      if constexpr (S + 2 < NP) ef_read<S + 2>(bA, bB, a[(S + 2) % 4], b[(S + 2) % 4]);
       if constexpr (S > 0) {  // pair S-1's operands stay allocated until these reads are out
-        constexpr int p = (S + 2) % 3;
+        constexpr int p = (S + 3) % 4;
         asm volatile("" ::"v"(a[p][0]), "v"(a[p][1]), "v"(b[p][0]), "v"(b[p][1]));
       }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!probe::ef_no_mfma) acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      io.template mid<S>();  // VALU work that issues in the shadow of that MFMA
+      io.template st<S>();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!probe::ef_no_mfma) {
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
-      } else {  // keep the operands live
-        asm volatile("" ::"v"(a[c][0]), "v"(a[c][1]), "v"(b[c][0]), "v"(b[c][1]));
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      io.template ld<S>();
+      __builtin_amdgcn_sched_barrier(0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      io.template mid<S>();  // VALU + one LDS write (WB) in the shadow of that MFMA
+      __builtin_amdgcn_sched_barrier(0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (S + 1 < NP) {  // pair S+1's reads (issued at pair S-1) landed
+        constexpr int n = (S >= 1 ? WB : 0) + (S + 2 < NP ? 4 : 0) + WB;
+        ef_wait<n>(a[(S + 1) % 4], b[(S + 1) % 4]);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (S + 1 < EF_KH / 2) ef_wait(a[n], b[n]);
-      run<S + 1>(bA, bB, a, b, io);
+      run<S + 1, WB>(bA, bB, a, b, io);
     }
   }
 
   // the 32 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
-  template <class IO>
+  template <int WB, class IO>
   PT2Q_DEV void half(uint32_t stg, IO& io) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
     const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
     const uint32_t bB = stg + EF_PANEL + lk * EF_ROWB + (wc * 64 + li) * 4;
-    float a[3][2], b[3][2];
+    float a[4][2], b[4][2];
     ef_read<0>(bA, bB, a[0], b[0]);
-    ef_wait(a[0], b[0]);
-    run<0>(bA, bB, a, b, io);
+    ef_read<1>(bA, bB, a[1], b[1]);
+    ef_wait<4>(a[0], b[0]);
+    run<0, WB>(bA, bB, a, b, io);
   }
 };
 
@@ -190,7 +205,9 @@ PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
 
 struct EfNoIO {
   template <int S>
-  PT2Q_DEV void at() {}
+  PT2Q_DEV void st() {}
+  template <int S>
+  PT2Q_DEV void ld() {}
   template <int S>
   PT2Q_DEV void mid() {}
 };
@@ -229,20 +246,27 @@ struct EfIO {
   int i0;
   const u32x4 (&pend)[EF_CV];
   u32x4 (&c)[EF_CV];
-  bool wb;     // form the previous tile's w-bar partials in this half
-  float* red;
+  float* red;  // the previous tile's w-bar wave sums (ef_wbar_step)
 
   template <int S>
-  PT2Q_DEV void at() {
+  PT2Q_DEV void st() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
       __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
-      c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
     }
   }
   template <int S>
+  PT2Q_DEV void ld() {
+    if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
+      constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
+      c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+    }
+  }
+  // always issued (one LDS write per pair, counted by the waits); without a partial buffer the
+  // sums land in `red` and nothing reads them
+  template <int S>
   PT2Q_DEV void mid() {
-    if (wb) ef_wbar_step<S>(prow, pend, red);
+    ef_wbar_step<S>(prow, pend, red);
   }
 };
 
@@ -332,37 +356,52 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
   for (int j = 0; j < EF_CV; ++j) pend[j] = u32x4{};
   // issue order per tile: [stores of the previous tile + this tile's old values, interleaved
   // with K half 0] [next stage 0] [K half 1] [next stage 1]
-  const int S1 = a.nh == 2 ? EF_DMA : 0;
+  int S1 = a.nh == 2 ? EF_DMA : 0;  // this tile's stage-1 DMAs (per wave), issued before its top
+  int nt = 0;  // tiles done (probe stamps only)
+  (void)nt;
   for (;;) {
+    PT2Q_EF_STAMP(nt, 0);
     const int tn = t + (int)gridDim.x;
     const bool more = tn < total;
     int en = 0, in = 0, nrow[2] = {-1, -1};
     EfArgs an = a;
     if (more) corner(tn, an, en, in);
+    // the next tile's E panel is this one's when it has the same linear and column block (tiles
+    // gridDim.x apart on the line share i0 whenever ti divides it: n = 4096)
+    const bool newB = !(more && an.Et == a.Et && in == i0);
+    int D0 = 0, D1 = 0;  // the next tile's stage DMAs per wave
     EfAcc F;
 #pragma unroll
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
       for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
     ef_vmcnt(S1 + P);  // stage 0 landed (younger: stage 1, the previous tile's part stores)
+    PT2Q_EF_STAMP(nt, 1);
     asm volatile("s_barrier" ::: "memory");
+    PT2Q_EF_STAMP(nt, 2);
     if (more) ef_rows(an, en, nrow);
     {
-      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, P > 0, red};
-      F.half(lds0, io);
+      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, red};
+      F.half<1>(lds0, io);
     }
+    PT2Q_EF_STAMP(nt, 3);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
-    if (more) ef_stage(an, en, in, 0, smem);
+    if (more) D0 = ef_stage(an, en, in, 0, smem, newB);
     if (P) ef_wbar_store(a0.n, prp, pe0 >= 0, pe0, pi0, red);  // the previous tile's partials
     if (a.nh == 2) {
-      ef_vmcnt(P + 2 * EF_CV + (more ? EF_DMA : 0));  // stage 1 landed
+      ef_vmcnt(P + 2 * EF_CV + D0);  // stage 1 landed
+      PT2Q_EF_STAMP(nt, 4);
       asm volatile("s_barrier" ::: "memory");
+      PT2Q_EF_STAMP(nt, 5);
       EfNoIO nio;
-      F.half(lds0 + EF_STAGE, nio);
+      F.half<0>(lds0 + EF_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (more) ef_stage(an, en, in, 1, smem + EF_STAGE);
+      if (more) D1 = ef_stage(an, en, in, 1, smem + EF_STAGE, newB);
     }
-    ef_vmcnt(more ? EF_DMA + P + S1 : 0);  // the old values landed (younger: next stages, part stores)
+    PT2Q_EF_STAMP(nt, 6);
+    ef_vmcnt(more ? D0 + P + D1 : 0);  // the old values landed (younger: next stages, part stores)
+    PT2Q_EF_STAMP(nt, 7);
+    ++nt;
 #pragma unroll
     for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
@@ -381,6 +420,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     if (P) prp = prsrc(a);
     prc = rc;
     if (!more) break;
+    S1 = D1;
     t = tn;
     a = an;
     rc = rsrc(a);

@@ -14,6 +14,8 @@ constexpr bool topk_stamps = (PT2Q_PROBE & 4) != 0;   // tools/topk_probe.hip: p
 constexpr bool ef_drop_wt = (PT2Q_PROBE & 8) != 0;    // tools/ef_probe.hip: Wt loads / stores dropped
 constexpr bool ef_no_mfma = (PT2Q_PROBE & 16) != 0;   // tools/ef_probe.hip: no MFMAs
 constexpr bool ef_zero_dma = (PT2Q_PROBE & 32) != 0;  // tools/ef_probe.hip: operand DMAs from one chunk
+constexpr bool ef_stamps = (PT2Q_PROBE & 64) != 0;    // tools/ef_probe.hip: per-tile phase timestamps
+constexpr bool ef_no_dma = (PT2Q_PROBE & 128) != 0;   // tools/ef_probe.hip: no operand DMAs (stale LDS)
 }  // namespace probe
 
 #if (PT2Q_PROBE & 4) != 0
@@ -23,4 +25,19 @@ __device__ long long topk_stamps[64][16];
   if (threadIdx.x == 0 && blockIdx.x < 64) topk_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
 #else
 #define PT2Q_TOPK_STAMP(i)
+#endif
+
+#if (PT2Q_PROBE & 64) != 0
+// thread 0 of each of the first 64 workgroups of the EF launch: s_memrealtime (100 MHz) at phase i of its
+// first 8 tiles (ef_stamps[wg][tile][i]); ef_stamp_tile counts the workgroup's tiles
+// (ef_clk: s_memtime, the shader clock, at phases 0 and 7: the clock the kernel ran at)
+__device__ long long ef_stamps[64][8][8];
+__device__ long long ef_clk[64][8][2];
+#define PT2Q_EF_STAMP(tile, i)                                                   \
+  if (threadIdx.x == 0 && blockIdx.x < 64 && (tile) < 8) {                       \
+    ef_stamps[blockIdx.x][tile][i] = __builtin_amdgcn_s_memrealtime();           \
+    if ((i) == 0 || (i) == 7) ef_clk[blockIdx.x][tile][(i) / 7] = __builtin_amdgcn_s_memtime(); \
+  }
+#else
+#define PT2Q_EF_STAMP(tile, i)
 #endif
