@@ -122,10 +122,11 @@ struct EfAcc {
   // k-pair S: its operands are in set S % 4; the reads of pair S+2 go to set (S+2) % 4, whose
   // registers the MFMAs of pair S-2 read long ago (no overwrite of an operand in flight), so an
   // LDS read has two pairs (~500 cycles) to land instead of one.  The IO work of the pair sits in
-  // the shadows of its MFMAs (one piece after each of the first three): a VMEM issue before the
-  // first MFMA would leave the MFMA pipe idle.  WB: LDS writes the IO issues per pair (the w-bar
-  // step), counted in the lgkmcnt waits.  The order reads -> MFMAs -> wait is pinned.
-  template <int S, int WB, class IO>
+  // the shadows of its four MFMAs (io.g0 .. g3, one piece after each): a VMEM issue or a dependent
+  // VALU chain longer than the 64-cycle shadow would leave the MFMA pipe idle.  The LDS writes
+  // of the IO (IO::lds_writes) are counted in the lgkmcnt waits.  The order reads -> MFMAs ->
+  // wait is pinned.
+  template <int S, class IO>
   PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[4][2], float (&b)[4][2], IO& io) {
     constexpr int NP = EF_KH / 2;
     if constexpr (S < NP) {
@@ -138,28 +139,32 @@ struct EfAcc {
       __builtin_amdgcn_sched_barrier(0);
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][0], acc[0][0], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      io.template st<S>();
+      io.template g0<S>();
       __builtin_amdgcn_sched_barrier(0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][0], acc[0][1], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      io.template ld<S>();
+      io.template g1<S>();
       __builtin_amdgcn_sched_barrier(0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][0], a[c][1], acc[1][0], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      io.template mid<S>();  // VALU + one LDS write (WB) in the shadow of that MFMA
+      io.template g2<S>();
       __builtin_amdgcn_sched_barrier(0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[c][1], a[c][1], acc[1][1], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (S + 1 < NP) {  // pair S+1's reads (issued at pair S-1) landed
-        constexpr int n = (S >= 1 ? WB : 0) + (S + 2 < NP ? 4 : 0) + WB;
+      io.template g3<S>();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (S + 1 < NP) {  // pair S+1's reads (issued at pair S-1) landed; younger LDS
+        // operations: pair S-1's IO writes, pair S+2's reads, pair S's IO writes
+        constexpr int n = (S >= 1 ? IO::template lds_writes<S - 1>() : 0) + (S + 2 < NP ? 4 : 0) +
+                          IO::template lds_writes<S>();
         ef_wait<n>(a[(S + 1) % 4], b[(S + 1) % 4]);
       }
-      run<S + 1, WB>(bA, bB, a, b, io);
+      run<S + 1>(bA, bB, a, b, io);
     }
   }
 
   // the 32 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
-  template <int WB, class IO>
+  template <class IO>
   PT2Q_DEV void half(uint32_t stg, IO& io) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
@@ -169,7 +174,7 @@ struct EfAcc {
     ef_read<0>(bA, bB, a[0], b[0]);
     ef_read<1>(bA, bB, a[1], b[1]);
     ef_wait<4>(a[0], b[0]);
-    run<0, WB>(bA, bB, a, b, io);
+    run<0>(bA, bB, a, b, io);
   }
 };
 
@@ -205,11 +210,15 @@ PT2Q_DEV void ef_rows(const EfArgs& a, int e0, int (&wrow)[2]) {
 
 struct EfNoIO {
   template <int S>
-  PT2Q_DEV void st() {}
+  PT2Q_DEV void g0() {}
   template <int S>
-  PT2Q_DEV void ld() {}
+  PT2Q_DEV void g1() {}
   template <int S>
-  PT2Q_DEV void mid() {}
+  PT2Q_DEV void g2() {}
+  template <int S>
+  PT2Q_DEV void g3() {}
+  template <int S>
+  static constexpr int lds_writes() { return 0; }
 };
 
 // ---- the next block's w-bar partials (see the file header), one column j per k-pair of the
@@ -232,6 +241,54 @@ PT2Q_DEV void ef_wbar_step(const int (&prow)[2], const u32x4 (&pend)[EF_CV], flo
   red[sel ? wave * 64 + (lane >> 5) * 32 + J : 256 + wave * 64 + lane] = x;
 }
 
+// ef_wbar_step for columns J and J+1 in four pieces, one per MFMA shadow of a k-pair: the two
+// columns' dependent DPP chains interleaved (each column's operations and order are
+// ef_wbar_step's, so the sums are the same bits).
+struct EfWb2 {
+  float x0, x1;
+};
+
+template <int J>
+PT2Q_DEV void ef_wb_a(EfWb2& w, const int (&prow)[2], const u32x4 (&pend)[EF_CV]) {
+  constexpr int rn = J >> 4, q = (J >> 2) & 3, u = J & 3;
+  constexpr int rn1 = (J + 1) >> 4, q1 = ((J + 1) >> 2) & 3, u1 = (J + 1) & 3;
+  const float a0 = prow[0] >= 0 ? __uint_as_float(pend[rn * 4 + q][u]) : 0.0f;
+  const float a1 = prow[0] >= 0 ? __uint_as_float(pend[rn1 * 4 + q1][u1]) : 0.0f;
+  const float b0 = prow[1] >= 0 ? __uint_as_float(pend[(2 + rn) * 4 + q][u]) : 0.0f;
+  const float b1 = prow[1] >= 0 ? __uint_as_float(pend[(2 + rn1) * 4 + q1][u1]) : 0.0f;
+  w.x0 = a0 + b0;
+  w.x1 = a1 + b1;
+}
+
+PT2Q_DEV void ef_wb_b(EfWb2& w) {
+  const float s0 = xor_lane<8>(w.x0), s1 = xor_lane<8>(w.x1);
+  w.x0 = w.x0 + s0;
+  w.x1 = w.x1 + s1;
+  const float t0 = xor_lane<4>(w.x0), t1 = xor_lane<4>(w.x1);
+  w.x0 = w.x0 + t0;
+  w.x1 = w.x1 + t1;
+}
+
+PT2Q_DEV void ef_wb_c(EfWb2& w) {
+  const float s0 = xor_lane<2>(w.x0), s1 = xor_lane<2>(w.x1);
+  w.x0 = w.x0 + s0;
+  w.x1 = w.x1 + s1;
+  const float t0 = xor_lane<1>(w.x0), t1 = xor_lane<1>(w.x1);
+  w.x0 = w.x0 + t0;
+  w.x1 = w.x1 + t1;
+}
+
+template <int J>
+PT2Q_DEV void ef_wb_d(EfWb2& w, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w.x0), 0x142, 0xA, 0xF, false));
+  const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w.x1), 0x142, 0xA, 0xF, false));
+  const float y0 = w.x0 + r0, y1 = w.x1 + r1;  // row_bcast:15
+  const bool sel = (lane & 31) == 16;
+  red[sel ? wave * 64 + (lane >> 5) * 32 + J : 256 + wave * 64 + lane] = y0;
+  red[sel ? wave * 64 + (lane >> 5) * 32 + J + 1 : 256 + wave * 64 + lane] = y1;
+}
+
 // The Wt traffic of a tile, spread over the first K half of the next one instead of bursting
 // at tile ends (every CU would burst at once): at every even k-pair one store of the previous
 // tile's results and one load of this tile's old values.  Rows of the previous tile are -1
@@ -248,26 +305,37 @@ struct EfIO {
   u32x4 (&c)[EF_CV];
   float* red;  // the previous tile's w-bar wave sums (ef_wbar_step)
 
+  EfWb2 w;     // the w-bar pieces' state between the gaps of an odd k-pair
+
+  // even k-pairs: one store of the previous tile's results, one load of this tile's old values;
+  // odd k-pairs S: the w-bar of columns S-1 and S of the previous tile's results
   template <int S>
-  PT2Q_DEV void st() {
+  PT2Q_DEV void g0() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
       __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
     }
+    if constexpr (S % 2 == 1) ef_wb_a<S - 1>(w, prow, pend);
   }
   template <int S>
-  PT2Q_DEV void ld() {
+  PT2Q_DEV void g1() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
       c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
     }
+    if constexpr (S % 2 == 1) ef_wb_b(w);
   }
-  // always issued (one LDS write per pair, counted by the waits); without a partial buffer the
-  // sums land in `red` and nothing reads them
   template <int S>
-  PT2Q_DEV void mid() {
-    ef_wbar_step<S>(prow, pend, red);
+  PT2Q_DEV void g2() {
+    if constexpr (S % 2 == 1) ef_wb_c(w);
   }
+  // (always issued; without a partial buffer the sums land in `red` and nothing reads them)
+  template <int S>
+  PT2Q_DEV void g3() {
+    if constexpr (S % 2 == 1) ef_wb_d<S - 1>(w, red);
+  }
+  template <int S>
+  static constexpr int lds_writes() { return S % 2 == 1 ? 2 : 0; }
 };
 
 // s_waitcnt vmcnt(N) for the small set of counts the schedule needs (immediate operand)
@@ -381,8 +449,8 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     PT2Q_EF_STAMP(nt, 2);
     if (more) ef_rows(an, en, nrow);
     {
-      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, red};
-      F.half<1>(lds0, io);
+      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, red, {}};
+      F.half(lds0, io);
     }
     PT2Q_EF_STAMP(nt, 3);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
@@ -394,7 +462,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
       asm volatile("s_barrier" ::: "memory");
       PT2Q_EF_STAMP(nt, 5);
       EfNoIO nio;
-      F.half<0>(lds0 + EF_STAGE, nio);
+      F.half(lds0 + EF_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (more) D1 = ef_stage(an, en, in, 1, smem + EF_STAGE, newB);
     }
