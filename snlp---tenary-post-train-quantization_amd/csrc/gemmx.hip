@@ -25,11 +25,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int XT = 128;              // tile side
-constexpr int XK = 32;               // k rows per stage
 constexpr int XROW = XT * 4;         // 512 B per k row of a panel
-constexpr int XPANEL = XK * XROW;    // 16 KiB
-constexpr int XSTG = 2 * XPANEL;     // A + B panels: 32 KiB
-constexpr int XDMA = 4;              // DMA wave-instructions per wave per panel per stage
+
+// ring geometry: KR k rows per stage, NS stages (LDS = NS * 2 * KR * 512 B)
+template <int KR>
+struct XGeo {
+  static constexpr int PANEL = KR * XROW;       // one operand's rows of a stage
+  static constexpr int STG = 2 * PANEL;         // A + B panels
+  static constexpr int DMA = PANEL / 1024 / 4;  // DMA wave-instructions per wave per panel
+};
 
 __device__ uint4 gxz_zero16[4];      // the source of out-of-range chunks (zero-initialised)
 
@@ -69,11 +73,13 @@ PT2Q_DEV int x_xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
 }
 
-// One panel of one stage: rows [k0, k0 + 32) (valid below kend) x columns [d0, d0 + 128) (valid
+// One panel of one stage: rows [k0, k0 + KR) (valid below kend) x columns [d0, d0 + 128) (valid
 // below DMAX) of a K-major operand, into panel memory `pan` (swizzled).  Lane l of the wave's
-// q-th instruction fills LDS chunk L = (wave * 4 + q) * 64 + l: row L / 32, position L % 32,
+// q-th instruction fills LDS chunk L = (wave * DMA + q) * 64 + l: row L / 32, position L % 32,
 // which holds global chunk (L % 32) ^ ((row & 1) << 3).
+template <int KR>
 PT2Q_DEV void x_panel_dma(const float* base, long ld, int d0, int DMAX, int k0, int kend, uint8_t* pan) {
+  constexpr int XDMA = XGeo<KR>::DMA;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   typedef __attribute__((address_space(3))) void* lptr;
@@ -143,14 +149,28 @@ PT2Q_DEV void x_chain(f32x16 (&acc)[2][2], XOps& o, uint32_t aA0, uint32_t aA1, 
   }
 }
 
+// wait until the y youngest stages (D DMAs each, 0 <= y <= 4) may stay in flight
+template <int D>
+PT2Q_DEV void x_vmwait(int y) {
+  switch (y) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * D) : "memory"); break;
+  }
+}
+
 struct XArgs {
   GemmDesc g;
   int tiles_m, tiles_n;
   int order;  // 0 row-major tiles, 1 upper (XCD super-tiles), 2 upper by columns (lauum)
 };
 
-template <int NS>
+template <int NS, int KR>
 __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
+  using GE = XGeo<KR>;
+  constexpr int XSTG = GE::STG, XPANEL = GE::PANEL, XDMA = GE::DMA, XK = KR;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * XSTG];
   const GemmDesc& g = X.g;
   int ti, tj;
@@ -195,15 +215,13 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
       }
     }
   asm volatile("" ::: "memory");
-  // prologue DMA: stages 0 and 1 (NS = 3) or 0 (NS = 2)
-  if (nst > 0) {
-    x_panel_dma(Ab, g.lda, i0, g.M, kbeg, kend, smem);
-    x_panel_dma(Bb, g.ldb, j0, g.N, kbeg, kend, smem + XPANEL);
-  }
-  if (NS == 3 && nst > 1) {
-    x_panel_dma(Ab, g.lda, i0, g.M, kbeg + XK, kend, smem + XSTG);
-    x_panel_dma(Bb, g.ldb, j0, g.N, kbeg + XK, kend, smem + XSTG + XPANEL);
-  }
+  // prologue DMA: stages 0 .. NS-2
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nst) {
+      x_panel_dma<KR>(Ab, g.lda, i0, g.M, kbeg + p * XK, kend, smem + p * XSTG);
+      x_panel_dma<KR>(Bb, g.ldb, j0, g.N, kbeg + p * XK, kend, smem + p * XSTG + XPANEL);
+    }
   f32x16 acc[2][2];
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
@@ -231,16 +249,14 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
     // stage t landed (this wave's DMAs; stage t+1 may stay in flight), then a raw barrier (the
     // fence of __syncthreads would wait vmcnt(0)); the barrier also retires every wave's reads
     // of the slot the next DMA reuses
-    if (NS == 3 && t + 1 < nst)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * XDMA) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (younger stages in flight: t+1 .. min(t+NS-2, nst-1))
+    x_vmwait<2 * XDMA>(min(NS - 2, nst - 1 - t));
     asm volatile("s_barrier" ::: "memory");
     const int tn = t + NS - 1;
     if (tn < nst) {
       uint8_t* st = smem + (tn % NS) * XSTG;
-      x_panel_dma(Ab, g.lda, i0, g.M, kbeg + tn * XK, kend, st);
-      x_panel_dma(Bb, g.ldb, j0, g.N, kbeg + tn * XK, kend, st + XPANEL);
+      x_panel_dma<KR>(Ab, g.lda, i0, g.M, kbeg + tn * XK, kend, st);
+      x_panel_dma<KR>(Bb, g.ldb, j0, g.N, kbeg + tn * XK, kend, st + XPANEL);
     }
     const uint32_t sb = lds0 + (uint32_t)((t % NS) * XSTG);
     x_chain<0, XK / 2>(acc, o, sb + oA0, sb + oA1, sb + oB0, sb + oB1);
@@ -291,10 +307,12 @@ int pt2q_launch_gemmx(const GemmDesc& g, hipStream_t st) {
     tiles = (long)X.tiles_m * X.tiles_n;
   }
   const dim3 grid((unsigned)tiles, (unsigned)(g.batch > 1 ? g.batch : 1));
-  if (pt2q_tuning().gemmx_stages == 2)  // 64 KiB of LDS: two workgroups per CU
-    hipLaunchKernelGGL(gemmx_kernel<2>, grid, dim3(256), 0, st, X);
-  else
-    hipLaunchKernelGGL(gemmx_kernel<3>, grid, dim3(256), 0, st, X);
+  switch (pt2q_tuning().gemmx_stages) {
+    case 3: hipLaunchKernelGGL((gemmx_kernel<3, 32>), grid, dim3(256), 0, st, X); break;  // 96 KiB
+    case 4: hipLaunchKernelGGL((gemmx_kernel<4, 16>), grid, dim3(256), 0, st, X); break;  // 64 KiB, 2 WGs/CU
+    case 5: hipLaunchKernelGGL((gemmx_kernel<5, 16>), grid, dim3(256), 0, st, X); break;  // 80 KiB, 2 WGs/CU
+    default: hipLaunchKernelGGL((gemmx_kernel<2, 32>), grid, dim3(256), 0, st, X); break;  // 64 KiB, 2 WGs/CU
+  }
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }
