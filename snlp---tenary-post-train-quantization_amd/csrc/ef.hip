@@ -192,6 +192,12 @@ PT2Q_DEV int ef_col(int i0, int rn, int q) {
 PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm, int rn, int q) {
   const int i = ef_col(i0, rn, q);
   if (wrow[rm] < 0 || i >= a.ldw || probe::ef_drop_wt) return EF_DROP;
+  if constexpr (probe::ef_row_io) {  // (identity rem: wrow[0] = e0 + wr * 64 + lane % 32)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31;
+    const int e0 = wrow[0] - ((wave >> 1) * 64 + li);
+    const int row = e0 + wave * 32 + (rm * 8 + rn * 4 + q) * 2 + (lane >> 5);
+    return (unsigned)(((long)row * a.ldw + i0 + 4 * li) * 4);
+  }
   return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
 }
 

@@ -16,6 +16,8 @@ constexpr bool ef_no_mfma = (PT2Q_PROBE & 16) != 0;   // tools/ef_probe.hip: no 
 constexpr bool ef_zero_dma = (PT2Q_PROBE & 32) != 0;  // tools/ef_probe.hip: operand DMAs from one chunk
 constexpr bool ef_stamps = (PT2Q_PROBE & 64) != 0;    // tools/ef_probe.hip: per-tile phase timestamps
 constexpr bool ef_no_dma = (PT2Q_PROBE & 128) != 0;   // tools/ef_probe.hip: no operand DMAs (stale LDS)
+constexpr bool ef_row_io = (PT2Q_PROBE & 256) != 0;   // tools/ef_probe.hip: Wt IO as 2 whole 512-B row
+                                                      // segments per instruction (identity rem; values garbage)
 }  // namespace probe
 
 #if (PT2Q_PROBE & 4) != 0

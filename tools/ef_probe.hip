@@ -33,6 +33,8 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(Et, h.data() + 7, (size_t)bs * n * 4, hipMemcpyHostToDevice);
   std::vector<int> r(m);
   for (int e = 0; e < m; ++e) r[e] = (int)(((long)e * 7919 + 3) % m);  // a permutation (gcd(7919, m) = 1)
+  if (PT2Q_PROBE & 256)
+    for (int e = 0; e < m; ++e) r[e] = e;  // ef_row_io needs the identity
   (void)hipMemcpy(crow, r.data(), m * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
