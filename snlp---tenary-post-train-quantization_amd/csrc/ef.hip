@@ -94,6 +94,49 @@ PT2Q_DEV int ef_stage(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, bool
   return withB ? EF_DMA : EF_DMA / 2;
 }
 
+// Fast staging (every k row and column of the stage in range: all tiles but ragged edges): this
+// lane's byte offsets of its 8 A and 8 B chunks from the stage's panel bases, fixed for the launch
+// (ldk and ldw are common to a group's linears), so a DMA is s_mov m0 + one global_load_lds with a
+// scalar base -- three instructions instead of the ~35 of ef_stage_q's per-lane address math,
+// which held every stage issue to ~1 us (tools/ef_probe.hip stamps).
+struct EfVo {
+  uint32_t a[8], b[8];
+};
+
+PT2Q_DEV void ef_voff(const EfArgs& a, EfVo& v) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int kr = (wave * 8 + q) * 2 + (lane >> 5), d = 4 * (lane & 31);
+    v.a[q] = (uint32_t)(((long)kr * a.ldk + d) * 4);
+    v.b[q] = (uint32_t)(((long)kr * a.ldw + d) * 4);
+  }
+}
+
+// one 16-B LDS-DMA: global (sbase + voff) -> LDS m0 + 16 lane (m0 is set afresh by every DMA)
+PT2Q_DEV void ef_dma_asm(const char* sbase, uint32_t voff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0)
+               : "memory");
+}
+
+// a stage by the fast path when it is whole, else by ef_stage; returns the DMAs issued per wave
+PT2Q_DEV int ef_stage_any(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, uint32_t stg_lds, const EfVo& v,
+                          bool withB) {
+  const bool fast = (h + 1) * EF_KH <= a.bs && e0 + EF_T <= a.nr && i0 + EF_T <= a.ldw &&
+                    !probe::ef_zero_dma && !probe::ef_no_dma;
+  if (!fast) return ef_stage(a, e0, i0, h, stg, withB);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* ba = (const char*)(a.Ck + (long)h * EF_KH * a.ldk + e0);
+  const char* bb = (const char*)(a.Et + (long)h * EF_KH * a.ldw + i0);
+  const uint32_t mA = stg_lds + (uint32_t)(wv * 8 * 1024), mB = mA + EF_PANEL;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ef_dma_asm(ba, v.a[q], mA + q * 1024);
+    if (withB) ef_dma_asm(bb, v.b[q], mB + q * 1024);
+  }
+  return withB ? EF_DMA : EF_DMA / 2;
+}
+
 template <int OFF>
 PT2Q_DEV float ef_ld(uint32_t addr) {
   float r;
@@ -192,13 +235,20 @@ PT2Q_DEV int ef_col(int i0, int rn, int q) {
 PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm, int rn, int q) {
   const int i = ef_col(i0, rn, q);
   if (wrow[rm] < 0 || i >= a.ldw || probe::ef_drop_wt) return EF_DROP;
-  if constexpr (probe::ef_row_io) {  // (identity rem: wrow[0] = e0 + wr * 64 + lane % 32)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31;
-    const int e0 = wrow[0] - ((wave >> 1) * 64 + li);
-    const int row = e0 + wave * 32 + (rm * 8 + rn * 4 + q) * 2 + (lane >> 5);
-    return (unsigned)(((long)row * a.ldw + i0 + 4 * li) * 4);
-  }
   return (unsigned)(((long)wrow[rm] * a.ldw + i) * 4);
+}
+
+// ef_coff as a per-tile row base: group (rm, rn, q) of this lane sits at rb[rm] + 4 (32 rn + 8 q)
+// bytes (the constant folds into the buffer instruction's offset field), rb[rm] = EF_DROP for a row
+// past nr or a column half past ldw (ldw % 64 == 0, so a wave's 64 columns are in or out together)
+PT2Q_DEV void ef_rowbase(const EfArgs& a, const int (&wrow)[2], int i0, uint32_t (&rb)[2]) {
+  const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
+  const int i = i0 + wc * 64 + 4 * (lane >> 5);
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+    rb[rm] = (wrow[rm] < 0 || i0 + wc * 64 >= a.ldw || probe::ef_drop_wt)
+                 ? EF_DROP
+                 : (uint32_t)(((long)wrow[rm] * a.ldw + i) * 4);
 }
 
 // the Wt rows of this lane's two output rows (crow from L2: two loads per lane, issued uniformly
@@ -303,10 +353,9 @@ struct EfIO {
   const EfArgs& a;
   __amdgpu_buffer_rsrc_t rc;   // this tile's Wt (old values)
   __amdgpu_buffer_rsrc_t prc;  // the previous tile's Wt (its results), possibly another linear's
-  const int (&prow)[2];
-  int pi0;
-  const int (&wrow)[2];
-  int i0;
+  const int (&prow)[2];          // the previous tile's Wt rows (-1 past nr): its w-bar pieces
+  const uint32_t (&rb)[2];       // ef_rowbase of this tile (old values)
+  const uint32_t (&prb)[2];      // ef_rowbase of the previous tile (its results)
   const u32x4 (&pend)[EF_CV];
   u32x4 (&c)[EF_CV];
   float* red;  // the previous tile's w-bar wave sums (ef_wbar_step)
@@ -319,7 +368,7 @@ struct EfIO {
   PT2Q_DEV void g0() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
-      __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, ef_coff(a, prow, pi0, rm, rn, q), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(pend[j], prc, prb[rm] + 4 * (32 * rn + 8 * q), 0, 0);
     }
     if constexpr (S % 2 == 1) ef_wb_a<S - 1>(w, prow, pend);
   }
@@ -327,7 +376,7 @@ struct EfIO {
   PT2Q_DEV void g1() {
     if constexpr (S % 2 == 0 && S / 2 < EF_CV) {
       constexpr int j = S / 2, rm = j >> 3, rn = (j >> 2) & 1, q = j & 3;
-      c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, ef_coff(a, wrow, i0, rm, rn, q), 0, 0);
+      c[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, rb[rm] + 4 * (32 * rn + 8 * q), 0, 0);
     }
     if constexpr (S % 2 == 1) ef_wb_b(w);
   }
@@ -419,8 +468,10 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   ef_rows(a, e0, wrow);
-  ef_stage(a, e0, i0, 0, smem);
-  if (a.nh == 2) ef_stage(a, e0, i0, 1, smem + EF_STAGE);
+  EfVo vo;
+  ef_voff(a0, vo);
+  ef_stage_any(a, e0, i0, 0, smem, lds0, vo, true);
+  if (a.nh == 2) ef_stage_any(a, e0, i0, 1, smem + EF_STAGE, lds0 + EF_STAGE, vo, true);
   // P dropped stores: every tile's first wait then sees the same count of younger operations
   for (int j = 0; j < P; ++j) __builtin_amdgcn_raw_buffer_store_b128(u32x4{}, rc, EF_DROP, 0, 0);
   int prow[2] = {-1, -1}, pi0 = 0, pe0 = -1;
@@ -455,13 +506,19 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     PT2Q_EF_STAMP(nt, 2);
     if (more) ef_rows(an, en, nrow);
     {
-      EfIO io{a, rc, prc, prow, pi0, wrow, i0, pend, c, red, {}};
+      uint32_t rb[2], prb[2];
+      ef_rowbase(a, wrow, i0, rb);
+      ef_rowbase(a, prow, pi0, prb);
+      EfIO io{a, rc, prc, prow, rb, prb, pend, c, red, {}};
       F.half(lds0, io);
     }
     PT2Q_EF_STAMP(nt, 3);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with stage 0
-    if (more) D0 = ef_stage(an, en, in, 0, smem, newB);
+    PT2Q_EF_STAMP(nt, 8);
+    if (more) D0 = ef_stage_any(an, en, in, 0, smem, lds0, vo, newB);
+    PT2Q_EF_STAMP(nt, 9);
     if (P) ef_wbar_store(a0.n, prp, pe0 >= 0, pe0, pi0, red);  // the previous tile's partials
+    PT2Q_EF_STAMP(nt, 10);
     if (a.nh == 2) {
       ef_vmcnt(P + 2 * EF_CV + D0);  // stage 1 landed
       PT2Q_EF_STAMP(nt, 4);
@@ -470,7 +527,7 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
       EfNoIO nio;
       F.half(lds0 + EF_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (more) D1 = ef_stage(an, en, in, 1, smem + EF_STAGE, newB);
+      if (more) D1 = ef_stage_any(an, en, in, 1, smem + EF_STAGE, lds0 + EF_STAGE, vo, newB);
     }
     PT2Q_EF_STAMP(nt, 6);
     ef_vmcnt(more ? D0 + P + D1 : 0);  // the old values landed (younger: next stages, part stores)

@@ -16,8 +16,6 @@ constexpr bool ef_no_mfma = (PT2Q_PROBE & 16) != 0;   // tools/ef_probe.hip: no 
 constexpr bool ef_zero_dma = (PT2Q_PROBE & 32) != 0;  // tools/ef_probe.hip: operand DMAs from one chunk
 constexpr bool ef_stamps = (PT2Q_PROBE & 64) != 0;    // tools/ef_probe.hip: per-tile phase timestamps
 constexpr bool ef_no_dma = (PT2Q_PROBE & 128) != 0;   // tools/ef_probe.hip: no operand DMAs (stale LDS)
-constexpr bool ef_row_io = (PT2Q_PROBE & 256) != 0;   // tools/ef_probe.hip: Wt IO as 2 whole 512-B row
-                                                      // segments per instruction (identity rem; values garbage)
 }  // namespace probe
 
 #if (PT2Q_PROBE & 4) != 0
@@ -33,7 +31,7 @@ __device__ long long topk_stamps[64][16];
 // thread 0 of each of the first 64 workgroups of the EF launch: s_memrealtime (100 MHz) at phase i of its
 // first 8 tiles (ef_stamps[wg][tile][i]); ef_stamp_tile counts the workgroup's tiles
 // (ef_clk: s_memtime, the shader clock, at phases 0 and 7: the clock the kernel ran at)
-__device__ long long ef_stamps[64][8][8];
+__device__ long long ef_stamps[64][8][12];
 __device__ long long ef_clk[64][8][2];
 #define PT2Q_EF_STAMP(tile, i)                                                   \
   if (threadIdx.x == 0 && blockIdx.x < 64 && (tile) < 8) {                       \

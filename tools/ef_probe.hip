@@ -33,8 +33,6 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(Et, h.data() + 7, (size_t)bs * n * 4, hipMemcpyHostToDevice);
   std::vector<int> r(m);
   for (int e = 0; e < m; ++e) r[e] = (int)(((long)e * 7919 + 3) % m);  // a permutation (gcd(7919, m) = 1)
-  if (PT2Q_PROBE & 256)
-    for (int e = 0; e < m; ++e) r[e] = e;  // ef_row_io needs the identity
   (void)hipMemcpy(crow, r.data(), m * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -61,9 +59,25 @@ int main(int argc, char** argv) {
   // phase durations (s_memrealtime ticks, 100 MHz -> us) of tiles 1..6 of the first 64 workgroups
   // (the stamps of the last launch): 0 top, 1 stage 0 landed, 2 barrier, 3 half 0 done,
   // 4 stage 1 landed, 5 barrier, 6 half 1 done, 7 old values landed
-  static long long st[64][8][8];
+  static long long st[64][8][12];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(ef_stamps), sizeof(st));
   const char* nm[8] = {"wait stage0", "barrier0", "half0", "wait stage1", "barrier1", "half1", "wait old Wt", "epilogue+loop"};
+  {  // the mid-tile gap (3 -> 4) in pieces: lgkmcnt + barrier, next stage-0 DMA issue, w-bar store, vmcnt
+    double g[4] = {0};
+    int c2 = 0;
+    for (int w = 0; w < 64; ++w)
+      for (int t = 1; t < 7; ++t) {
+        if (!st[w][t][3] || !st[w][t][8]) continue;
+        g[0] += (double)(st[w][t][8] - st[w][t][3]);
+        g[1] += (double)(st[w][t][9] - st[w][t][8]);
+        g[2] += (double)(st[w][t][10] - st[w][t][9]);
+        g[3] += (double)(st[w][t][4] - st[w][t][10]);
+        ++c2;
+      }
+    if (c2)
+      printf("  mid-tile: barrier %.2f us, stage-0 DMA issue %.2f us, w-bar store %.2f us, stage-1 wait %.2f us\n",
+             g[0] / c2 / 100.0, g[1] / c2 / 100.0, g[2] / c2 / 100.0, g[3] / c2 / 100.0);
+  }
   double sum[8] = {0};
   int cnt = 0;
   for (int w = 0; w < 64; ++w)
