@@ -95,6 +95,35 @@ PT2Q_DEV void x_panel_dma(const float* base, long ld, int d0, int DMAX, int k0, 
   }
 }
 
+// Fast staging of a whole in-range panel (rows [k0, k0 + KR) below kend, columns [d0, d0 + 128)
+// below DMAX): this lane's byte offsets from the panel's first element, fixed for the launch, and a
+// scalar base -- s_mov m0 + one global_load_lds per chunk instead of per-lane address math.
+template <int KR>
+PT2Q_DEV void x_panel_voff(long ld, uint32_t (&vo)[XGeo<KR>::DMA]) {
+  constexpr int XDMA = XGeo<KR>::DMA;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int q = 0; q < XDMA; ++q) {
+    const int L = (wave * XDMA + q) * 64 + lane;
+    const int kr = L >> 5, c = (L & 31) ^ ((kr & 1) << 3);
+    vo[q] = (uint32_t)(((long)kr * ld + 4 * c) * 4);
+  }
+}
+
+template <int KR>
+PT2Q_DEV void x_panel_dma_fast(const float* base, long ld, int d0, int k0, const uint32_t (&vo)[XGeo<KR>::DMA],
+                               uint32_t pan) {
+  constexpr int XDMA = XGeo<KR>::DMA;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* sb = (const char*)(base + (long)k0 * ld + d0);
+#pragma unroll
+  for (int q = 0; q < XDMA; ++q)
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(vo[q]), "s"(sb),
+                 "s"(pan + (uint32_t)((wave * XDMA + q) * 1024))
+                 : "memory");
+}
+
 template <int OFF>
 PT2Q_DEV float x_ld(uint32_t addr) {
   float r;
@@ -215,13 +244,24 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
       }
     }
   asm volatile("" ::: "memory");
-  // prologue DMA: stages 0 .. NS-2
+  // prologue DMA: stages 0 .. NS-2 (stage p is whole -- the fast path -- when p < nfull)
+  uint32_t voA[XDMA], voB[XDMA];
+  x_panel_voff<KR>(g.lda, voA);
+  x_panel_voff<KR>(g.ldb, voB);
+  const uint32_t ldsb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  const int nfull = (i0 + XT <= g.M && j0 + XT <= g.N) ? (kend - kbeg) / XK : 0;
+  auto stage = [&](int p) {
+    if (p < nfull) {
+      x_panel_dma_fast<KR>(Ab, g.lda, i0, kbeg + p * XK, voA, ldsb + (uint32_t)((p % NS) * XSTG));
+      x_panel_dma_fast<KR>(Bb, g.ldb, j0, kbeg + p * XK, voB, ldsb + (uint32_t)((p % NS) * XSTG + XPANEL));
+    } else {
+      x_panel_dma<KR>(Ab, g.lda, i0, g.M, kbeg + p * XK, kend, smem + (p % NS) * XSTG);
+      x_panel_dma<KR>(Bb, g.ldb, j0, g.N, kbeg + p * XK, kend, smem + (p % NS) * XSTG + XPANEL);
+    }
+  };
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nst) {
-      x_panel_dma<KR>(Ab, g.lda, i0, g.M, kbeg + p * XK, kend, smem + p * XSTG);
-      x_panel_dma<KR>(Bb, g.ldb, j0, g.N, kbeg + p * XK, kend, smem + p * XSTG + XPANEL);
-    }
+    if (p < nst) stage(p);
   f32x16 acc[2][2];
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
@@ -253,11 +293,7 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
     x_vmwait<2 * XDMA>(min(NS - 2, nst - 1 - t));
     asm volatile("s_barrier" ::: "memory");
     const int tn = t + NS - 1;
-    if (tn < nst) {
-      uint8_t* st = smem + (tn % NS) * XSTG;
-      x_panel_dma<KR>(Ab, g.lda, i0, g.M, kbeg + tn * XK, kend, st);
-      x_panel_dma<KR>(Bb, g.ldb, j0, g.N, kbeg + tn * XK, kend, st + XPANEL);
-    }
+    if (tn < nst) stage(tn);
     const uint32_t sb = lds0 + (uint32_t)((t % NS) * XSTG);
     x_chain<0, XK / 2>(acc, o, sb + oA0, sb + oA1, sb + oB0, sb + oB1);
   }
