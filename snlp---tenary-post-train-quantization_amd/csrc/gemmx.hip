@@ -146,8 +146,33 @@ PT2Q_DEV void x_read(XOps& o, uint32_t aA0, uint32_t aA1, uint32_t aB0, uint32_t
   o.v[c][3] = x_ld<off>(aB1);
 }
 
-template <int S, int NP>
-PT2Q_DEV void x_chain(f32x16 (&acc)[2][2], XOps& o, uint32_t aA0, uint32_t aA1, uint32_t aB0, uint32_t aB1) {
+// the next stage's fast DMAs, one A and one B chunk after the first MFMA of k-pair q (q < DMA), so
+// their issue sits in MFMA shadows instead of in front of the stage (on = false: nothing)
+template <int KR>
+struct XStageIO {
+  const char* sbA;
+  const char* sbB;
+  const uint32_t (&voA)[XGeo<KR>::DMA];
+  const uint32_t (&voB)[XGeo<KR>::DMA];
+  uint32_t mA, mB;
+  bool on;
+  template <int S>
+  PT2Q_DEV void at() {
+    if constexpr (S < XGeo<KR>::DMA) {
+      if (on) {
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voA[S]), "s"(sbA),
+                     "s"(mA + S * 1024)
+                     : "memory");
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voB[S]), "s"(sbB),
+                     "s"(mB + S * 1024)
+                     : "memory");
+      }
+    }
+  }
+};
+
+template <int S, int NP, class IO>
+PT2Q_DEV void x_chain(f32x16 (&acc)[2][2], XOps& o, uint32_t aA0, uint32_t aA1, uint32_t aB0, uint32_t aB1, IO& io) {
   if constexpr (S == 0) {
     x_read<0>(o, aA0, aA1, aB0, aB1);
     x_read<1>(o, aA0, aA1, aB0, aB1);
@@ -161,11 +186,14 @@ PT2Q_DEV void x_chain(f32x16 (&acc)[2][2], XOps& o, uint32_t aA0, uint32_t aA1, 
       asm volatile("" ::"v"(o.v[p][0]), "v"(o.v[p][1]), "v"(o.v[p][2]), "v"(o.v[p][3]));
     }
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < 2; ++rn)  // transposed tile: lane <-> C row (16-byte epilogue)
-        acc[rm][rn] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.v[c][2 + rn], o.v[c][rm], acc[rm][rn], 0, 0, 0);
+    // transposed tile: lane <-> C row (16-byte epilogue)
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.v[c][2], o.v[c][0], acc[0][0], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    io.template at<S>();
+    __builtin_amdgcn_sched_barrier(0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.v[c][3], o.v[c][0], acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.v[c][2], o.v[c][1], acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(o.v[c][3], o.v[c][1], acc[1][1], 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + 1 < NP) {  // pair S+1 landed (pair S+2 may stay in flight)
       constexpr int c1 = (S + 1) % 4;
@@ -174,7 +202,7 @@ PT2Q_DEV void x_chain(f32x16 (&acc)[2][2], XOps& o, uint32_t aA0, uint32_t aA1, 
       else
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o.v[c1][0]), "+v"(o.v[c1][1]), "+v"(o.v[c1][2]), "+v"(o.v[c1][3]));
     }
-    x_chain<S + 1, NP>(acc, o, aA0, aA1, aB0, aB1);
+    x_chain<S + 1, NP>(acc, o, aA0, aA1, aB0, aB1, io);
   }
 }
 
@@ -250,6 +278,7 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
   x_panel_voff<KR>(g.ldb, voB);
   const uint32_t ldsb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   const int nfull = (i0 + XT <= g.M && j0 + XT <= g.N) ? (kend - kbeg) / XK : 0;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   auto stage = [&](int p) {
     if (p < nfull) {
       x_panel_dma_fast<KR>(Ab, g.lda, i0, kbeg + p * XK, voA, ldsb + (uint32_t)((p % NS) * XSTG));
@@ -293,9 +322,15 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
     x_vmwait<2 * XDMA>(min(NS - 2, nst - 1 - t));
     asm volatile("s_barrier" ::: "memory");
     const int tn = t + NS - 1;
-    if (tn < nst) stage(tn);
+    // a whole next stage goes out inside the chain (XStageIO), any other one here
+    const bool fastn = tn < nfull;
+    if (tn < nst && !fastn) stage(tn);
+    XStageIO<KR> sio{(const char*)(Ab + (long)(kbeg + tn * XK) * g.lda + i0),
+                     (const char*)(Bb + (long)(kbeg + tn * XK) * g.ldb + j0), voA, voB,
+                     ldsb + (uint32_t)((tn % NS) * XSTG + wv * XDMA * 1024),
+                     ldsb + (uint32_t)((tn % NS) * XSTG + XPANEL + wv * XDMA * 1024), tn < nst && fastn};
     const uint32_t sb = lds0 + (uint32_t)((t % NS) * XSTG);
-    x_chain<0, XK / 2>(acc, o, sb + oA0, sb + oA1, sb + oB0, sb + oB1);
+    x_chain<0, XK / 2>(acc, o, sb + oA0, sb + oA1, sb + oB0, sb + oB1, sio);
   }
   // epilogue
   const bool mirror = g.upper && g.mirror && ti != tj;
