@@ -244,11 +244,22 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
   float p = 0.0f;
   typedef float f4 __attribute__((ext_vector_type(4)));
   if constexpr (NV > 0) {
-    f4 v[NV];
+    // NV <= 16: the column and the (shared, L2-resident) mean vector are both loaded up front, so
+    // the dot pass does not wait a second L2 round trip after the norm (NV = 48 keeps the mean's
+    // loads in the dot loop: 256 VGPRs)
+    constexpr bool PRE = NV <= 16;
+    f4 v[NV], w[PRE ? NV : 1];
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const long base = 4 * t + 256 * u;
       if (base < n) v[u] = *(const f4*)(x + base);
+    }
+    if constexpr (PRE) {
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const long base = 4 * t + 256 * u;
+        if (base < n) w[u] = *(const f4*)(wn + base);
+      }
     }
     float ss = 0.0f;
 #pragma unroll
@@ -265,11 +276,11 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
     for (int u = 0; u < NV; ++u) {
       const long base = 4 * t + 256 * u;
       if (base < n) {
-        const f4 w = *(const f4*)(wn + base);
-        p = fmaf(v[u][0] / nj, w[0], p);
-        p = fmaf(v[u][1] / nj, w[1], p);
-        p = fmaf(v[u][2] / nj, w[2], p);
-        p = fmaf(v[u][3] / nj, w[3], p);
+        const f4 wu = PRE ? w[PRE ? u : 0] : *(const f4*)(wn + base);
+        p = fmaf(v[u][0] / nj, wu[0], p);
+        p = fmaf(v[u][1] / nj, wu[1], p);
+        p = fmaf(v[u][2] / nj, wu[2], p);
+        p = fmaf(v[u][3] / nj, wu[3], p);
       }
     }
   } else if ((n & 3) == 0 && (ldw & 3) == 0) {
