@@ -19,4 +19,4 @@ for w in "4096 24" "11008 8"; do
   run g$1_write "WRITE_SIZE" grams 262144 $1 $2 2
   run g$1_hit "TCC_HIT_sum TCC_MISS_sum" grams 262144 $1 $2 2
 done
-python3 $R/tools/pmc_multi.py $OUT/g4096_* $OUT/g11008_* > $OUT/summary.txt && cat $OUT/summary.txt
+python3 $R/tools/pmc_multi.py $OUT/g4096_mfma $OUT/g4096_fetch $OUT/g4096_write $OUT/g11008_mfma $OUT/g11008_fetch $OUT/g11008_write > $OUT/summary.txt && cat $OUT/summary.txt
