@@ -13,7 +13,6 @@ import pt2q_loader  # noqa: E402
 pt2q = pt2q_loader.load()
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-tag = os.environ.get("PT2Q_GRAM_MFMA16", "1")
 for m, count in ((4096, 96), (11008, 32)):
     X = pt2q.fill_synthetic((N, m), 79, outliers=True).half()
     G = torch.empty(count, m, m, device=X.device)
@@ -27,6 +26,6 @@ for m, count in ((4096, 96), (11008, 32)):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     fl = float(N) * m * (m + 1) * count
-    print(f"mfma16={tag} m={m} x{count}: {ms:.1f} ms/launch  {fl / ms / 1e9:.0f} TF/s work done", flush=True)
+    print(f"m={m} x{count}: {ms:.1f} ms/launch  {fl / ms / 1e9:.0f} TF/s work done", flush=True)
     del X, G
     torch.cuda.empty_cache()
