@@ -153,11 +153,19 @@ def config_runs(a, dev):
             torch.cuda.synchronize()
             s = (time.perf_counter() - t0) / b.steps
             cols = sharding.units_cols(w.units)
+            # live roofline of this config: phase walls + one-lane stage busy times (outside the timing)
+            ph = w.phase_step()
+            busy = w.stage_busy()
+            peak = MI355X_F32_MFMA_PEAK_TFLOPS if b.io_dtype == "fp32" else MI355X_F16_MFMA_PEAK_TFLOPS
+            st = stage_roofline(model_work(w.units, b.block_size, IO_BYTES[b.io_dtype], not b.no_ssr), ph, busy,
+                                s * 1e3, 1, peak)
             out[name] = {"config": sharding.MODELS[name]["config"], "workload": describe_units(w.units, b.layers),
                          "tokens": b.tokens, "block_size": b.block_size if b.block_size < (1 << 14) else "m (per-channel)",
                          "io_dtype": b.io_dtype, "weight_columns_per_step": cols, "ms_per_step": s * 1e3,
                          "cols_per_s": cols / s, "s_per_decoder_layer": s / b.layers,
-                         "steps": b.steps, "warmup": b.warmup}
+                         "steps": b.steps, "warmup": b.warmup,
+                         "roofline": {"dominant": st["dominant"], "floor_s": st["step"]["floor_s"],
+                                      "frac_step": st["step"]["frac"], "phase_s": ph, "stages": st}}
             del w
             gc.collect()
         except Exception as e:  # a config that fails is reported, not allowed to drop the line
@@ -340,11 +348,13 @@ def gram_time_ms(X, m, reps=3):
     return ev0.elapsed_time(ev1) / reps
 
 
-def gram_batched_time_ms(X, m, count, reps=2):
-    """Average time of ONE batched Gram launch over `count` Grams of X (pt2q_gram_batched, as the
-    step issues it), HIP events on torch's current stream (the launch stream)."""
-    G = torch.empty((count, m, m), dtype=torch.float32, device=X.device)
-    Xs = [X] * count
+def gram_batched_time_ms(Xl, m, count, reps=2):
+    """Average time of ONE batched Gram launch over `count` Grams (pt2q_gram_batched, as the
+    step issues it) of the activation tensors Xl rotated over the items (item z reads
+    Xl[z % len(Xl)], as ModelStep's units do), HIP events on torch's current stream (the launch
+    stream)."""
+    G = torch.empty((count, m, m), dtype=torch.float32, device=Xl[0].device)
+    Xs = [Xl[z % len(Xl)] for z in range(count)]
     pt2q.engine.gram_batched(Xs, G)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
@@ -364,8 +374,16 @@ def load_traffic():
     return None
 
 
+X_DISTINCT = 4  # distinct resident activation tensors per input width, rotated over its units
+
+
 class ModelStep:
-    """This rank's share of the model: resident inputs, per-width workspaces, one step."""
+    """This rank's share of the model: resident inputs, per-width workspaces, one step.
+
+    Activations: X_DISTINCT distinct tensors per input width, rotated over that width's units
+    (unit j of a width reads tensor j % X_DISTINCT), so the items of one batched Gram launch
+    stream different rows -- a real model's layers have their own activations, and a single
+    shared tensor would let concurrent items hit each other's X lines in L2 / MALL."""
 
     def __init__(self, a, rank, world, dev, io):
         self.units = model_units(a)
@@ -378,14 +396,19 @@ class ModelStep:
                                        overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams)
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
+        self.xi = {}  # unit -> which of its width's activation tensors it reads
         self.index = {u[0]: i for i, u in enumerate(self.units)}
         for i in self.mine:
             name, lins, N = self.units[i]
             m = lins[0][2]
             if m not in self.X:
-                self.X[m] = pt2q.fill_synthetic((N, m), 2000 + 97 * rank + m, std=1.0, outliers=True,
-                                                device=dev).to(io)
+                self.X[m] = []
                 self.ws[m] = self.pipe.workspace(m) if self.pipe else pt2q.UnitWorkspace(m, dev, self.bs)
+            cnt = sum(1 for j in self.xi if self.units[j][1][0][2] == m)
+            if cnt < X_DISTINCT:
+                self.X[m].append(pt2q.fill_synthetic((N, m), 2000 + 97 * rank + m + 7919 * cnt, std=1.0,
+                                                     outliers=True, device=dev).to(io))
+            self.xi[i] = cnt % X_DISTINCT
             for k, (p, n, _) in enumerate(lins):
                 self.W[(i, p)] = pt2q.fill_synthetic((n, m), 100_000 + 16 * i + k, std=0.02,
                                                      device=dev).to(io)
@@ -394,7 +417,7 @@ class ModelStep:
     def provider(self, unit):
         i = self.index[unit[0]]
         _, lins, _ = unit
-        return self.X[lins[0][2]], {p: self.W[(i, p)] for p, _, _ in lins}
+        return self.X[lins[0][2]][self.xi[i]], {p: self.W[(i, p)] for p, _, _ in lins}
 
     def run_unit(self, Ws, X):
         if self.pipe is not None:
@@ -437,74 +460,147 @@ class ModelStep:
         gf.check()
         return t
 
+    def stage_busy(self):
+        """Per-stage busy milliseconds of one grams-first step with the block loops on ONE lane
+        (every launch of the step on one stream at a time), from the library's HIP-event
+        brackets (pt2q_stage_timing: Gram, inverse, setup, SSR, ATQ, EF, outputs).  Outside the
+        timed region."""
+        lib = pt2q._lib
+        lanes = self.gf.pipe.lanes
+        self.gf.pipe.lanes = lanes[:1]
+        try:
+            torch.cuda.synchronize()
+            lib.stage_timing(True)
+            wall = self.phase_step()
+        finally:
+            lib.stage_timing(False)
+            self.gf.pipe.lanes = lanes
+        busy = lib.stage_timing_read()
+        busy["phase_wall_ms"] = {k: v * 1e3 for k, v in wall.items()}
+        return busy
+
 
 # ------------------------------------------------------------------ stage rooflines
 
-TAIL_STAGE = (("ef_gemm", "ef"), ("ssr_", "ssr"), ("atq_", "atq"))
+IO_BYTES = {"fp16": 2, "bf16": 2, "fp32": 4}
 
 
-def model_work(units, bs):
-    """Algorithmic work of one model step per stage: flops and HBM bytes."""
+def model_work(units, bs, io_bytes=2, ssr=True):
+    """Algorithmic work of one model step per stage: flops and HBM bytes.
+    Per-channel units (bs >= m: one block) have no inverse, no error feedback and no SSR pass."""
     w = {k: 0.0 for k in ("gram_fl_2nm2", "gram_fl_done", "gram_bytes", "chol_fl", "ef_fl", "ef_bytes",
-                          "ssr_bytes", "atq_bytes")}
+                          "ssr_bytes", "atq_bytes", "setup_bytes", "out_bytes")}
     for _, lins, N in units:
         m = lins[0][2]
         w["gram_fl_2nm2"] += 2.0 * N * m * m          # §8(d) basis: the full product
         w["gram_fl_done"] += float(N) * m * (m + 1)    # the symmetric half actually formed
-        w["gram_bytes"] += 2.0 * N * m                 # X read once (fp16)
-        w["chol_fl"] += float(m) ** 3                  # potrf + trtri + lauum, m^3/3 each
+        w["gram_bytes"] += float(io_bytes) * N * m     # X read once
         nblk = -(-m // bs) if bs < m else 1
+        if nblk > 1:
+            w["chol_fl"] += float(m) ** 3              # potrf + trtri + lauum, m^3/3 each
         rsum = sum(max(m - (k + 1) * bs, 0) for k in range(nblk))
         for _, n, _ in lins:
             w["ef_fl"] += 2.0 * n * bs * rsum          # W[:, rem] -= E C, K = b
             w["ef_bytes"] += 8.0 * n * rsum            # read + write of W[:, rem] (fp32)
-            # similarity pass over W[:, rem] of every SSR block (r = m, m - b, ...: m + rsum columns)
-            # plus block 0's stand-alone w-bar pass (m columns); later blocks' w-bar partials come
-            # out of the error feedback (no pass over W, DESIGN.md §3 CHUNK128)
-            w["ssr_bytes"] += 4.0 * n * (2 * m + rsum)
-            w["atq_bytes"] += 9.0 * n * m              # W block read, codes + error term written
+            if ssr and nblk > 1:
+                # similarity pass over W[:, rem] of every SSR block (r = m, m - b, ...: m + rsum
+                # columns) plus block 0's stand-alone w-bar pass (m columns); later blocks' w-bar
+                # partials come out of the error feedback (no pass over W, DESIGN.md §3 CHUNK128)
+                w["ssr_bytes"] += 4.0 * n * (2 * m + rsum)
+            # every block's W columns read (fp32) and codes written; the error term E written
+            # for every block that leaves columns behind
+            w["atq_bytes"] += 5.0 * n * m + (4.0 * n * (m - (m - (nblk - 1) * bs)) if nblk > 1 else 0.0)
+            w["setup_bytes"] += (io_bytes + 4.0) * n * m  # W in, feature-major fp32 copy out
+            w["out_bytes"] += 2.0 * n * m              # codes transposed back (int8 in + out)
     return w
 
 
-def stage_roofline(work, phase_s, kern, ms_per_step, world):
-    """roofline.stages: every stage's algorithmic work per step against its peak.  gram /
-    cholesky / tails: live phase walls (bench.py phase_step); ef / ssr / atq: their kernel-busy
-    time in the tail phase of the committed rocprof trace of one step with the block loops on ONE
-    lane (profiles/stage_kernels.json, tools/round_r03.sh -> tools/phase_trace.sh --lanes 1), so
-    each kernel's time is its own, not stretched by co-running lanes."""
-    F32, F16, HBM = MI355X_F32_MFMA_PEAK_TFLOPS * 1e12, MI355X_F16_MFMA_PEAK_TFLOPS * 1e12, MI355X_HBM_PEAK_GBS * 1e9
+STAGE_KERNELS = {"gram": "gram16b_kernel / gram_streamk_kernel", "inverse": "chol_* + rank_update2 + gemmx_kernel",
+                 "setup": "transpose_to_f32 + group_init", "ssr": "ssr_wbar_* + ssr_sim* + ssr_topk",
+                 "atq": "atq_block_kernel / atq_wide_* + atq_post", "ef": "ef_gemm_kernel",
+                 "out": "transpose_i8 / transpose_f32"}
+
+
+def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, committed=None):
+    """roofline.stages: every stage's algorithmic work per step against its peak.  Phase walls
+    (gram / inverse / tails) are live (ModelStep.phase_step); every `kernel_busy_s` is live too:
+    the library's HIP-event brackets around each stage's launches in one grams-first step with
+    the block loops on ONE lane (ModelStep.stage_busy), so a stage's time is its own.  `committed`
+    (profiles/stage_kernels.json, a rocprof trace of the same one-lane step) rides along as a
+    cross-check only."""
+    F32, HBM = MI355X_F32_MFMA_PEAK_TFLOPS * 1e12, MI355X_HBM_PEAK_GBS * 1e9
+    GP = gram_peak_tf * 1e12
+    b = {k: busy.get(k, 0.0) / 1e3 for k in ("gram", "inverse", "setup", "ssr", "atq", "ef", "out")}
+    src = "live: pt2q_stage_timing HIP-event brackets, one-lane grams-first step (bench.py ModelStep.stage_busy)"
     st = {}
-    g = phase_s["gram"]
-    st["gram"] = {"bound": "mfma", "seconds": g, "source": "live phase wall",
-                  "flops_2nm2": work["gram_fl_2nm2"], "frac_2nm2": work["gram_fl_2nm2"] / g / F16,
-                  "flops_done": work["gram_fl_done"], "frac_done": work["gram_fl_done"] / g / F16,
-                  "hbm_frac": work["gram_bytes"] / g / HBM}
-    c = phase_s["inverse"]
-    st["cholesky_inverse"] = {"bound": "mfma", "seconds": c, "source": "live phase wall (batched per width)",
-                              "flops": work["chol_fl"], "frac": work["chol_fl"] / c / F32}
-    st["tails"] = {"seconds": phase_s["tails"], "source": "live phase wall (grouped block loops on the lanes)"}
-    if kern and "tails" in kern:
-        busy = {"ef": 0.0, "ssr": 0.0, "atq": 0.0}
-        for name, (ms, _) in kern["tails"]["kernels"].items():
+    g = b["gram"] or phase_s["gram"]
+    st["gram"] = {"bound": "mfma", "seconds": phase_s["gram"], "kernel_busy_s": b["gram"], "source": src,
+                  "flops_2nm2": work["gram_fl_2nm2"], "frac_2nm2": work["gram_fl_2nm2"] / g / GP,
+                  "flops_done": work["gram_fl_done"], "frac_done": work["gram_fl_done"] / g / GP,
+                  "hbm_frac": work["gram_bytes"] / g / HBM, "peak_tflops": gram_peak_tf}
+    if work["chol_fl"] > 0:
+        c = b["inverse"] or phase_s["inverse"]
+        st["cholesky_inverse"] = {"bound": "mfma", "seconds": phase_s["inverse"], "kernel_busy_s": b["inverse"],
+                                  "source": src, "flops": work["chol_fl"], "frac": work["chol_fl"] / c / F32}
+    else:
+        st["cholesky_inverse"] = {"seconds": phase_s["inverse"], "kernel_busy_s": b["inverse"], "flops": 0.0,
+                                  "note": "per-channel: no inverse (H^-1 feeds only the error feedback)"}
+    st["tails"] = {"seconds": phase_s["tails"], "source": "live phase wall (block loops on the lanes)"}
+    if b["ef"] > 0 and work["ef_fl"] > 0:
+        st["ef"] = {"bound": "mfma+hbm", "kernel_busy_s": b["ef"], "flops": work["ef_fl"],
+                    "frac_mfma": work["ef_fl"] / b["ef"] / F32, "bytes": work["ef_bytes"],
+                    "frac_hbm": work["ef_bytes"] / b["ef"] / HBM, "source": src}
+    if b["ssr"] > 0:
+        st["ssr"] = {"bound": "hbm", "kernel_busy_s": b["ssr"], "bytes": work["ssr_bytes"],
+                     "frac_hbm": work["ssr_bytes"] / b["ssr"] / HBM, "source": src}
+    if b["atq"] > 0:
+        st["atq"] = {"bound": "hbm/latency", "kernel_busy_s": b["atq"], "bytes": work["atq_bytes"],
+                     "frac_hbm": work["atq_bytes"] / b["atq"] / HBM, "source": src}
+    io = b["setup"] + b["out"]
+    if io > 0:
+        st["layout"] = {"bound": "hbm", "kernel_busy_s": io, "bytes": work["setup_bytes"] + work["out_bytes"],
+                        "frac_hbm": (work["setup_bytes"] + work["out_bytes"]) / io / HBM, "source": src,
+                        "what": "W -> feature-major fp32 copies and the result transposes"}
+    if committed and "tails" in committed:
+        cc = {"ef": 0.0, "ssr": 0.0, "atq": 0.0}
+        for name, (ms, _) in committed["tails"]["kernels"].items():
             for pre, stage in TAIL_STAGE:
                 if name.startswith(pre):
-                    busy[stage] += ms / 1e3
-        if busy["ef"] > 0:
-            st["ef"] = {"bound": "mfma+hbm", "kernel_busy_s": busy["ef"], "flops": work["ef_fl"],
-                        "frac_mfma": work["ef_fl"] / busy["ef"] / F32, "bytes": work["ef_bytes"],
-                        "frac_hbm": work["ef_bytes"] / busy["ef"] / HBM, "source": kern.get("source")}
-        if busy["ssr"] > 0:
-            st["ssr"] = {"bound": "hbm", "kernel_busy_s": busy["ssr"], "bytes": work["ssr_bytes"],
-                         "frac_hbm": work["ssr_bytes"] / busy["ssr"] / HBM, "source": kern.get("source")}
-        if busy["atq"] > 0:
-            st["atq"] = {"bound": "hbm/latency", "kernel_busy_s": busy["atq"], "bytes": work["atq_bytes"],
-                         "frac_hbm": work["atq_bytes"] / busy["atq"] / HBM, "source": kern.get("source")}
-    floor = (work["gram_fl_done"] / F16 + work["chol_fl"] / F32 + work["ef_fl"] / F32 +
-             (work["ef_bytes"] + work["ssr_bytes"] + work["atq_bytes"]) / HBM) / max(world, 1)
+                    cc[stage] += ms / 1e3
+        st["cross_check"] = {"kernel_busy_s": cc, "source": "committed:profiles/stage_kernels.json "
+                                                            "(rocprof kernel trace of a one-lane step)"}
+    floor = (work["gram_fl_done"] / GP + work["chol_fl"] / F32 + work["ef_fl"] / F32 +
+             (work["ef_bytes"] + work["ssr_bytes"] + work["atq_bytes"] + work["setup_bytes"] + work["out_bytes"]) / HBM
+             ) / max(world, 1)
     st["step"] = {"floor_s": floor, "frac": floor / (ms_per_step * 1e-3),
-                  "floor": "Gram work done at the 16-bit MFMA peak + Cholesky inverse and EF flops at the "
-                           "f32 MFMA peak + EF/SSR/ATQ bytes at HBM peak, stages back to back, / ranks"}
+                  "floor": "Gram work done at the MFMA peak of its input type + Cholesky inverse and EF flops at "
+                           "the f32 MFMA peak + EF/SSR/ATQ/layout bytes at HBM peak, stages back to back, / ranks"}
+    # the dominant stage: the largest live busy time, against the roofline that bounds it
+    dom = max(("gram", "inverse", "ssr", "atq", "ef"), key=lambda k: b[k])
+    d = {"stage": dom, "kernels": STAGE_KERNELS[dom], "busy_s": b[dom]}
+    if dom == "gram":
+        d.update(bound="mfma", unit="TFLOP/s", achieved=work["gram_fl_done"] / b[dom] / 1e12, peak=gram_peak_tf,
+                 basis="work done N*m*(m+1)")
+    elif dom == "inverse" or dom == "ef":
+        fl = work["chol_fl"] if dom == "inverse" else work["ef_fl"]
+        d.update(bound="mfma", unit="TFLOP/s", achieved=fl / b[dom] / 1e12, peak=MI355X_F32_MFMA_PEAK_TFLOPS)
+    else:
+        by = work["ssr_bytes"] if dom == "ssr" else work["atq_bytes"]
+        d.update(bound="hbm", unit="GB/s", achieved=by / b[dom] / 1e9, peak=MI355X_HBM_PEAK_GBS)
+    d["frac"] = d["achieved"] / d["peak"]
+    st["dominant"] = d
     return st
+
+
+TAIL_STAGE = (("ef_gemm", "ef"), ("ssr_", "ssr"), ("atq_", "atq"))
+
+
+def load_committed_stages():
+    kp = os.path.join(ROOT, "profiles", "stage_kernels.json")
+    if os.path.exists(kp):
+        with open(kp) as f:
+            return json.load(f)
+    return None
 
 
 class LayerStep:
@@ -628,8 +724,12 @@ def main(argv=None):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    step_ms = []
     for i in range(a.steps):
+        ts = time.perf_counter()
         work.step()
+        sync()  # per-step wall (box-to-box and step-to-step spread); the step ends in host reads anyway
+        step_ms.append(1e3 * (time.perf_counter() - ts))
         if a.steps > 3:
             log(rank, f"step {i + 1}/{a.steps}")
     sync()
@@ -648,7 +748,9 @@ def main(argv=None):
         me = {"rank": rank, "units": len(mine),
               "linears": sum(len(work.units[i][1]) for i in mine),
               "cols": sharding.units_cols([work.units[i] for i in mine]),
-              "ms_per_step": 1e3 * t_rank / max(a.steps, 1)}
+              "ms_per_step": 1e3 * t_rank / max(a.steps, 1),
+              "step_ms": {"min": min(step_ms), "median": float(np.median(step_ms)), "max": max(step_ms)}
+              if step_ms else None}
         if a.dry_run:
             me["ran"] = sorted(set(work.ran))
         if world > 1:
@@ -680,7 +782,7 @@ def main(argv=None):
         # the d=4096 q_proj layer alone (s/layer at d=4096): one hipGraph replay per layer
         if a.workload == "model":
             Wl = pt2q.fill_synthetic((d, d), 1000, std=0.02, device=dev).to(io)
-            Xl = work.X.get(d)
+            Xl = work.X[d][0] if d in work.X else None
             if Xl is None:
                 Xl = pt2q.fill_synthetic((N, d), 2000 + d, std=1.0, outliers=True, device=dev).to(io)
             g = pt2q.LayerGraph(Wl, Xl, bs, use_ssr)
@@ -723,13 +825,20 @@ def main(argv=None):
         tot_ms = tot_fl = 0.0
         per_m = {}
         for m, cnt in sorted(mix.items()):
-            Xm = work.X.get(m) if a.workload == "model" else work.Xl
+            Xm = work.X.get(m) if a.workload == "model" else [work.Xl]
             if Xm is None:
-                Xm = pt2q.fill_synthetic((N, m), 2000 + m, std=1.0, outliers=True, device=dev).to(io)
-            ms = gram_batched_time_ms(Xm, m, per_launch[m]) if gb else gram_time_ms(Xm, m)
+                Xm = [pt2q.fill_synthetic((N, m), 2000 + m, std=1.0, outliers=True, device=dev).to(io)]
+            # the step's own activations (X_DISTINCT distinct tensors rotated over the items) set
+            # the line; one tensor shared by every item is timed beside it (cross-item L2 / MALL hits)
+            ms = gram_batched_time_ms(Xm, m, per_launch[m]) if gb else gram_time_ms(Xm[0], m)
             fl = float(N) * m * (m + 1) * per_launch[m]  # unique entries of each symmetric product, 2 flop each
             per_m[str(m)] = {"launches_per_step": nl[m], "grams_per_launch": per_launch[m], "avg_launch_ms": ms,
-                             "ms_per_gram": ms / per_launch[m], "tflops": fl / ms / 1e9}
+                             "ms_per_gram": ms / per_launch[m], "tflops": fl / ms / 1e9,
+                             "distinct_x": len(Xm) if gb else 1}
+            if gb:
+                ms1 = gram_batched_time_ms(Xm[:1], m, per_launch[m])
+                per_m[str(m)]["shared_x"] = {"avg_launch_ms": ms1, "tflops": fl / ms1 / 1e9,
+                                             "note": "every item reads ONE activation tensor"}
             tot_ms += nl[m] * ms
             tot_fl += nl[m] * fl
         avg_ms, avg_fl = tot_ms / launches, tot_fl / launches
@@ -754,13 +863,11 @@ def main(argv=None):
         if a.workload == "model" and work.gf is not None and a.schedule == "grams-first" and world == 1:
             work.phase_step()
             ph = work.phase_step()
-            kern = None
-            kp = os.path.join(ROOT, "profiles", "stage_kernels.json")
-            if os.path.exists(kp):
-                with open(kp) as f:
-                    kern = json.load(f)
+            busy = work.stage_busy()
             roof["phase_s"] = ph
-            roof["stages"] = stage_roofline(model_work(work.units, bs), ph, kern, ms_per_step, world)
+            roof["stage_busy_ms"] = busy
+            roof["stages"] = stage_roofline(model_work(work.units, bs, IO_BYTES[a.io_dtype], use_ssr), ph, busy,
+                                            ms_per_step, world, peak, load_committed_stages())
         tr = load_traffic()
         key = "batched" if gb else "per_item"
         if tr and key in tr and all(str(m) in tr[key]["per_width"] for m in mix):
@@ -769,7 +876,7 @@ def main(argv=None):
             pw = tr[key]["per_width"]
             roof["traffic"] = sum(cnt * pw[str(m)]["fabric_bytes_per_gram"] for m, cnt in mix.items()) / launches
             roof["traffic_algorithmic"] = sum(cnt * 2.0 * N * m for m, cnt in mix.items()) / launches
-            roof["traffic_source"] = tr[key].get("source")
+            roof["traffic_source"] = "committed:profiles/gram_pmc.json (" + str(tr[key].get("source")) + ")"
 
     if rank == 0:
         model_desc = (f"{a.model} shapes: {describe_units(work.units, a.layers)}" if a.workload == "model" else

@@ -71,6 +71,16 @@ extern "C" {
 #define PT2Q_STAGE_AGA 4    /* activation_aware_grid_alignment quantizer.py:177 (given S1, d) */
 #define PT2Q_STAGE_FULL 5   /* quantize                quantizer.py:250 (init+ITF[+AGA]) */
 
+/* stage-timer classes (pt2q_stage_timing) */
+#define PT2Q_TIMER_SETUP 0    /* W -> feature-major fp32 copy, counters, remaining set */
+#define PT2Q_TIMER_SSR 1      /* similarity + top-k / sequential selection (reorder.py:107-143) */
+#define PT2Q_TIMER_ATQ 2      /* ATQ init/ITF/AGA + S1/d + EF coefficients (quantizer.py:250-277) */
+#define PT2Q_TIMER_EF 3       /* error feedback W[:, rem] -= E C (main.py:214) */
+#define PT2Q_TIMER_OUT 4      /* result transposes (main.py:217-230) */
+#define PT2Q_TIMER_GRAM 5     /* pt2q_gram / pt2q_gram_batched / the layer's Gram (main.py:128) */
+#define PT2Q_TIMER_INVERSE 6  /* damping + Cholesky inverse, single or batched (main.py:129-139) */
+#define PT2Q_TIMER_COUNT 7
+
 const char* pt2q_version(void);
 const char* pt2q_strerror(int status);
 
@@ -78,6 +88,19 @@ const char* pt2q_strerror(int status);
  * for an n x m layer with block size b. */
 size_t pt2q_layer_workspace_bytes(int n, int m, int b, int flags);
 size_t pt2q_cholesky_workspace_bytes(int m);
+/* The (smaller) workspace pt2q_quantize_blocks alone needs: status word + block-loop buffers. */
+size_t pt2q_blocks_workspace_bytes(int n, int m, int b, int flags);
+
+/* Measurement only (bench.py's live stage rooflines; no reference counterpart).  While enabled,
+ * each stage of the block-loop entries (pt2q_quantize_blocks / _group / _layer) and every Gram /
+ * Hessian-inverse entry brackets its launches with a pair of HIP events on its stream, tagged by
+ * PT2Q_TIMER_* class.  pt2q_stage_timing(1) clears the log and enables it, (0) disables it;
+ * pt2q_stage_timing_read waits for the recorded events and sums each class's elapsed
+ * milliseconds into ms[0..nstages) (records: number of bracketed intervals).  One host thread, not
+ * under graph capture.  With several streams in flight the intervals overlap other streams' work,
+ * so a caller wanting kernel-busy times runs one stream. */
+int pt2q_stage_timing(int enable);
+int pt2q_stage_timing_read(double* ms, int nstages, int* records);
 
 /* G = XᵀX (accumulate=0), G = G + XᵀX (accumulate=1), or continue (accumulate=2): every
  * entry's chain resumes from G, so Grams streamed batch by batch are bit-identical to one Gram
@@ -131,7 +154,8 @@ int pt2q_hessian_inverse_batched(const float* G, int m, int batch, int64_t nsamp
 /* The block loop of main.py:158-230 (flags & PT2Q_AGA_ACT) or gptq.py:124-199 (PT2Q_AGA_HESS).
  *   W      n x m weights (row-major, wdtype), read only.
  *   A      AGA matrix: raw Gram XᵀX (ACT) or damped H (HESS); m x m; may be NULL for NONE.
- *   Hinv   m x m inverse Hessian.
+ *   Hinv   m x m inverse Hessian; read by the error feedback only, so it may be NULL when
+ *          b >= m (one block: per-channel quantisation, main.py:198 never feeds back).
  *   alpha, mu  n x B fp32 (B = ceil(m/b)), column k = k-th selected block.
  *   T      n x m codes in ORIGINAL column order, int8 (tdtype PT2Q_I8) or fp32 (PT2Q_F32).
  *   perm   m int64, concatenated block indices in selection order.
@@ -150,11 +174,15 @@ int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int n, int m, i
  * alpha[z], mu[z], T[z], perm[z], iters_dev[z] (nullable array / entries) exactly as
  * pt2q_quantize_blocks on that linear alone -- bit for bit.  The pointer arrays are HOST arrays of
  * device pointers, read during the call only.  Supports blocks of <= 128 columns with b < m,
- * PT2Q_AGA_ACT or PT2Q_AGA_NONE, n <= 16384 with n % 4 == 0; else PT2Q_E_UNSUPPORTED (use
+ * PT2Q_AGA_ACT or PT2Q_AGA_NONE, n <= 16384 with n % 4 == 0 (pt2q_quantize_blocks_group_supported); else PT2Q_E_UNSUPPORTED (use
  * pt2q_quantize_blocks per linear).  Replaces main.py:158-230 run over a list of linears (the
  * q/k/v of several decoder layers, main.py:289-299).  workspace:
  * pt2q_quantize_blocks_group_workspace_bytes(count, n, m, b, flags). */
 size_t pt2q_quantize_blocks_group_workspace_bytes(int count, int n, int m, int b, int flags);
+/* 1 if pt2q_quantize_blocks_group takes n x m linears with block b and these flags (every
+ * condition of its PT2Q_E_UNSUPPORTED return, including the tuning overrides and the error
+ * feedback's buffer limits: m % 4 == 0, m * round_up(n, 64) * 4 < 2 GiB), else 0. */
+int pt2q_quantize_blocks_group_supported(int n, int m, int b, int flags);
 int pt2q_quantize_blocks_group(int count, const void* const* W, int wdtype, int64_t ldw, int n, int m,
                                int b, int flags, const float* const* A, int64_t lda,
                                const float* const* Hinv, int64_t ldhi, int max_iter,

@@ -21,6 +21,8 @@ FLAG_SSR = 0x1
 AGA_NONE, AGA_ACT, AGA_HESS = 0x0, 0x10, 0x20
 AGA_MASK = 0x30
 STAGE_INIT, STAGE_GRID, STAGE_ROUND, STAGE_ITF, STAGE_AGA, STAGE_FULL = range(6)
+# stage-timer classes (pt2q_stage_timing, include/pt2q.h PT2Q_TIMER_*)
+TIMERS = ("setup", "ssr", "atq", "ef", "out", "gram", "inverse")
 
 _DT = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16, torch.int8: I8}
 
@@ -46,6 +48,10 @@ _SIGS = {
     "pt2q_strerror": (ctypes.c_char_p, [I]),
     "pt2q_layer_workspace_bytes": (SZ, [I, I, I, I]),
     "pt2q_cholesky_workspace_bytes": (SZ, [I]),
+    "pt2q_blocks_workspace_bytes": (SZ, [I, I, I, I]),
+    "pt2q_stage_timing": (I, [I]),
+    "pt2q_stage_timing_read": (I, [P, I, P]),
+    "pt2q_quantize_blocks_group_supported": (I, [I, I, I, I]),
     "pt2q_ssr_workspace_bytes": (SZ, [I, I]),
     "pt2q_gram_workspace_bytes": (SZ, [I]),
     "pt2q_gram": (I, [P, I, I64, I, I64, P, I64, I, P, SZ, P]),
@@ -149,6 +155,22 @@ def compute_device(*tensors):
         raise Pt2qError("pt2q kernels need an MI355X (HIP device); none is visible and there is "
                         "no CPU path")
     return torch.device("cuda", torch.cuda.current_device())
+
+
+def stage_timing(enable: bool):
+    """Enable (clearing the log) or disable the library's per-stage HIP-event brackets."""
+    check(_h.pt2q_stage_timing(1 if enable else 0), "pt2q_stage_timing")
+
+
+def stage_timing_read():
+    """{class: ms} summed over the bracketed intervals since stage_timing(True) (waits for the
+    recorded events), plus "records": the number of intervals."""
+    arr = (ctypes.c_double * len(TIMERS))()
+    cnt = ctypes.c_int(0)
+    check(_h.pt2q_stage_timing_read(ctypes.cast(arr, P), len(TIMERS), ctypes.cast(ctypes.pointer(cnt), P)), "pt2q_stage_timing_read")
+    out = {k: arr[i] for i, k in enumerate(TIMERS)}
+    out["records"] = cnt.value
+    return out
 
 
 def ptr_array(tensors):

@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 #include <climits>
 
 #include "common.hpp"
@@ -80,6 +81,49 @@ struct Carve {
 };
 
 inline long round_up(long a, long b) { return (a + b - 1) / b * b; }
+
+// ---- stage timing (measurement only, pt2q_stage_timing): while enabled, the launches of each
+// block-loop stage are bracketed by a pair of HIP events on their stream.  One host thread, no
+// graph capture; read back after the stream has drained.
+struct StageRec {
+  int stage;
+  hipEvent_t a, b;
+};
+struct StageLog {
+  bool on = false;
+  std::vector<StageRec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t next = 0;
+  hipEvent_t take() {
+    if (next == pool.size()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[next++];
+  }
+};
+StageLog& stage_log() {
+  static StageLog l;
+  return l;
+}
+struct StageScope {
+  int stage;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  StageScope(int s, hipStream_t stream) : stage(s), st(stream) {
+    StageLog& l = stage_log();
+    if (l.on && (a = l.take()) && hipEventRecord(a, st) != hipSuccess) a = nullptr;
+  }
+  void close() {
+    if (!a) return;
+    StageLog& l = stage_log();
+    hipEvent_t b = l.take();
+    if (b && hipEventRecord(b, st) == hipSuccess) l.recs.push_back({stage, a, b});
+    a = nullptr;
+  }
+  ~StageScope() { close(); }
+};
 
 struct BlockWs {
   int* status;  // the call's status word (stall reports)
@@ -193,15 +237,18 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   const bool ssr = (flags & PT2Q_FLAG_SSR) != 0;
   const int aga = flags & PT2Q_AGA_MASK;
   int* iters = iters_dev ? iters_dev : w.iters;
-  // W (n x m) -> Wt (m x ldw, fp32)
-  if ((rc = pt2q_launch_transpose_to_f32(W, wdtype, ldw_in, n, m, w.Wt, w.ldw, st)) != PT2Q_OK)
-    return rc;
-  if (hipMemsetAsync(w.counters, 0, sizeof(int) * (4 * B + pt2q_ssr_counter_ints(n)), st) != hipSuccess)
-    return PT2Q_E_HIP;
-  if (hipMemsetAsync(iters, 0, sizeof(int) * B, st) != hipSuccess) return PT2Q_E_HIP;
-  // rem0 = [0, m)
-  if ((rc = pt2q_launch_select_seq(0, 0, 0, m, nullptr, w.blk, w.rem[0], nullptr, st)) != PT2Q_OK)
-    return rc;
+  {
+    StageScope ts(PT2Q_TIMER_SETUP, st);
+    // W (n x m) -> Wt (m x ldw, fp32)
+    if ((rc = pt2q_launch_transpose_to_f32(W, wdtype, ldw_in, n, m, w.Wt, w.ldw, st)) != PT2Q_OK)
+      return rc;
+    if (hipMemsetAsync(w.counters, 0, sizeof(int) * (4 * B + pt2q_ssr_counter_ints(n)), st) != hipSuccess)
+      return PT2Q_E_HIP;
+    if (hipMemsetAsync(iters, 0, sizeof(int) * B, st) != hipSuccess) return PT2Q_E_HIP;
+    // rem0 = [0, m)
+    if ((rc = pt2q_launch_select_seq(0, 0, 0, m, nullptr, w.blk, w.rem[0], nullptr, st)) != PT2Q_OK)
+      return rc;
+  }
   float* part = w.ssr;
   float* wn = part + (size_t)ceil_div(m, 128) * n;
   float* sim = wn + n;
@@ -216,6 +263,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     // the critical path of the rows, which need it only for their AGA)
     const bool s1_in_atq = aga == PT2Q_AGA_ACT && bs <= 128 && pt2q_tuning().s1_in_atq;
     const bool s1_in_topk = !s1_in_atq && ssr && r > b && aga == PT2Q_AGA_ACT && bs <= 128;
+    StageScope ts_ssr(PT2Q_TIMER_SSR, st);
     if (ssr) {
       if (r > b) {
         if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B,
@@ -233,6 +281,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
       if ((rc = pt2q_launch_select_seq(0, processed, bs, m, nullptr, w.blk, nrem, perm + processed, st)) != PT2Q_OK)
         return rc;
     }
+    ts_ssr.close();
+    StageScope ts_atq(PT2Q_TIMER_ATQ, st);
     const float* S1 = nullptr;
     if (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_HESS) {
       if (hess_wide(flags, bs)) {
@@ -250,6 +300,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
                                     s1_in_atq ? A : nullptr, lda,
                                     s1_in_atq ? w.counters + 2 * B + 2 * k : nullptr, w.status)) != PT2Q_OK)
       return rc;  // (also forms the EF coefficients C[k][e] when nr > 0)
+    ts_atq.close();
+    StageScope ts_ef(PT2Q_TIMER_EF, st);
     const bool want = ssr && nr > b && ef_wbar_ok(n, w.ldw, w.Wt);  // the next block runs SSR over nrem
     rc = (nr > 0 && pt2q_tuning().ef_kernel)
              ? pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, nullptr, want ? part : nullptr, n)
@@ -271,6 +323,7 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     cur ^= 1;
   }
   // outputs: T (n x m) from Tt (m x ldw); alpha/mu (n x B) from (B x n)
+  StageScope ts(PT2Q_TIMER_OUT, st);
   if ((rc = pt2q_launch_transpose_i8(w.Tt, w.ldw, m, n, T, tdtype, m, st)) != PT2Q_OK) return rc;
   if ((rc = pt2q_launch_transpose_f32(w.alpha_t, n, B, n, alpha, B, st)) != PT2Q_OK) return rc;
   if ((rc = pt2q_launch_transpose_f32(w.mu_t, n, B, n, mu, B, st)) != PT2Q_OK) return rc;
@@ -308,6 +361,7 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
   Grp g{};
   g.ws = zs;
   g.count = count;
+  StageScope ts0(PT2Q_TIMER_SETUP, st);
   for (int z = 0; z < count; ++z) {
     g.G[z] = act ? A[z] : nullptr;
     g.Hinv[z] = Hinv[z];
@@ -320,6 +374,7 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
   hipLaunchKernelGGL(group_init_kernel, dim3(ceil_div(std::max(std::max(ncnt, B), m), 256), 1, count), dim3(256),
                      0, st, w.counters, ncnt, w.iters, B, w.rem[0], m, zs);
   PT2Q_LAUNCH_CHECK();
+  ts0.close();
   float* part = w.ssr;
   float* wn = part + (size_t)ceil_div(m, 128) * n;
   float* sim = wn + n;
@@ -330,6 +385,7 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
     const int nr = r - bs;
     int* rem = w.rem[cur];
     int* nrem = w.rem[cur ^ 1];
+    StageScope ts_ssr(PT2Q_TIMER_SSR, st);
     if (ssr && r > b) {
       if ((rc = pt2q_launch_ssr_similarity(w.Wt, w.ldw, n, rem, r, part, wn, sim, st, w.counters + 4 * B, &g,
                                            pre)) != PT2Q_OK)
@@ -341,6 +397,8 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
                                             nrem, perm64 + processed, st, &g)) != PT2Q_OK) {
       return rc;
     }
+    ts_ssr.close();
+    StageScope ts_atq(PT2Q_TIMER_ATQ, st);
     // variant M: S1/d of every linear's block formed inside its ATQ launch (table g.G)
     if ((rc = pt2q_launch_atq_block(w.Wt, w.ldw, n, w.blk, bs, act ? w.S1 : nullptr, w.d, max_iter,
                                     w.alpha_t + (size_t)k * n, w.mu_t + (size_t)k * n, w.Tt, w.ldw,
@@ -348,6 +406,8 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
                                     Hinv[0], ldhi, nrem, nr, w.Ck, m, w.iters_part, act ? A[0] : nullptr, lda,
                                     act ? w.counters + 2 * B + 2 * k : nullptr, w.status, &g)) != PT2Q_OK)
       return rc;
+    ts_atq.close();
+    StageScope ts_ef(PT2Q_TIMER_EF, st);
     const bool want = ssr && nr > b && ef_wbar_ok(n, w.ldw, w.Wt);  // the next block runs SSR over nrem
     if (nr > 0 && (rc = pt2q_launch_ef(w.Ck, m, w.Et, w.Wt, w.ldw, m, nrem, nr, bs, st, &g,
                                        want ? part : nullptr, n)) != PT2Q_OK)
@@ -357,6 +417,7 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
     r = nr;
     cur ^= 1;
   }
+  StageScope ts1(PT2Q_TIMER_OUT, st);
   for (int z = 0; z < count; ++z) {  // outputs: T (n x m), alpha / mu (n x B), perm, iters
     auto sl = [&](auto* p) { return (decltype(p))((char*)p + z * zs); };
     if ((rc = pt2q_launch_transpose_i8(sl(w.Tt), w.ldw, m, n, T[z], tdtype, m, st)) != PT2Q_OK) return rc;
@@ -372,6 +433,18 @@ int run_blocks_group(int count, const void* const* W, int wdtype, long ldw_in, i
 }
 
 bool dtype_ok(int dt) { return dt == PT2Q_F32 || dt == PT2Q_F16 || dt == PT2Q_BF16; }
+
+// Every condition under which pt2q_quantize_blocks_group runs (else PT2Q_E_UNSUPPORTED): blocks
+// of <= 128 columns with b < m, variant M or no AGA, the tuning defaults (S1 in the ATQ launch,
+// the EF kernel, the fused w-bar), n <= 16384 with n % 4 == 0, and the error feedback's own
+// limits (pt2q_launch_ef: coefficient rows 16-byte aligned, every Wt under 2 GiB of buffer range).
+bool group_ok(int n, int m, int b, int flags) {
+  const int aga = flags & PT2Q_AGA_MASK;
+  const Pt2qTuning& tu = pt2q_tuning();
+  return n > 0 && m > 0 && b > 0 && b <= 128 && b < m && m < 65536 &&
+         (aga == PT2Q_AGA_ACT || aga == PT2Q_AGA_NONE) && tu.s1_in_atq && tu.ef_kernel && tu.wbar_fused &&
+         n <= 16384 && n % 4 == 0 && m % 4 == 0 && (long)m * round_up(n, 64) * 4 < 0x80000000L;
+}
 
 // The status word every workspace-taking call reserves first (PT2Q_STATUS_BYTES), zeroed on the
 // call's stream before any kernel that may report into it.
@@ -397,6 +470,39 @@ extern "C" const char* pt2q_strerror(int status) {
     case PT2Q_E_STALL: return "a cross-workgroup wait timed out (results invalid)";
   }
   return "unknown status";
+}
+
+extern "C" int pt2q_stage_timing(int enable) {
+  StageLog& l = stage_log();
+  if (enable) {
+    l.recs.clear();
+    l.next = 0;
+  }
+  l.on = enable != 0;
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_stage_timing_read(double* ms, int nstages, int* records) {
+  if (!ms || nstages <= 0) return PT2Q_E_ARG;
+  StageLog& l = stage_log();
+  for (int i = 0; i < nstages; ++i) ms[i] = 0.0;
+  for (const StageRec& r : l.recs) {
+    float t = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&t, r.a, r.b) != hipSuccess)
+      return PT2Q_E_HIP;
+    if (r.stage >= 0 && r.stage < nstages) ms[r.stage] += t;
+  }
+  if (records) *records = (int)l.recs.size();
+  return PT2Q_OK;
+}
+
+extern "C" int pt2q_quantize_blocks_group_supported(int n, int m, int b, int flags) {
+  return group_ok(n, m, b, flags) ? 1 : 0;
+}
+
+extern "C" size_t pt2q_blocks_workspace_bytes(int n, int m, int b, int flags) {
+  if (n <= 0 || m <= 0 || b <= 0) return 0;
+  return PT2Q_STATUS_BYTES + blocks_bytes(n, m, b, flags);
 }
 
 extern "C" size_t pt2q_cholesky_workspace_bytes(int m) {
@@ -441,12 +547,14 @@ extern "C" int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ld
     if (rc != PT2Q_OK) return rc;
     flags = c.take<int>(pt2q_gram_flags_ints(m));
   }
+  StageScope ts(PT2Q_TIMER_GRAM, (hipStream_t)stream);
   return pt2q_launch_gram(g, flags, (hipStream_t)stream, status);
 }
 
 extern "C" int pt2q_gram_batched(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
                                  float* G, void* stream) {
   if (batch <= 0 || !X || !G || N < 0 || N > INT_MAX || m <= 0 || ldx < m) return PT2Q_E_ARG;
+  StageScope ts(PT2Q_TIMER_GRAM, (hipStream_t)stream);
   return pt2q_launch_gram16_batched(X, xdtype, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream);
 }
 
@@ -466,6 +574,7 @@ extern "C" int pt2q_cholesky_inverse(const float* H, int64_t ldh, int m, float* 
   float* U = c.take<float>((size_t)m * m);
   float* Ui = c.take<float>((size_t)m * m);
   if (!c.ok) return PT2Q_E_WORKSPACE;
+  StageScope ts(PT2Q_TIMER_INVERSE, (hipStream_t)stream);
   return pt2q_launch_cholesky_inverse(H, ldh, m, Hinv, ldhi, U, Ui, info_dev, (hipStream_t)stream);
 }
 
@@ -490,6 +599,7 @@ extern "C" int pt2q_hessian_inverse_batched(const float* G, int m, int batch, in
   // pass can (m <= SUMN_LDS_MAX); else in full form, then made upper in place by the factor
   const bool upper = m <= SUMN_LDS_MAX;
   int rc;
+  StageScope ts(PT2Q_TIMER_INVERSE, st);
   for (int z = 0; z < batch; ++z)
     if ((rc = pt2q_launch_prepare_hessian(G + z * mm, m, m, nsamples, percdamp, H + z * mm, m, damp + z, st,
                                           upper)) != PT2Q_OK)
@@ -502,9 +612,11 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
                                     int64_t ldhi, int max_iter, float* alpha, float* mu, void* T,
                                     int tdtype, int64_t* perm, int* iters_dev, void* workspace,
                                     size_t workspace_bytes, void* stream) {
-  if (!W || !Hinv || !alpha || !mu || !T || !perm || n <= 0 || m <= 0 || b <= 0 ||
+  // Hinv feeds only the error feedback: a single block (per-channel, b >= m) leaves no columns
+  // behind and never reads it, so it may be NULL there
+  if (!W || (!Hinv && b < m) || !alpha || !mu || !T || !perm || n <= 0 || m <= 0 || b <= 0 ||
       !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0 || ldw < m ||
-      ldhi < m)
+      (Hinv && ldhi < m))
     return PT2Q_E_ARG;
   int aga = flags & PT2Q_AGA_MASK;
   if (aga != PT2Q_AGA_NONE && (!A || lda < m)) return PT2Q_E_ARG;
@@ -540,11 +652,8 @@ extern "C" int pt2q_quantize_blocks_group(int count, const void* const* W, int w
     if (!W[z] || !Hinv[z] || !alpha[z] || !mu[z] || !T[z] || !perm[z] || (aga == PT2Q_AGA_ACT && !A[z]))
       return PT2Q_E_ARG;
   // grouped launches: blocks of at most 128 columns, several blocks (the error feedback runs),
-  // variant M (S1/d in the ATQ launch) or no AGA, the fused w-bar, the EF kernel
-  const Pt2qTuning& tu = pt2q_tuning();
-  if (b > 128 || b >= m || m >= 65536 || (aga != PT2Q_AGA_ACT && aga != PT2Q_AGA_NONE) || !tu.s1_in_atq ||
-      !tu.ef_kernel || !tu.wbar_fused || n > 16384 || n % 4)
-    return PT2Q_E_UNSUPPORTED;
+  // variant M (S1/d in the ATQ launch) or no AGA, the fused w-bar, the EF kernel (group_ok)
+  if (!group_ok(n, m, b, flags)) return PT2Q_E_UNSUPPORTED;
   Carve c{(char*)workspace, workspace_bytes};
   BlockWs w;
   int rc;
@@ -593,8 +702,10 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
     g.C = G; g.ldc = m;
     g.mode = GEMM_STORE;
     g.upper = 1; g.mirror = 1;
+    StageScope ts(PT2Q_TIMER_GRAM, st);
     if ((rc = pt2q_launch_gram(g, gflags, st, status)) != PT2Q_OK) return rc;
   }
+  StageScope ts_inv(PT2Q_TIMER_INVERSE, st);
   // H is consumed in place as the Cholesky work matrix (variant M's AGA uses the raw Gram G), so
   // it is written in that form at once (strictly lower part zero; no separate copy pass).
   // Hinv only feeds the error feedback; a single block (per-channel, b >= m) has none, so the
@@ -607,6 +718,7 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
   } else if (hipMemsetAsync(info_dev, 0, sizeof(int), st) != hipSuccess) {
     return PT2Q_E_HIP;
   }
+  ts_inv.close();
   int f = (flags & ~PT2Q_AGA_MASK) | PT2Q_AGA_ACT;
   return run_blocks(W, wdtype, ldw, n, m, b, f, G, m, Hinv, m, max_iter, alpha, mu, T, tdtype,
                     perm, iters_dev, w, st);

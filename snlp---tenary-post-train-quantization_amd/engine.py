@@ -137,10 +137,24 @@ def cholesky_inverse(H: torch.Tensor):
     return Hinv, True
 
 
-def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: torch.Tensor,
+def needs_inverse(m: int, block_size: int) -> bool:
+    """Whether the block loop reads H⁻¹: only the error feedback does (main.py:198-214), and a
+    single block (per-channel, block_size >= m) leaves no columns to feed back into."""
+    return block_size < m
+
+
+def blocks_workspace_bytes(n: int, m: int, block_size: int, flags: int) -> int:
+    return int(_lib.lib().pt2q_blocks_workspace_bytes(n, m, int(block_size), flags))
+
+
+def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[torch.Tensor],
                     block_size: int = 128, use_ssr: bool = True, aga: int = _lib.AGA_ACT,
-                    max_iter: int = 100, t_dtype=torch.int8) -> LayerOutput:
-    """The block loop given the AGA matrix A (raw Gram for variant M, damped H for variant G)."""
+                    max_iter: int = 100, t_dtype=torch.int8, workspace: Optional[torch.Tensor] = None,
+                    check: bool = True) -> LayerOutput:
+    """The block loop given the AGA matrix A (raw Gram for variant M, damped H for variant G).
+    Hinv may be None for a single block (block_size >= m: it is never read).  workspace: reused
+    when large enough (pt2q_blocks_workspace_bytes); check=False leaves the status word to the
+    caller (`_lib.check_status(workspace)`; no host read here)."""
     W = _float_input(W)
     n, m = W.shape
     dev = W.device
@@ -151,15 +165,21 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: torch.Tens
     perm = torch.empty(m, dtype=torch.int64, device=dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     flags = (_lib.FLAG_SSR if use_ssr else 0) | aga
-    ws = _lib.workspace(_lib.lib().pt2q_layer_workspace_bytes(n, m, block_size, flags), dev)
-    Hinv = Hinv.contiguous().float()
+    nbytes = blocks_workspace_bytes(n, m, block_size, flags)
+    ws = workspace if workspace is not None and workspace.numel() >= nbytes else _lib.workspace(nbytes, dev)
+    if Hinv is None:
+        if needs_inverse(m, block_size):
+            raise ValueError("quantize_blocks: Hinv is required when block_size < m (error feedback)")
+    else:
+        Hinv = Hinv.contiguous().float()
     rc = _lib.lib().pt2q_quantize_blocks(
         _lib.ptr(W), _lib.dtype_code(W), m, n, m, int(block_size), flags,
         _lib.ptr(A), m, _lib.ptr(Hinv), m, int(max_iter), _lib.ptr(alpha), _lib.ptr(mu), _lib.ptr(T),
         _lib.dtype_code(T), _lib.ptr(perm), _lib.ptr(iters), _lib.ptr(ws), ws.numel(),
         _lib.stream_of(dev))
     _lib.check(rc, "pt2q_quantize_blocks")
-    _lib.check_status(ws, "pt2q_quantize_blocks")
+    if check:
+        _lib.check_status(ws, "pt2q_quantize_blocks")
     return LayerOutput(alpha, mu, T, perm, iters)
 
 
@@ -167,9 +187,10 @@ GROUP_MAX = 16  # linears per pt2q_quantize_blocks_group call (PT2Q_GROUP_MAX)
 
 
 def group_supported(n: int, m: int, block_size: int, flags: int = _lib.FLAG_SSR | _lib.AGA_ACT) -> bool:
-    """Whether pt2q_quantize_blocks_group takes linears of this shape (else per-linear loops)."""
-    return (block_size <= 128 and block_size < m and m < 65536 and n <= 16384 and n % 4 == 0
-            and (flags & _lib.AGA_MASK) in (_lib.AGA_ACT, _lib.AGA_NONE))
+    """Whether pt2q_quantize_blocks_group takes linears of this shape (else per-linear loops):
+    the library's own answer (pt2q_quantize_blocks_group_supported), so shape limits, tuning
+    overrides and the error feedback's buffer limits are never restated here."""
+    return bool(_lib.lib().pt2q_quantize_blocks_group_supported(int(n), int(m), int(block_size), int(flags)))
 
 
 def quantize_blocks_group(Ws, As, Hinvs, block_size: int = 128, use_ssr: bool = True,
@@ -261,8 +282,14 @@ def quantize_shared(Ws, G: torch.Tensor, nsamples: int, block_size: int = 128,
                     t_dtype=torch.int8):
     """Variant M for several linears that read the same activations (q/k/v, gate/up): one Gram
     G = XᵀX and one Cholesky inverse, then the block loop per weight.  Each result is
-    bit-identical to quantize_layer(W, X) on that linear alone (same kernels, same inputs)."""
-    Hinv, spd = hessian_inverse(G, nsamples, percdamp)
+    bit-identical to quantize_layer(W, X) on that linear alone (same kernels, same inputs).
+    Per-channel (block_size >= m): no inverse -- nothing reads it (pt2q_quantize_layer skips it
+    the same way)."""
+    m = G.shape[-1]
+    if needs_inverse(m, block_size):
+        Hinv, spd = hessian_inverse(G, nsamples, percdamp)
+    else:
+        Hinv, spd = None, True
     outs = []
     for W in Ws:
         out = quantize_blocks(W, G, Hinv, block_size, use_ssr, _lib.AGA_ACT, max_iter, t_dtype)
@@ -289,8 +316,8 @@ class UnitWorkspace:
 
     def blocks(self, n: int) -> torch.Tensor:
         if n not in self._blocks:
-            self._blocks[n] = _lib.workspace(
-                _lib.lib().pt2q_layer_workspace_bytes(n, self.m, self.block_size, self.flags), self.device)
+            self._blocks[n] = _lib.workspace(blocks_workspace_bytes(n, self.m, self.block_size, self.flags),
+                                             self.device)
         return self._blocks[n]
 
 
@@ -363,7 +390,9 @@ def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percda
     m, dev = Ws[0].shape[1], Ws[0].device
     L = _lib.lib()
     st = _lib.stream_of(dev)
-    if Hinv is None:
+    if Hinv is None and not needs_inverse(m, block_size):  # per-channel: H⁻¹ is never read
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+    elif Hinv is None:
         _lib.check(L.pt2q_prepare_hessian(_lib.ptr(Gm), m, m, int(nsamples), float(percdamp),
                                           _lib.ptr(ws.H), m, _lib.ptr(ws.damp), st), "pt2q_prepare_hessian")
         info = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -391,7 +420,7 @@ def _unit_tail(Ws, Gm, nsamples, ws, statuses, X, G, block_size, use_ssr, percda
         statuses.append(_lib.status_view(bws).clone())
         outs.append(out)
 
-    def redo():  # main.py:140-141: pinv of the damped Hessian, then the block loops again
+    def redo():  # main.py:140-141: pinv of the damped Hessian, then the block loops again (B > 1)
         Gr = gram(X) if X is not None else G.contiguous().float()
         Hinv = torch.linalg.pinv(prepare_hessian(Gr, nsamples, percdamp)[0])
         return [quantize_blocks(W, Gr, Hinv, block_size, use_ssr, _lib.AGA_ACT, max_iter, t_dtype)

@@ -356,16 +356,23 @@ class GramsFirst:
 
     Stall reporting: the Grams of one width share a workspace, and every pt2q_gram call zeroes
     its status word first, so after each Gram its word is OR-ed (on the stream) into one
-    per-step device word; check() reads that word once and clears it."""
+    per-step device word; check() reads that word once and clears it.
 
-    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, percdamp: float = 0.01,
-                 group: int = 16, overlap: bool = False, batch_grams: bool = True):
+    Per-channel groups (block size >= m: one block per linear) get no inverse at all -- H⁻¹
+    feeds only the error feedback (main.py:198-214), which a single block never reaches -- so
+    neither the Hinv buffer nor the batched factorisation exists for them (as pt2q_quantize_layer).
+
+    The damping is the pipeline's (pipe.percdamp) everywhere: batched inverses, the per-lane
+    inverses of batched=False and the pinv fallback, so no path damps differently."""
+
+    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, group: int = 16,
+                 overlap: bool = False, batch_grams: bool = True):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         # step 1 batched: the Grams of each (m, N) group in data-parallel launches
         # (pt2q_gram_batched) instead of one stream-K launch per unit
         self.batch_grams, self.pending = batch_grams, {}
-        self.batched, self.chunk, self.percdamp = batched, chunk, percdamp
+        self.batched, self.chunk = batched, chunk
         # step 3 grouped: the block loops of up to `group` same-shape linears (across units) per
         # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
         self.group = group if batched else 0
@@ -382,7 +389,15 @@ class GramsFirst:
         self.slot = {}       # key -> (group, index)
         self.groups = {}     # (m, N) -> {"G", "Hinv", "info"} packed over the group's units
         self.scratch = {}
+        self.ows = {}        # per-lane workspaces of the per-linear ("one") block loops
         self.stall = torch.zeros(1, dtype=torch.int32, device=self.dev)
+
+    @property
+    def percdamp(self):
+        return self.pipe.percdamp
+
+    def needs_inverse(self, m: int) -> bool:
+        return self.engine.needs_inverse(m, self.pipe.bs)
 
     def begin(self, units):
         """Slots for this step's units [(key, m, N)]: one packed buffer per (m, N) group,
@@ -395,11 +410,12 @@ class GramsFirst:
             count[g] = count.get(g, 0) + 1
         for g, c in count.items():
             have = self.groups.get(g)
-            if have is None or have["G"].shape[0] != c:
-                m = g[0]
+            m = g[0]
+            inv = self.batched and self.needs_inverse(m)
+            if have is None or have["G"].shape[0] != c or (have["Hinv"] is not None) != inv:
                 self.groups[g] = {"G": torch.empty((c, m, m), dtype=torch.float32, device=self.dev),
                                   "Hinv": torch.empty((c, m, m), dtype=torch.float32, device=self.dev)
-                                  if self.batched else None,
+                                  if inv else None,
                                   "info": torch.zeros(c, dtype=torch.int32, device=self.dev)}
         for g in [g for g in self.groups if g not in count]:
             del self.groups[g]
@@ -445,20 +461,22 @@ class GramsFirst:
 
     def inverses(self):
         """Step 2: every group's Hessian inverses, batched (no-op with batched=False), narrowest
-        width first, on the inverse stream; each group records its event."""
+        width first, on the inverse stream; each group records its event.  Per-channel groups
+        (no Hinv buffer, see needs_inverse) are skipped: their info words stay 0."""
         if not self.batched:
             return
         caller = torch.cuda.current_stream(self.dev)
         self.inv_done = {}
+        live = [g for g in sorted(self.groups) if self.groups[g]["Hinv"] is not None]
         if self.inv_stream is None:  # no overlap: on the caller's stream, before any tail
-            for g in sorted(self.groups):
+            for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
                                                     info=grp["info"], scratch=self.scratch, chunk=self.chunk)
             return
         self.inv_stream.wait_stream(caller)  # the Grams
         with torch.cuda.stream(self.inv_stream):
-            for g in sorted(self.groups):
+            for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
                                                     info=grp["info"], scratch=self.scratch, chunk=self.chunk)
@@ -477,7 +495,7 @@ class GramsFirst:
         if key in self.slot:
             g, z = self.slot[key]
             grp = self.groups[g]
-            if self.batched:
+            if self.batched and grp["Hinv"] is not None:
                 self._wait_inverse(torch.cuda.current_stream(self.dev), key)
                 return self.pipe.run(Ws, G=grp["G"][z], nsamples=nsamples, Hinv=grp["Hinv"][z],
                                      info=grp["info"][z:z + 1])
@@ -501,12 +519,14 @@ class GramsFirst:
             Ws = [eng._float_input(W) for W in Ws]
             run = _GroupedRun(state, key, Ws, grp["G"][z], N, grp["info"][z:z + 1])
             runs.append(run)
+            state.runs.append(run)
+            Hz = grp["Hinv"][z] if grp["Hinv"] is not None else None  # None: per-channel, never read
             for k, W in enumerate(Ws):
                 n, m = W.shape
                 if eng.group_supported(n, m, bs, flags):
-                    classes.setdefault((n, m, W.dtype), []).append((run, k, W, grp["G"][z], grp["Hinv"][z]))
+                    classes.setdefault((n, m, W.dtype), []).append((run, k, W, grp["G"][z], Hz))
                 else:  # a lone linear of an unsupported shape: its own loop on the next lane
-                    classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], grp["Hinv"][z]))
+                    classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], Hz))
         caller = torch.cuda.current_stream(self.dev)
         lanes = self.pipe.lanes
         # groups: at most `group` linears, and small enough that every lane gets work; issued
@@ -528,10 +548,16 @@ class GramsFirst:
             for key in {c[0].key for c in chunk}:
                 self._wait_inverse(ln.stream, key)
             with torch.cuda.stream(ln.stream):
-                if ckey[0] == "one":
+                if ckey[0] == "one":  # stream-ordered like a group: lane workspace, status read in finish()
                     run, k, W, G, H = chunk[0]
-                    out = eng.quantize_blocks(W, G, H, bs, ssr, lib.AGA_ACT, mi)  # checks its status
-                    run.outs[k] = out
+                    n, m = W.shape
+                    nbytes = eng.blocks_workspace_bytes(n, m, bs, flags)
+                    okey = (id(ln), W.device)
+                    if okey not in self.ows or self.ows[okey].numel() < nbytes:
+                        self.ows[okey] = lib.workspace(nbytes, self.dev)
+                    ws = self.ows[okey]
+                    run.outs[k] = eng.quantize_blocks(W, G, H, bs, ssr, lib.AGA_ACT, mi, workspace=ws, check=False)
+                    state.statuses.append(lib.status_view(ws).clone())
                     continue
                 n, m, _ = ckey
                 wkey = (id(ln), n, m)
@@ -558,37 +584,48 @@ class GramsFirst:
 
 
 class _GroupState:
-    """The device words of one grouped tail phase, read once by the first finish()."""
+    """The device words of one grouped tail phase -- every block-loop stall word and every
+    unit's Cholesky info word -- read in ONE host read by the first finish()."""
 
     def __init__(self, gf):
-        self.gf, self.statuses, self.join, self.read = gf, [], None, None
+        self.gf, self.statuses, self.runs, self.join, self.read = gf, [], [], None, None
+
+    def read_once(self):
+        if self.read is not None:
+            return
+        if self.join is not None:
+            self.join()
+        words = torch.cat([s.reshape(1) for s in self.statuses] +
+                          [r.info.reshape(1) for r in self.runs]).cpu().tolist()
+        ns = len(self.statuses)
+        for v in words[:ns]:
+            self.gf.lib.raise_stall(int(v), "pt2q_quantize_blocks_group")
+        for r, v in zip(self.runs, words[ns:]):
+            r.info_val = int(v)
+        self.read = True
 
 
 class _GroupedRun:
     """One unit's outputs from GramsFirst.tails: finish() joins the lanes, reads every group's
-    stall word and every unit's Cholesky status once (the first call), and re-runs this unit
-    with pinv (main.py:140-141) if its Hessian was not positive definite."""
+    stall word and every unit's Cholesky status once (the first call, _GroupState.read_once),
+    and re-runs this unit with pinv (main.py:140-141) if its Hessian was not positive definite
+    (never for per-channel units: they have no inverse, and nothing would read one)."""
 
     def __init__(self, state, key, Ws, G, nsamples, info):
         self.state, self.key, self.Ws, self.G, self.N, self.info = state, key, Ws, G, nsamples, info
         self.outs = [None] * len(Ws)
         self.spd = None
+        self.info_val = None
 
     def finish(self):
         if self.spd is not None:
             return self.outs
-        st = self.state
-        if st.read is None:
-            if st.join is not None:
-                st.join()
-            words = torch.cat([s.reshape(1) for s in st.statuses]).cpu().tolist() if st.statuses else []
-            for v in words:
-                st.gf.lib.raise_stall(int(v), "pt2q_quantize_blocks_group")
-            st.read = True
-        self.spd = int(self.info.item()) == 0
+        self.state.read_once()
+        self.spd = self.info_val == 0
         if not self.spd:
-            eng, pipe = self.state.gf.engine, self.state.gf.pipe
-            H, _ = eng.prepare_hessian(self.G, self.N, pipe.percdamp)
+            gf = self.state.gf
+            eng, pipe = gf.engine, gf.pipe
+            H, _ = eng.prepare_hessian(self.G, self.N, gf.percdamp)
             Hinv = torch.linalg.pinv(H)
             self.outs = [eng.quantize_blocks(W, self.G, Hinv, pipe.bs, pipe.use_ssr, eng._lib.AGA_ACT,
                                              pipe.max_iter) for W in self.Ws]

@@ -197,6 +197,20 @@ def gen_hessian():
              damp=np.float32(damp.item()))
 
 
+def gen_hessian512():
+    """m = 512 beside the m = 256 pair: the element-wise H^-1 pin (test_hessian_inverse_elementwise)."""
+    print("Hessian / inverse, m = 512 (main.py:127-141)")
+    m, N = 512, 1024
+    X = torch.from_numpy(synth.activations(300 + N + m, N, m))
+    H = X.T @ X
+    H = H / X.shape[0]
+    damp = 0.01 * torch.diag(H).mean()
+    H.diagonal().add_(damp)
+    Hinv = torch.cholesky_inverse(torch.linalg.cholesky(H.float()))
+    save(f"hess_{m}_n{N}", xseed=300 + N + m, N=N, m=m, Hinv=Hinv.numpy(),
+         damp=np.float32(damp.item()))
+
+
 def gen_trace():
     """Teacher-forced per-block trace of main.py:158-215 using the reference's own components."""
     print("per-block trace (variant M, SSR on)")
@@ -594,7 +608,7 @@ def gen_ppl():
          nlin=len(params), **kw)
 
 
-GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian,
+GENERATORS = {"layers": gen_layers, "atq": gen_atq, "ssr": gen_ssr, "hessian": gen_hessian, "hessian512": gen_hessian512,
               "trace": gen_trace, "examples": gen_examples, "wide": gen_wide,
               "ternary": gen_ternary, "fp16": gen_fp16, "loop16": gen_loop16,
               "model": gen_model, "model_tf": gen_model_tf, "ppl": gen_ppl}

@@ -155,3 +155,77 @@ def test_grams_first_schedule_equals_sequential(pt2q, batched, chunk, group):
             o = res[f"{name}.{p}"]
             for k, b in (("alpha", r.alpha), ("mu", r.mu), ("T", r.T), ("perm", r.perm)):
                 assert bits_equal(host(o[k]), host(b)), (name, p, k)
+
+
+def _units_and_data(pt2q, specs, seed):
+    units, data = [], {}
+    for i, (m, ns, N, dt) in enumerate(specs):
+        X = cuda(synth.activations(seed + i, N, m)).to(dt)
+        Ws = {f"p{k}": cuda(synth.weights(seed + 100 + 10 * i + k, n, m)).to(dt) for k, n in enumerate(ns)}
+        units.append((f"u{i}", [(f"p{k}", n, m) for k, n in enumerate(ns)], N))
+        data[f"u{i}"] = (X, Ws)
+    return units, data
+
+
+@pytest.mark.parametrize("bs,batched", [(1024, True), (1 << 14, True), (1 << 14, False)])
+def test_grams_first_per_channel_equals_quantize_layer(pt2q, bs, batched):
+    """the per-channel (block >= m, C5) grams-first step runs no Hessian inverse
+    -- H^-1 feeds only the error feedback (main.py:198-214), which one block never reaches -- and
+    its results equal pt2q_quantize_layer (which skips the inverse the same way) bit for bit:
+    bf16 640 x 1024 linears, a shared-input unit of two, batched Grams, the per-linear block
+    loops issued on the lanes with their status read once at finish."""
+    import importlib
+    sharding = importlib.import_module("pt2q.sharding")
+    specs = [(1024, (640, 512), 4096, torch.bfloat16), (1024, (640,), 4096, torch.bfloat16)]
+    units, data = _units_and_data(pt2q, specs, 1200)
+    pipe = pt2q.UnitPipeline("cuda", bs, True, lanes=3)
+    gf = sharding.GramsFirst(pipe, "cuda", batched=batched)
+    res, _ = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False, grams_first=gf)
+    assert gf.groups and all(grp["Hinv"] is None for grp in gf.groups.values())  # no inverse buffer
+    assert not gf.inv_done and not gf.scratch  # ... and no batched factorisation ran
+    for name, lins, _ in units:
+        X, Ws = data[name]
+        for p, _, _ in lins:
+            r = pt2q.quantize_layer(Ws[p], X, bs, True)
+            o = res[f"{name}.{p}"]
+            for k, b in (("alpha", r.alpha), ("mu", r.mu), ("T", r.T), ("perm", r.perm)):
+                assert bits_equal(host(o[k]), host(b)), (name, p, k)
+    Ws = [data["u0"][1]["p0"], data["u0"][1]["p1"]]
+    shared = pt2q.quantize_shared(Ws, pt2q.gram(data["u0"][0]), 4096, bs, True)
+    for W, o in zip(Ws, shared):
+        r = pt2q.quantize_layer(W, data["u0"][0], bs, True)
+        assert o.spd and bits_equal(host(o.T), host(r.T)) and bits_equal(host(o.alpha), host(r.alpha))
+
+
+@pytest.mark.parametrize("group", [1, 16])
+def test_grams_first_pinv_fallback(pt2q, group):
+    """a unit whose Hessian is not positive definite (its Gram negated after the Gram
+    phase) takes the reference's pinv fallback (main.py:140-141) through GramsFirst.tails /
+    _GroupedRun.finish (group > 1) or the lanes (group 1), with the SAME damping as every other
+    path, and equals quantize_unit on that Gram; the SPD units beside it are untouched."""
+    import importlib
+    sharding = importlib.import_module("pt2q.sharding")
+    specs = [(512, (384, 256), 1024, torch.float16), (512, (256,), 1024, torch.float16)]
+    units, data = _units_and_data(pt2q, specs, 1300)
+    pipe = pt2q.UnitPipeline("cuda", 128, True, percdamp=0.02, lanes=2)
+    gf = sharding.GramsFirst(pipe, "cuda", batched=True, group=group)
+    assert gf.percdamp == 0.02
+    gf.begin([(i, u[1][0][2], u[2]) for i, u in enumerate(units)])
+    for i, u in enumerate(units):
+        gf.gram(i, data[u[0]][0])
+    gf.flush()
+    g, z = gf.slot[0]
+    gf.groups[g]["G"][z].neg_()
+    Gneg = gf.groups[g]["G"][z].clone()
+    gf.inverses()
+    jobs = [(i, [data[u[0]][1][p] for p, _, _ in u[1]], u[2]) for i, u in enumerate(units)]
+    runs = gf.tails(jobs) if gf.grouped else [gf.tail(i, Ws, N) for i, Ws, N in jobs]
+    outs = [r.finish() for r in runs]
+    gf.check()
+    assert [o.spd for o in outs[0]] == [False, False] and outs[1][0].spd
+    want0 = pt2q.quantize_unit(jobs[0][1], G=Gneg, nsamples=1024, percdamp=0.02)
+    want1 = pt2q.quantize_unit(jobs[1][1], X=data["u1"][0], percdamp=0.02)
+    for got, want in ((outs[0], want0), (outs[1], want1)):
+        for o, r in zip(got, want):
+            for a, b in ((o.alpha, r.alpha), (o.mu, r.mu), (o.T, r.T), (o.perm, r.perm)):
+                assert bits_equal(host(a), host(b))

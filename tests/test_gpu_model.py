@@ -95,10 +95,12 @@ def test_model_layer1_teacher_forced_vs_reference(pt2q):
     engine reproduces the reference's loop (engine H^-1, the library-defined sums and tie order
     fixed to the contract's, see gen_golden.canonical_matvecs) bit for bit -- permutation,
     codes, alpha, mu -- on all seven linears.  Against the reference's unmodified quantize_layer
-    on the same inputs, block 0 of every linear whose AGA rows are well conditioned matches
-    exactly; the rest differ only through MKL's summation order, which this fixture records."""
+    on the same inputs (the fixture's ref_*), block-0 permutation and codes are exact, >= 97.9 %
+    of all codes agree and block-0 scales meet the 1e-5 contract on the well-conditioned rows
+    (test_oracle_golden.check_vs_unmodified_reference: the rest differ only through MKL's
+    summation order, which this fixture records)."""
     from conftest import unpack2
-    from test_oracle_golden import layer1_inputs_tf
+    from test_oracle_golden import check_vs_unmodified_reference, layer1_inputs_tf
     g, names, data = layer1_inputs_tf()
     for i, (name, (W, X)) in enumerate(zip(names, data)):
         out = pt2q.quantize_layer(torch.from_numpy(W).cuda(), torch.from_numpy(X).cuda())
@@ -107,3 +109,5 @@ def test_model_layer1_teacher_forced_vs_reference(pt2q):
         np.testing.assert_array_equal(out.T.cpu().numpy(), unpack2(g[f"T2_{i}"], m), err_msg=name)
         assert np.array_equal(out.alpha.cpu().numpy(), g[f"alpha{i}"]), name
         assert np.array_equal(out.mu.cpu().numpy(), g[f"mu{i}"]), name
+        check_vs_unmodified_reference(g, i, name, out.perm.cpu().numpy(), out.T.cpu().numpy(),
+                                      out.alpha.cpu().numpy(), out.mu.cpu().numpy())

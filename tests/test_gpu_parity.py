@@ -559,12 +559,15 @@ def test_reference_call_shapes_with_cpu_tensors(pt2q):
 
 @pytest.mark.parametrize("n,m,count,ssr,dt", [(256, 512, 3, True, torch.float32), (384, 700, 5, True, torch.float16),
                                              (512, 384, 2, False, torch.float32), (1024, 1024, 16, True, torch.float16),
-                                             (4096, 4096, 3, True, torch.float16)])
+                                             (4096, 4096, 3, True, torch.float16),
+                                             (11008, 4096, 3, True, torch.float16),
+                                             (4096, 11008, 2, True, torch.float16)])
 def test_blocks_group_equals_per_linear(pt2q, n, m, count, ssr, dt):
     """pt2q_quantize_blocks_group (one launch per block step for all linears, grid.z = linear)
     == quantize_blocks on each linear alone, bit for bit: every linear has its own W, raw Gram
-    and H^-1 (and some share them, as q/k/v do); ragged m, fp16 weights, sequential blocks, and a
-    full group of 16."""
+    and H^-1 (and some share them, as q/k/v do); ragged m, fp16 weights, sequential blocks, a
+    full group of 16, and the 7B step's MLP shapes as the bench groups them (gate/up 11008 x
+    4096: n > 4096 takes the split similarity kernel ssr_sim_split_kernel; down 4096 x 11008)."""
     Ws, Gs, Hs = [], [], []
     for z in range(count):
         X = pt2q.fill_synthetic((2 * m + 64 * z, m), 300 + 7 * z, outliers=True, device="cuda").half()
@@ -596,3 +599,44 @@ def test_gram_batched_equals_per_item(pt2q, m, N, batch, dt):
     pt2q.engine.gram_batched(Xs, G)
     for z in (0, batch // 2, batch - 1):
         assert bits_equal(host(G[z]), host(pt2q.gram(Xs[z]))), z
+
+
+def test_stage_timing_brackets_the_block_loop(pt2q):
+    """pt2q_stage_timing (bench.py's live stage rooflines): a grouped block loop on one stream
+    records SSR, ATQ and EF intervals whose sum stays within the wall of the call; disabled, it
+    records nothing.  The results are the untimed call's, bit for bit."""
+    lib = pt2q._lib
+    n, m, count = 1024, 1024, 4
+    Ws, Gs, Hs = [], [], []
+    for z in range(count):
+        X = pt2q.fill_synthetic((4 * m, m), 500 + z, outliers=True, device="cuda").half()
+        G = pt2q.gram(X)
+        Hinv, spd = pt2q.hessian_inverse(G, X.shape[0])
+        assert spd
+        Gs.append(G)
+        Hs.append(Hinv)
+        Ws.append(pt2q.fill_synthetic((n, m), 600 + z, std=0.02, device="cuda").half())
+    want = pt2q.engine.quantize_blocks_group(Ws, Gs, Hs, 128, True)
+    torch.cuda.synchronize()
+    lib.stage_timing(True)
+    try:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        got = pt2q.engine.quantize_blocks_group(Ws, Gs, Hs, 128, True)
+        ev1.record()
+        torch.cuda.synchronize()
+    finally:
+        lib.stage_timing(False)
+    t = lib.stage_timing_read()
+    B = m // 128
+    assert t["records"] == 2 + 3 * B, t  # setup + per block (SSR, ATQ, EF) + outputs
+    assert t["ssr"] > 0 and t["atq"] > 0 and t["ef"] > 0, t
+    wall = ev0.elapsed_time(ev1)
+    assert sum(t[k] for k in lib.TIMERS) <= wall * 1.01 + 0.05, (t, wall)
+    for z in range(count):
+        for a, b in ((got[z].perm, want[z].perm), (got[z].T, want[z].T), (got[z].alpha, want[z].alpha)):
+            assert bits_equal(host(a), host(b)), z
+    lib.stage_timing(True)
+    lib.stage_timing(False)
+    pt2q.engine.quantize_blocks_group(Ws, Gs, Hs, 128, True)
+    assert lib.stage_timing_read()["records"] == 0

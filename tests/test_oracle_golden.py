@@ -211,21 +211,37 @@ def test_ssr_select(name):
     np.testing.assert_array_equal(newrem, g["newrem"])
 
 
-@pytest.mark.parametrize("N", [512, 128])
-def test_hessian_and_inverse(N):
+@pytest.mark.parametrize("name", ["hess_256_n512", "hess_256_n128", "hess_512_n1024"])
+def test_hessian_and_inverse(name):
+    """Damped Hessian and its Cholesky inverse (main.py:127-139) vs the reference's (MKL, fp32).
+    Measured (round 4): error scaled by sqrt(Hinv_ii Hinv_jj) max 1.9e-6 / 1.2e-5 / 3.4e-6 (m =
+    256 N = 512, m = 256 N = 128, m = 512 N = 1024); diagonal relative error the same; element-wise
+    relative error median 1.6e-6 / 8.8e-6 / 2.1e-6, 99th percentile 7e-5 / 4.6e-4 / 1e-4 (the
+    maximum, 0.02-0.36, sits on entries ~1e-5 of the diagonal scale, where both fp32 results are
+    rounding noise); and the oracle is at least as close to the f64 inverse as the reference is
+    (1.4e-6 vs 1.7e-6, 6.7e-6 vs 8.7e-6, 2.0e-6 vs 2.7e-6)."""
     import synth
-    g = load_golden(f"hess_256_n{N}")
-    X = synth.activations(int(g["xseed"]), N, 256)
+    g = load_golden(name)
+    N, m = int(g["N"]), int(g["m"])
+    X = synth.activations(int(g["xseed"]), N, m)
     G = orc.gram(X)
     H, damp = orc.prepare_hessian(G, N, 0.01)
     assert abs(damp - float(g["damp"])) <= 1e-6 * abs(float(g["damp"]))
-    np.testing.assert_allclose(H, g["H"], rtol=0, atol=2e-6 * np.abs(g["H"]).max())
+    if "H" in g:
+        np.testing.assert_allclose(H, g["H"], rtol=0, atol=2e-6 * np.abs(g["H"]).max())
     Hinv, spd = orc.cholesky_inverse(H)
     assert spd
-    # fp32 inverse of cond ~1e3 matrices: relative agreement ~1e-4
-    err = np.abs(Hinv - g["Hinv"]).max() / np.abs(g["Hinv"]).max()
-    assert err < 2e-3, err
     np.testing.assert_array_equal(Hinv, Hinv.T)
+    ref = g["Hinv"]
+    scale = np.sqrt(np.abs(np.outer(np.diag(ref), np.diag(ref))))
+    scaled = np.abs(Hinv - ref) / scale
+    assert scaled.max() <= 2e-5, scaled.max()
+    diag = np.abs(np.diag(Hinv) - np.diag(ref)) / np.diag(ref)
+    assert diag.max() <= 2e-5, diag.max()
+    rel = np.abs(Hinv - ref) / np.maximum(np.abs(ref), 1e-30)
+    assert np.median(rel) <= 2e-5 and np.percentile(rel, 99) <= 1e-3, (np.median(rel), np.percentile(rel, 99))
+    exact = np.linalg.inv(H.astype(np.float64))
+    assert (np.abs(Hinv - exact) / scale).max() <= 1.5 * (np.abs(ref - exact) / scale).max()
 
 
 def test_trace_teacher_forced():
@@ -349,6 +365,32 @@ def layer1_inputs_tf():
     return g, names, out
 
 
+def check_vs_unmodified_reference(g, i, name, perm, T, alpha, mu):
+    """Layer-1 results (oracle or GPU: they are bit-identical) against the reference's UNMODIFIED
+    quantize_layer on the same captured inputs (the fixture's ref_* arrays: MKL H^-1, MKL sgemv
+    sums in the AGA, nth_element tie order).  Measured: block-0 permutation and codes
+    exact on all seven linears; full permutation equal on six (down_proj's later blocks see the
+    H^-1 difference); code agreement 97.90 % (down_proj) to 100 %; block-0 alpha / mu within
+    1e-5 on every row with |alpha_ref| <= 1 except two rows of q_proj, where the AGA's 2x2 solve
+    cancels exactly in the contract's order (alpha = 0) and leaves 2^-5 in MKL's.  Rows with
+    |alpha_ref| > 1 are the degenerate AGA rows the reference itself produces (alpha up to 5e14)."""
+    from conftest import unpack2
+    m = int(g[f"m{i}"])
+    rT, rp = unpack2(g[f"ref_T2_{i}"], m), g[f"ref_perm{i}"]
+    b0 = rp[:128]
+    np.testing.assert_array_equal(perm[:128], b0, err_msg=name)
+    np.testing.assert_array_equal(T[:, b0], rT[:, b0], err_msg=name)
+    agree = float((T == rT).mean())
+    assert agree >= 0.979, (name, agree)
+    a0, r0 = alpha[:, 0], g[f"ref_alpha{i}"][:, 0]
+    mu0, rmu0 = mu[:, 0], g[f"ref_mu{i}"][:, 0]
+    rows = np.abs(r0) <= 1
+    bad = rows & ((np.abs(a0 - r0) > SCALE_TOL) | (np.abs(mu0 - rmu0) > SCALE_TOL))
+    assert bad.sum() <= 2 and bad.sum() <= 0.01 * rows.sum(), (name, np.where(bad)[0])
+    assert np.all(a0[bad] == 0), (name, a0[bad])  # the only misses: exact cancellation in the contract
+    return agree
+
+
 def test_oracle_model_layer1_teacher_forced():
     """Layer 1 of the model loop on the reference's own captured inputs: the
     oracle reproduces the reference's loop -- run with the engine's H^-1 and with the two orders
@@ -364,3 +406,4 @@ def test_oracle_model_layer1_teacher_forced():
         np.testing.assert_array_equal(o["perm"], g[f"perm{i}"], err_msg=name)
         np.testing.assert_array_equal(o["T"], unpack2(g[f"T2_{i}"], m), err_msg=name)
         assert np.array_equal(o["alpha"], g[f"alpha{i}"]) and np.array_equal(o["mu"], g[f"mu{i}"]), name
+        check_vs_unmodified_reference(g, i, name, o["perm"], o["T"], o["alpha"], o["mu"])
