@@ -93,6 +93,9 @@ def parse(argv=None):
     p.add_argument("--inverse-overlap", action="store_true",
                    help="model workload: each width's block loops start once its own batched inverses "
                         "are done, beside the other widths' inverses (default: all inverses first)")
+    p.add_argument("--inv-streams", type=int, default=1,
+                   help="model workload, grams-first: streams the batched inverse chunks spread over "
+                        "(sharding.GramsFirst inv_streams)")
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
@@ -102,6 +105,9 @@ def parse(argv=None):
                         "step's launches)")
     p.add_argument("--no-configs", action="store_true",
                    help="skip extra.configs (one short run of each other BASELINE config)")
+    p.add_argument("--no-h2d", action="store_true",
+                   help="skip extra.h2d (the transfer-inclusive step: inputs from pinned host memory, "
+                        "packed results back to the host)")
     return p.parse_args(argv)
 
 
@@ -140,7 +146,7 @@ def config_runs(a, dev):
         if name == a.model:
             continue
         b = resolve(parse(["--model", name, "--steps", "2", "--warmup", "1", "--group", str(a.group),
-                           "--lanes", str(a.lanes)]))
+                           "--lanes", str(a.lanes), "--inv-streams", str(a.inv_streams)]))
         io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[b.io_dtype]
         try:
             w = ModelStep(b, 0, 1, dev, io)
@@ -393,7 +399,8 @@ class ModelStep:
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.schedule = a.schedule
         self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group,
-                                       overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams)
+                                       overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams,
+                                       inv_streams=a.inv_streams)
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.xi = {}  # unit -> which of its width's activation tensors it reads
@@ -601,6 +608,116 @@ def load_committed_stages():
         with open(kp) as f:
             return json.load(f)
     return None
+
+
+class H2DStep:
+    """extra.h2d: SURVEY §8(d)'s whole window, "from H2D of inputs to results resident on rank 0":
+    the step of `ms` (a grams-first ModelStep) with every input starting in PINNED HOST memory and
+    the results ending there, as the reference's flow hands them over (main.py:225-230 returns
+    `.cpu()` tensors).
+
+    Per step: every linear's fp16 W is uploaded on a copy stream; every unit's activations
+    (the same X_DISTINCT tensors per width as the resident line, each unit's own copy) are
+    uploaded in chunks of `chunk` units into two device staging buffers per width, each chunk's
+    batched Gram starting as soon as its copy lands while the next chunk copies; then the batched
+    inverses and grouped block loops as usual; then every result (2-bit codes, alpha, mu, perm)
+    is packed into one flat device buffer and copied into a pinned host buffer.  The staging
+    replaces the resident activations, so the device holds 2 x chunk activation tensors per width
+    instead of all of them."""
+
+    def __init__(self, ms, chunk=2):
+        self.ms, self.chunk = ms, chunk
+        dev = ms.gf.dev
+        self.copy = torch.cuda.Stream(dev)
+        self.Xh = {m: [x.cpu().pin_memory() for x in xs] for m, xs in ms.X.items()}
+        self.Wh = {k: w.cpu().pin_memory() for k, w in ms.W.items()}
+        self.stage = {}
+        for m, xs in ms.X.items():
+            N = xs[0].shape[0]
+            self.stage[m] = [torch.empty((chunk, N, m), dtype=xs[0].dtype, device=dev) for _ in range(2)]
+        self.h2d_bytes = (sum(t.numel() * t.element_size() for t in self.Wh.values()) +
+                          sum(self.Xh[u[1][0][2]][ms.xi[i]].numel() * 2 for i, u in
+                              ((i, ms.units[i]) for i in ms.mine)))
+        self.host_res = None
+        self.d2h_bytes = 0
+
+    def step(self):
+        ms = self.ms
+        gf, units, mine = ms.gf, ms.units, ms.mine
+        eng = pt2q.engine
+        comp = torch.cuda.current_stream(gf.dev)
+        gf.begin([(i, units[i][1][0][2], units[i][2]) for i in mine])
+        self.copy.wait_stream(comp)
+        with torch.cuda.stream(self.copy):
+            for k, Wd in ms.W.items():
+                Wd.copy_(self.Wh[k], non_blocking=True)
+        w_done = torch.cuda.Event()
+        w_done.record(self.copy)
+        # Grams: per width, units in slot order, chunk by chunk through the staging buffers
+        by_group = {}
+        for i in mine:
+            by_group.setdefault(gf.slot[i][0], []).append(i)
+        freed = {}
+        for g, items in sorted(by_group.items()):
+            m = g[0]
+            G = gf.groups[g]["G"]
+            for c, c0 in enumerate(range(0, len(items), self.chunk)):
+                part = items[c0:c0 + self.chunk]
+                buf = self.stage[m][c % 2]
+                ev = freed.get((m, c % 2))
+                if ev is not None:
+                    self.copy.wait_event(ev)  # the Gram that last read this buffer is done
+                with torch.cuda.stream(self.copy):
+                    for j, i in enumerate(part):
+                        buf[j].copy_(self.Xh[m][ms.xi[i]], non_blocking=True)
+                landed = torch.cuda.Event()
+                landed.record(self.copy)
+                comp.wait_event(landed)
+                z0 = gf.slot[part[0]][1]
+                assert [gf.slot[i][1] for i in part] == list(range(z0, z0 + len(part)))
+                eng.gram_batched([buf[j] for j in range(len(part))], G[z0:z0 + len(part)])
+                done = torch.cuda.Event()
+                done.record(comp)
+                freed[(m, c % 2)] = done
+        comp.wait_event(w_done)
+        gf.inverses()
+        jobs = [(i, [ms.W[(i, p)] for p, _, _ in units[i][1]], units[i][2]) for i in mine]
+        runs = gf.tails(jobs)
+        results = {}
+        for i, run in zip(mine, runs):
+            name, lins, _ = units[i]
+            for (p, _, _), out in zip(lins, run.finish()):
+                results[f"{name}.{p}"] = {"T2": eng.pack_ternary(out.T)[0], "alpha": out.alpha, "mu": out.mu,
+                                          "perm": out.perm}
+        gf.check()
+        manifest, flat = sharding._flatten(results)
+        if self.host_res is None or self.host_res.numel() < flat.numel():
+            self.host_res = torch.empty(flat.numel(), dtype=torch.uint8).pin_memory()
+        self.host_res[:flat.numel()].copy_(flat, non_blocking=True)
+        self.d2h_bytes = flat.numel()
+        torch.cuda.synchronize(gf.dev)
+        return manifest
+
+
+def h2d_run(ms, steps=2, warmup=1):
+    """extra.h2d: H2DStep timed like the main line (warmup, then `steps` steps, synchronised)."""
+    h = H2DStep(ms)
+    for _ in range(warmup):
+        h.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        h.step()
+    torch.cuda.synchronize()
+    s = (time.perf_counter() - t0) / steps
+    cols = sharding.units_cols([ms.units[i] for i in ms.mine])
+    out = {"ms_per_step": s * 1e3, "cols_per_s": cols / s, "steps": steps, "warmup": warmup,
+           "h2d_bytes_per_step": h.h2d_bytes, "d2h_bytes_per_step": h.d2h_bytes,
+           "pcie_gbs_if_transfer_bound": (h.h2d_bytes + h.d2h_bytes) / s / 1e9,
+           "window": "from pinned-host fp16 W and X to packed results in pinned host memory (SURVEY §8(d))",
+           "chunk_units": h.chunk}
+    del h
+    return out
 
 
 class LayerStep:
@@ -913,6 +1030,15 @@ def main(argv=None):
             res["ranks"] = ranks
         if roof is not None:
             res["roofline"] = roof
+        if (a.workload == "model" and world == 1 and not a.no_extra and not a.no_h2d and work.gf is not None
+                and a.schedule == "grams-first" and all(len(v) > 0 for v in work.X.values())):
+            log(rank, "h2d (transfer-inclusive) run ...")
+            try:
+                extra["h2d"] = h2d_run(work)
+            except Exception as e:  # reported, never allowed to drop the line
+                extra["h2d"] = {"error": f"{type(e).__name__}: {e}"}
+            gc.collect()
+            torch.cuda.empty_cache()
         if (a.workload == "model" and world == 1 and not a.no_extra and not a.no_configs
                 and not a.hidden_given and a.layers == sharding.MODELS[a.model]["layers"]):
             log(rank, "per-config runs ...")

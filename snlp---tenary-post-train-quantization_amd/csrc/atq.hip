@@ -386,11 +386,52 @@ PT2Q_DEV void atq_s1_part(const BlockArgs& A) {
   }
 }
 
+// The error-feedback coefficients C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k])
+// (main.py:201-209) of the block.  They depend only on the selection (blk, rem), not on the ATQ
+// results, so they are formed by extra workgroups of the ATQ launch itself, placed AFTER the row
+// workgroups: dispatched last, they fill the CUs the rows' ITF convergence tail leaves idle.
+struct CoeffArgs {
+  const float* Hinv;
+  long ldh;
+  const int* rem;
+  int nr, bs;
+  float* C;
+  long ldc;
+  int per_k;  // coefficient workgroups per k row (COEF_SPAN columns e each)
+};
+constexpr int COEF_SPAN = 1024;  // columns e per coefficient workgroup (4 per lane)
+
+PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
+  const int k = cb / K.per_k;
+  if (k >= K.bs) return;
+  const int e0 = (cb - k * K.per_k) * COEF_SPAN + 4 * (int)threadIdx.x;
+  const long rowb = (long)A.blk[k] * K.ldh;
+  const float dg = clampmin(K.Hinv[rowb + A.blk[k]]);
+  int re[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) re[u] = e0 + u < K.nr ? K.rem[e0 + u] : 0;
+  float h[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) h[u] = K.Hinv[rowb + re[u]];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (e0 + u < K.nr) K.C[(long)k * K.ldc + e0 + u] = h[u] / dg;
+}
+
 template <int NS, bool F>
-__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A0, Grp g) {
+__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
   const BlockArgs A = at_linear(A0, g);
   if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
     atq_s1_part(A);
+    return;
+  }
+  if ((int)blockIdx.x >= A.nS1 + rowgrid) {  // dispatched last: the EF coefficients
+    if (g.count > 0) {
+      K.Hinv = g.Hinv[blockIdx.z];
+      K.rem = zws(K.rem, g.ws);
+      K.C = zws(K.C, g.ws);
+    }
+    coeff_part(A, K, (int)blockIdx.x - A.nS1 - rowgrid);
     return;
   }
   __shared__ int wmax[WAVES];
@@ -419,52 +460,21 @@ PT2Q_DEV void finish_iters(const BlockArgs& A, int nparts) {
   if (threadIdx.x == 0) *A.iters = (A.counters[0] == A.n) ? 0 : v;
 }
 
-// The whole-block T_init == 0 case (quantizer.py:164 breaks at iteration 0 and returns the init
-// grid): a second launch reads the zero-row count after the kernel boundary and, only then,
-// redoes every row without ITF.  (A last-arriving-workgroup repair inside atq_block_kernel cost
-// an agent-scope release fence - an L2 write-back - per workgroup.)
+// After the block's ATQ, one workgroup per linear: the block's ITF iteration count
+// (finish_iters) and, only for an all-zero block, the repair of every row.  The whole-block
+// T_init == 0 case (quantizer.py:164 breaks at iteration 0 and returns the init grid) is known
+// only after every row workgroup: this launch reads the zero-row count after the kernel boundary
+// and, only then, redoes every row without ITF (one workgroup: it costs nothing when it never
+// runs; a last-arriving-workgroup repair inside atq_block_kernel cost an agent-scope release
+// fence -- an L2 write-back -- per workgroup).
 template <int NS>
-__global__ __launch_bounds__(256) void atq_zero_fixup_kernel(BlockArgs A0, int nparts, Grp g) {
+__global__ __launch_bounds__(256) void atq_finish_kernel(BlockArgs A0, int rowgrid, Grp g) {
   const BlockArgs A = at_linear(A0, g);
-  finish_iters(A, nparts);
+  finish_iters(A, rowgrid);
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
-  if (A.iters && !A.iters_part && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
-  block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
-}
-
-// After the block's ATQ: the zero-block repair (rare) and the error-feedback coefficients
-// C[k][e] = Hinv[blk_k][rem_e] / clamp(Hinv[blk_k][blk_k]) (main.py:201-209) in ONE launch; the
-// two parts are independent.
-struct CoeffArgs {
-  const float* Hinv;
-  long ldh;
-  const int* rem;
-  int nr, bs;
-  float* C;
-  long ldc;
-};
-
-template <int NS>
-__global__ __launch_bounds__(256) void atq_post_kernel(BlockArgs A0, CoeffArgs K, int fix_wgs, Grp g) {
-  const BlockArgs A = at_linear(A0, g);
-  if (g.count > 0) {
-    K.Hinv = g.Hinv[blockIdx.z];
-    K.rem = zws(K.rem, g.ws);
-    K.C = zws(K.C, g.ws);
-  }
-  finish_iters(A, fix_wgs);
-  const long q = (long)blockIdx.x * 256 + threadIdx.x;
-  if (q < (long)K.nr * K.bs) {
-    const int k = (int)(q / K.nr), e = (int)(q % K.nr);
-    const long rowb = (long)A.blk[k] * K.ldh;
-    const float dg = clampmin(K.Hinv[rowb + A.blk[k]]);
-    K.C[(long)k * K.ldc + e] = K.Hinv[rowb + K.rem[e]] / dg;
-  }
-  if ((int)blockIdx.x >= fix_wgs || A.counters[0] != A.n) return;
-  const int wave = threadIdx.x >> 6;
-  if (A.iters && !A.iters_part && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
-  block_rows<NS>(A, blockIdx.x * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
+  if (A.iters && !A.iters_part && threadIdx.x == 0) *A.iters = 0;
+  for (int rb = 0; rb < rowgrid; ++rb) block_rows<NS>(A, rb * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
 }
 
 // ----------------------------------------------------------------- per-stage kernel (row-major)
@@ -578,7 +588,7 @@ __global__ void count_zero_rows_kernel(const float* T, long ldt, int n, int b, i
 // waves of the workgroup through L1) or 64 B of one row (row-major).  The codes live in the
 // output array T between passes.  Passes: sum(w); sum|w - mu|; init (writes T, also the first
 // grid's partials); one pass per ITF iteration (round + the next grid's partials); AGA; E.
-constexpr int WIDE_WAVES = 4;  // 16 rows per workgroup
+constexpr int WIDE_WAVES = 8;  // 32 rows per workgroup: one 128-B line of a Wt column per workgroup
 
 struct WideArgs {
   int mode;          // PT2Q_STAGE_* ; BLOCK = fused init+ITF+AGA+E of the block loop
@@ -795,7 +805,7 @@ __global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_block_kernel(WideArg
   wide_block_rows<FM>(A, false, true);
 }
 
-// whole-block T_init == 0 repair after the kernel boundary (see atq_zero_fixup_kernel)
+// whole-block T_init == 0 repair after the kernel boundary (see atq_finish_kernel)
 template <bool FM>
 __global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_zero_fixup_kernel(WideArgs A) {
   if (A.counters[0] != A.n) return;
@@ -885,21 +895,20 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part,
               G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_fallback};
   int grid = ceil_div(n, ROWS_PER_WG);
+  // the EF coefficient workgroups (Hinv given, columns left): COEF_SPAN columns e of one k row each
+  const int per_k = (Hinv && nr > 0) ? ceil_div(nr, COEF_SPAN) : 0;
+  const CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc, per_k > 0 ? per_k : 1};
+  const int cgrid = per_k * b;
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
     if (b == 16 * NS)
-      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(grid + nS1, 1, nz), dim3(256), 0, st, A, g);
+      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(nS1 + grid + cgrid, 1, nz), dim3(256), 0, st, A, g, K,
+                         grid);
     else
-      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(grid + nS1, 1, nz), dim3(256), 0, st, A, g);
+      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(nS1 + grid + cgrid, 1, nz), dim3(256), 0, st, A, g, K,
+                         grid);
     PT2Q_LAUNCH_CHECK();
-    if (Hinv && nr > 0) {  // zero-block repair + EF coefficients in one launch
-      CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc};
-      const int cgrid = ceil_div((long)nr * b, 256);
-      hipLaunchKernelGGL(atq_post_kernel<NS>, dim3(cgrid > grid ? cgrid : grid, 1, nz), dim3(256), 0, st, A,
-                         K, grid, g);
-    } else {
-      hipLaunchKernelGGL(atq_zero_fixup_kernel<NS>, dim3(grid, 1, nz), dim3(256), 0, st, A, grid, g);
-    }
+    hipLaunchKernelGGL(atq_finish_kernel<NS>, dim3(1, 1, nz), dim3(256), 0, st, A, grid, g);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   });

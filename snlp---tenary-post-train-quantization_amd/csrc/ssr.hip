@@ -794,24 +794,53 @@ __global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, lo
   }
 }
 
-// Wide blocks (b > 512, per-channel): S1[j] = sequential row sum of A[blk_j][blk_l] over l, one
-// thread per j across many workgroups (the same order as aga_s1_kernel), then d in order.
+// Wide blocks (b > 512, per-channel): S1[j] = sequential row sum of A[blk_j][blk_l] over l (the
+// same order as aga_s1_kernel).  A workgroup owns S1W_ROWS rows j: all 256 threads stage a
+// S1W_ROWS x S1W_COLS tile of them (coalesced along l) into one of two LDS buffers while lanes
+// 0..S1W_ROWS-1 of wave 0 run their rows' serial chains over the other buffer, so the chains never
+// wait on a global load and every load instruction reads whole rows segments (one thread per j
+// striding over whole rows read 64 rows per instruction and ran 3.3 ms at b = 13824).
+constexpr int S1W_ROWS = 32, S1W_COLS = 256;
 __global__ __launch_bounds__(256) void s1_rows_kernel(const float* A, long lda, const int* blk,
                                                       int b, float* S1) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= b) return;
-  const float* row = A + (long)(blk ? blk[j] : j) * lda;
+  __shared__ float tile[2][S1W_ROWS][S1W_COLS + 1];
+  const int tid = threadIdx.x, j0 = blockIdx.x * S1W_ROWS;
+  const int nj = min(S1W_ROWS, b - j0);
+  auto stage = [&](int c, int buf) {  // columns [c, c + S1W_COLS) of the workgroup's rows
+    const int l = c + tid;
+    const int bl = l < b ? (blk ? blk[l] : l) : 0;
+    float v[S1W_ROWS];
+#pragma unroll
+    for (int r = 0; r < S1W_ROWS; ++r) {
+      const int j = j0 + (r < nj ? r : 0);
+      v[r] = A[(long)(blk ? blk[j] : j) * lda + bl];
+    }
+#pragma unroll
+    for (int r = 0; r < S1W_ROWS; ++r) tile[buf][r][tid] = v[r];
+  };
   float s = 0.0f;
-  int l = 0;
-  for (; l + 8 <= b; l += 8) {
-    float v[8];
+  stage(0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int c = 0; c < b; c += S1W_COLS) {
+    if (c + S1W_COLS < b) stage(c + S1W_COLS, buf ^ 1);
+    if (tid < nj) {
+      const int len = min(S1W_COLS, b - c);
+      const float* row = tile[buf][tid];
+      int l = 0;
+      for (; l + 8 <= len; l += 8) {
+        float t[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = row[blk ? blk[l + u] : l + u];
+        for (int u = 0; u < 8; ++u) t[u] = row[l + u];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s = s + v[u];
+        for (int u = 0; u < 8; ++u) s = s + t[u];
+      }
+      for (; l < len; ++l) s = s + row[l];
+    }
+    __syncthreads();
+    buf ^= 1;
   }
-  for (; l < b; ++l) s = s + row[blk ? blk[l] : l];
-  S1[j] = s;
+  if (tid < nj) S1[j0 + tid] = s;
 }
 
 // Blocks up to 512 columns: one workgroup per row j gathers A[blk_j][blk_l] (all loads in
@@ -965,7 +994,7 @@ int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b,
   }
   if (src == 1) {
     if (b > 512)
-      hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, 256)), dim3(256), 0, st, A, lda, blk, b, S1);
+      hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, S1W_ROWS)), dim3(256), 0, st, A, lda, blk, b, S1);
     else
       hipLaunchKernelGGL(s1_row_wg_kernel, dim3(b), dim3(128), 0, st, A, lda, blk, b, S1);
     PT2Q_LAUNCH_CHECK();

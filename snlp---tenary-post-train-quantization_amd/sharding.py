@@ -366,7 +366,7 @@ class GramsFirst:
     inverses of batched=False and the pinv fallback, so no path damps differently."""
 
     def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, group: int = 16,
-                 overlap: bool = False, batch_grams: bool = True):
+                 overlap: bool = False, batch_grams: bool = True, inv_streams: int = 1):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         # step 1 batched: the Grams of each (m, N) group in data-parallel launches
@@ -385,6 +385,12 @@ class GramsFirst:
         self.inv_stream = (torch.cuda.Stream(self.dev, priority=-1) if batched and overlap and self.dev.type == "cuda"
                            else None)
         self.inv_done = {}
+        # inv_streams > 1 (without overlap): the batched inverse chunks of all widths spread over
+        # that many streams (longest first, least-loaded stream), so one chunk's latency-bound
+        # panel steps run beside another chunk's MFMA-bound trailing updates; each stream has its
+        # own scratch, and the caller's stream joins them all before any tail
+        self.inv_streams = max(1, int(inv_streams))
+        self._istreams, self._iscratch = [], []
         self.G, self.ws = {}, {}
         self.slot = {}       # key -> (group, index)
         self.groups = {}     # (m, N) -> {"G", "Hinv", "info"} packed over the group's units
@@ -468,6 +474,30 @@ class GramsFirst:
         caller = torch.cuda.current_stream(self.dev)
         self.inv_done = {}
         live = [g for g in sorted(self.groups) if self.groups[g]["Hinv"] is not None]
+        if self.inv_stream is None and self.inv_streams > 1 and self.dev.type == "cuda":
+            jobs = []
+            for g in live:
+                c = self.groups[g]["G"].shape[0]
+                jobs += [(float(g[0]) ** 3 * min(self.chunk, c - z0), g, z0, min(self.chunk, c - z0))
+                         for z0 in range(0, c, self.chunk)]
+            jobs.sort(key=lambda j: (-j[0], j[1], j[2]))
+            while len(self._istreams) < min(self.inv_streams, len(jobs)):
+                self._istreams.append(torch.cuda.Stream(self.dev))
+                self._iscratch.append({})
+            load = [0.0] * len(self._istreams)
+            for cost, g, z0, k in jobs:
+                si = min(range(len(load)), key=lambda i: (load[i], i))
+                load[si] += cost
+                st = self._istreams[si]
+                st.wait_stream(caller)  # the Grams
+                grp = self.groups[g]
+                with torch.cuda.stream(st):
+                    self.engine.hessian_inverse_batched(grp["G"][z0:z0 + k], g[1], self.percdamp,
+                                                        Hinv=grp["Hinv"][z0:z0 + k], info=grp["info"][z0:z0 + k],
+                                                        scratch=self._iscratch[si], chunk=k)
+            for st in self._istreams:
+                caller.wait_stream(st)
+            return
         if self.inv_stream is None:  # no overlap: on the caller's stream, before any tail
             for g in live:
                 grp = self.groups[g]

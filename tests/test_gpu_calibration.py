@@ -121,13 +121,14 @@ def test_unit_pipeline_equals_sequential(pt2q, lanes):
                 assert bits_equal(host(a), host(b))
 
 
-@pytest.mark.parametrize("batched,chunk,group", [(False, 32, 1), (True, 32, 1), (True, 1, 1), (True, 32, 16),
-                                                 (True, 2, 2)])
-def test_grams_first_schedule_equals_sequential(pt2q, batched, chunk, group):
+@pytest.mark.parametrize("batched,chunk,group,inv_streams", [(False, 32, 1, 1), (True, 32, 1, 1), (True, 1, 1, 1),
+                                                             (True, 32, 16, 1), (True, 2, 2, 1), (True, 1, 16, 3)])
+def test_grams_first_schedule_equals_sequential(pt2q, batched, chunk, group, inv_streams):
     """sharding.GramsFirst (every Gram of the step first into packed per-width slots, then --
     batched -- every width's Hessian inverses in batched launches, then the block loops on the
     pipeline lanes, per unit or -- group > 1 -- grouped across units by shape) through
-    quantize_units_sharded == quantize_unit per unit."""
+    quantize_units_sharded == quantize_unit per unit; inv_streams > 1 spreads the inverse chunks
+    over streams with scratch of their own."""
     import importlib
     sharding = importlib.import_module("pt2q.sharding")
     specs = [(512, (384, 256), 1024, torch.float16), (768, (512,), 2048, torch.float16),
@@ -139,7 +140,7 @@ def test_grams_first_schedule_equals_sequential(pt2q, batched, chunk, group):
         units.append((f"u{i}", [(f"p{k}", n, m) for k, n in enumerate(ns)], N))
         data[f"u{i}"] = (X, Ws)
     pipe = pt2q.UnitPipeline("cuda", 128, True, lanes=3)
-    gf = sharding.GramsFirst(pipe, "cuda", batched=batched, chunk=chunk, group=group)
+    gf = sharding.GramsFirst(pipe, "cuda", batched=batched, chunk=chunk, group=group, inv_streams=inv_streams)
     res, mine = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False,
                                                 grams_first=gf)
     res2, _ = sharding.quantize_units_sharded(units, lambda u: data[u[0]], pack=False,
