@@ -40,6 +40,9 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_GEMMX_STAGES", t.gemmx_stages);
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);
+  geti("PT2Q_WIDE_WAVES", t.wide_waves);
+  getb("PT2Q_EF_V2", t.ef_v2);
+  if (t.wide_waves != 8) t.wide_waves = 4;
   if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
     const long c = std::atol(e);
     if (c >= 0) t.spin_cap_long = t.spin_cap_short = t.spin_cap_fallback = c;
@@ -237,6 +240,23 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
   const bool ssr = (flags & PT2Q_FLAG_SSR) != 0;
   const int aga = flags & PT2Q_AGA_MASK;
   int* iters = iters_dev ? iters_dev : w.iters;
+  if (B == 1 && m > 512 && aga != PT2Q_AGA_HESS) {
+    // Per-channel (block_size >= m, main.py:176-189 with one block): the block is every column in
+    // ascending order -- SSR over the whole remaining set returns it in rem order, and rem is
+    // [0, m) -- so the wide ATQ reads the caller's row-major W in place (no feature-major copy, no
+    // code transpose) and writes T, alpha, mu (n x 1) straight into the outputs.
+    {
+      StageScope ts(PT2Q_TIMER_SETUP, st);
+      if (hipMemsetAsync(w.counters, 0, sizeof(int) * 2, st) != hipSuccess) return PT2Q_E_HIP;
+      if (hipMemsetAsync(iters, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
+      if ((rc = pt2q_launch_select_seq(0, 0, m, m, nullptr, w.blk, w.rem[1], perm, st)) != PT2Q_OK) return rc;
+    }
+    StageScope ts_atq(PT2Q_TIMER_ATQ, st);
+    const bool act = aga == PT2Q_AGA_ACT;
+    if (act && (rc = pt2q_launch_aga_s1(1, A, lda, nullptr, m, w.S1, w.d, st)) != PT2Q_OK) return rc;
+    return pt2q_launch_atq_wide_rm(W, wdtype, ldw_in, n, m, act ? w.S1 : nullptr, w.d, max_iter, alpha, mu, T,
+                                   tdtype, m, iters, w.counters, st);
+  }
   {
     StageScope ts(PT2Q_TIMER_SETUP, st);
     // W (n x m) -> Wt (m x ldw, fp32)

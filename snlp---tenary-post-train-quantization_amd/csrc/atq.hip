@@ -588,7 +588,9 @@ __global__ void count_zero_rows_kernel(const float* T, long ldt, int n, int b, i
 // waves of the workgroup through L1) or 64 B of one row (row-major).  The codes live in the
 // output array T between passes.  Passes: sum(w); sum|w - mu|; init (writes T, also the first
 // grid's partials); one pass per ITF iteration (round + the next grid's partials); AGA; E.
-constexpr int WIDE_WAVES = 8;  // 32 rows per workgroup: one 128-B line of a Wt column per workgroup
+// waves per workgroup (4 rows each): pt2q_tuning().wide_waves (4 or 8), up to WIDE_WAVES_MAX
+constexpr int WIDE_WAVES_MAX = 8;
+inline int wide_waves() { return pt2q_tuning().wide_waves; }
 
 struct WideArgs {
   int mode;          // PT2Q_STAGE_* ; BLOCK = fused init+ITF+AGA+E of the block loop
@@ -611,20 +613,39 @@ struct WideArgs {
 };
 constexpr int MODE_BLOCK = 100;
 
-template <bool FM>
+// Storage layouts of a wide row (the policy of WideRow): where column c of row i lives in W and
+// T, and their element types.  FM: the block loop's feature-major fp32 Wt / int8 Tt; RM<TI, TO>:
+// row-major W of type TI (float / _Float16 / uint16_t bf16 bits, read as exact fp32) and T of type TO (fp32 codes for
+// the per-method stage surface, int8 or fp32 for the per-channel block loop, which reads the
+// caller's weights in place).
+struct LayFM {
+  static constexpr bool FM = true;
+  PT2Q_DEV static float w(const WideArgs& A, long i, long c) { return A.W[c * A.ldw + i]; }
+  PT2Q_DEV static float t(const WideArgs& A, long i, long c) { return (float)((const int8_t*)A.T)[c * A.ldt + i]; }
+  PT2Q_DEV static void set_t(const WideArgs& A, long i, long c, float v) { ((int8_t*)A.T)[c * A.ldt + i] = (int8_t)v; }
+};
+PT2Q_DEV float to_f32(float x) { return x; }
+PT2Q_DEV float to_f32(_Float16 x) { return (float)x; }
+PT2Q_DEV float to_f32(uint16_t x) { return __uint_as_float(((uint32_t)x) << 16); }  // bf16 bits
+template <class TI, class TO>
+struct LayRM {
+  static constexpr bool FM = false;
+  PT2Q_DEV static float w(const WideArgs& A, long i, long c) {
+    return to_f32(((const TI*)(const void*)A.W)[i * A.ldw + c]);
+  }
+  PT2Q_DEV static float t(const WideArgs& A, long i, long c) { return (float)((const TO*)A.T)[i * A.ldt + c]; }
+  PT2Q_DEV static void set_t(const WideArgs& A, long i, long c, float v) { ((TO*)A.T)[i * A.ldt + c] = (TO)v; }
+};
+typedef LayRM<float, float> LayStage;
+
+template <class L>
 struct WideRow {
   const WideArgs& A;
   int i, l;  // row (clamped to 0 when invalid: reads stay in range), residue class
   bool valid;
-  PT2Q_DEV long woff(long c) const { return FM ? c * A.ldw + i : (long)i * A.ldw + c; }
-  PT2Q_DEV long toff(long c) const { return FM ? c * A.ldt + i : (long)i * A.ldt + c; }
-  PT2Q_DEV float t(long c) const {
-    return FM ? (float)((const int8_t*)A.T)[toff(c)] : ((const float*)A.T)[toff(c)];
-  }
+  PT2Q_DEV float t(long c) const { return L::t(A, i, c); }
   PT2Q_DEV void set_t(long c, float v) const {
-    if (!valid) return;
-    if (FM) ((int8_t*)A.T)[toff(c)] = (int8_t)v;
-    else ((float*)A.T)[toff(c)] = v;
+    if (valid) L::set_t(A, i, c, v);
   }
 
   // One streamed pass: f(k, c, w, t) for this lane's columns k = l + 16 s in s order (c = the
@@ -639,10 +660,10 @@ struct WideRow {
       for (int u = 0; u < 16; ++u) {
         const int k = k0 + 16 * u + l;
         const int kc = k < b ? k : 0;
-        c[u] = FM ? (long)A.blk[kc] : (long)kc;
+        c[u] = (L::FM && A.blk) ? (long)A.blk[kc] : (long)kc;
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) w[u] = A.W[woff(c[u])];
+      for (int u = 0; u < 16; ++u) w[u] = L::w(A, i, c[u]);
       if constexpr (TC) {
 #pragma unroll
         for (int u = 0; u < 16; ++u) tv[u] = t(c[u]);
@@ -656,8 +677,8 @@ struct WideRow {
   }
 };
 
-template <bool FM>
-PT2Q_DEV float wide_sum_w(const WideRow<FM>& R) {
+template <class L>
+PT2Q_DEV float wide_sum_w(const WideRow<L>& R) {
   float p = 0.0f;
   R.template pass<false>([&](int, long, float w, float) { p = p + w; });
   return bfly16(p);
@@ -665,8 +686,8 @@ PT2Q_DEV float wide_sum_w(const WideRow<FM>& R) {
 
 // ternary_init (quantizer.py:32-69): writes T; also returns the first grid's sums (row_grid's
 // partials over the codes just written -- same values, same order).  Returns all-zero.
-template <bool FM>
-PT2Q_DEV bool wide_init(const WideRow<FM>& R, float wsum, float* a, float* m, float* g) {
+template <class L>
+PT2Q_DEV bool wide_init(const WideRow<L>& R, float wsum, float* a, float* m, float* g) {
   const float fb = (float)R.A.b;
   const float mu = wsum / fb;
   float p = 0.0f;
@@ -700,8 +721,8 @@ PT2Q_DEV void wide_grid(const float* g, float fb, float wsum, float* a, float* m
 }
 
 // grid partials over the codes in T (the ITF stage entry without a preceding init pass)
-template <bool FM>
-PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, float* g) {
+template <class L>
+PT2Q_DEV void wide_grid_pass(const WideRow<L>& R, float* g) {
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
   R.template pass<true>([&](int, long, float w, float t) {
     pwt = pwt + w * t;
@@ -715,8 +736,8 @@ PT2Q_DEV void wide_grid_pass(const WideRow<FM>& R, float* g) {
 
 // flexible_round (quantizer.py:110-134) over the row, writing changed codes; accumulates the
 // next grid's sums into g.  Returns whether this lane changed a code.
-template <bool FM>
-PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, float a, float m, float* g) {
+template <class L>
+PT2Q_DEV bool wide_round_pass(const WideRow<L>& R, float a, float m, float* g) {
   const float as = clampmin(a);
   const float ras = rcp_approx(as);
   const bool rok = rcp_ok(as);
@@ -740,8 +761,8 @@ PT2Q_DEV bool wide_round_pass(const WideRow<FM>& R, float a, float m, float* g) 
 
 // iterative_ternary_fitting (quantizer.py:136-175), wave-level stop as row_itf; g holds the
 // grid sums of the codes in T on entry.
-template <bool FM>
-PT2Q_DEV int wide_itf(const WideRow<FM>& R, float wsum, int max_iter, float* a, float* m, float* g) {
+template <class L>
+PT2Q_DEV int wide_itf(const WideRow<L>& R, float wsum, int max_iter, float* a, float* m, float* g) {
   int it = 0;
   bool any = true;
   for (; it < max_iter; ++it) {
@@ -754,8 +775,8 @@ PT2Q_DEV int wide_itf(const WideRow<FM>& R, float wsum, int max_iter, float* a, 
 }
 
 // activation_aware_grid_alignment (quantizer.py:177-248) given S1 and d
-template <bool FM>
-PT2Q_DEV void wide_aga(const WideRow<FM>& R, const float* S1, float d, float* a, float* m) {
+template <class L>
+PT2Q_DEV void wide_aga(const WideRow<L>& R, const float* S1, float d, float* a, float* m) {
   float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
   R.template pass<true>([&](int k, long, float w, float t) {
     const float c = S1[k];
@@ -771,18 +792,18 @@ PT2Q_DEV void wide_aga(const WideRow<FM>& R, const float* S1, float d, float* a,
   *m = (t2s1 * ws1 - v * wts1) / den;
 }
 
-template <bool FM>
-PT2Q_DEV WideRow<FM> wide_row(const WideArgs& A) {
+template <class L>
+PT2Q_DEV WideRow<L> wide_row(const WideArgs& A) {
   const int lane = threadIdx.x & 63;
-  const int i = ((int)blockIdx.x * WIDE_WAVES + (int)(threadIdx.x >> 6)) * 4 + (lane >> 4);
+  const int i = ((int)blockIdx.x * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6)) * 4 + (lane >> 4);
   const bool valid = i < A.n;
-  return WideRow<FM>{A, valid ? i : 0, lane & 15, valid};
+  return WideRow<L>{A, valid ? i : 0, lane & 15, valid};
 }
 
 // Block-loop mode for this wave's 4 rows: init -> ITF -> AGA -> E.
-template <bool FM>
+template <class L>
 PT2Q_DEV void wide_block_rows(const WideArgs& A, bool skip_itf, bool count_zero) {
-  const WideRow<FM> R = wide_row<FM>(A);
+  const WideRow<L> R = wide_row<L>(A);
   const float wsum = wide_sum_w(R);
   float a, m, g[3];
   const bool zero = wide_init(R, wsum, &a, &m, g);
@@ -800,22 +821,22 @@ PT2Q_DEV void wide_block_rows(const WideArgs& A, bool skip_itf, bool count_zero)
     R.template pass<true>([&](int k, long, float w, float t) { A.Et[(long)k * A.lde + R.i] = w - (a * t + m); });
 }
 
-template <bool FM>
-__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_block_kernel(WideArgs A) {
-  wide_block_rows<FM>(A, false, true);
+template <class L>
+__global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_block_kernel(WideArgs A) {
+  wide_block_rows<L>(A, false, true);
 }
 
 // whole-block T_init == 0 repair after the kernel boundary (see atq_finish_kernel)
-template <bool FM>
-__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_zero_fixup_kernel(WideArgs A) {
+template <class L>
+__global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_zero_fixup_kernel(WideArgs A) {
   if (A.counters[0] != A.n) return;
   if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
-  wide_block_rows<FM>(A, true, false);
+  wide_block_rows<L>(A, true, false);
 }
 
 // Per-method stages on row-major W / float T (quantizer.py surface) for b > 512.
-__global__ __launch_bounds__(64 * WIDE_WAVES) void atq_wide_stage_kernel(WideArgs A) {
-  const WideRow<false> R = wide_row<false>(A);
+__global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_stage_kernel(WideArgs A) {
+  const WideRow<LayStage> R = wide_row<LayStage>(A);
   const float wsum = wide_sum_w(R);
   float a = R.valid ? A.alpha[R.i] : 0.0f, m = R.valid ? A.mu[R.i] : 0.0f, g[3];
   int it = 0;
@@ -883,10 +904,10 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   if (b > 512) {
     WideArgs WA{MODE_BLOCK, Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde,
                 iters, counters, 0};
-    const int wgrid = ceil_div(n, 4 * WIDE_WAVES);
-    hipLaunchKernelGGL(atq_wide_block_kernel<true>, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
+    const int wgrid = ceil_div(n, 4 * wide_waves());
+    hipLaunchKernelGGL(atq_wide_block_kernel<LayFM>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<true>, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
+    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<LayFM>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
     if (Hinv && nr > 0) return pt2q_launch_ef_coeffs(Hinv, ldh, blk, b, rem, nr, C, ldc, st);
     return PT2Q_OK;
@@ -914,6 +935,34 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   });
 }
 
+// Per-channel block of the block loop (b = m > 512, one block of every column in ascending
+// order): the wide ATQ on the caller's row-major W (wdtype f32 / f16 / bf16, read as exact fp32)
+// writing T (tdtype int8 / f32, ld ldt) and alpha / mu (n) in place -- the same values, in the
+// same order, as the feature-major wide path on the transposed copy (LayRM vs LayFM: only the
+// addresses differ).  counters[0] (zero rows) and *iters are zeroed by the caller.
+int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, const float* S1, const float* d,
+                            int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
+                            int* counters, hipStream_t st) {
+  WideArgs WA{MODE_BLOCK, (const float*)W, ldw, n, b, nullptr, S1, d, max_iter, alpha, mu, T, ldt, nullptr, 0,
+              iters, counters, 0};
+  const int wgrid = ceil_div(n, 4 * wide_waves());
+  auto go = [&](auto lay) {
+    typedef decltype(lay) L;
+    hipLaunchKernelGGL(atq_wide_block_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  };
+  const bool i8 = tdtype == PT2Q_I8;
+  switch (wdtype) {
+    case PT2Q_F32: return i8 ? go(LayRM<float, int8_t>{}) : go(LayRM<float, float>{});
+    case PT2Q_F16: return i8 ? go(LayRM<_Float16, int8_t>{}) : go(LayRM<_Float16, float>{});
+    case PT2Q_BF16: return i8 ? go(LayRM<uint16_t, int8_t>{}) : go(LayRM<uint16_t, float>{});
+  }
+  return PT2Q_E_ARG;
+}
+
 extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int b, float* alpha,
                               float* mu, float* T, int64_t ldt, const float* S1,
                               const float* d_dev, int max_iter, int* iters_dev, void* workspace,
@@ -939,14 +988,14 @@ extern "C" int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int 
   if (b > 512) {
     WideArgs WA{mode, Wp, ldw, n, b, nullptr, S1, d_dev, max_iter, alpha, mu, T,
                 ldt, nullptr, 0, iters_dev, zero_rows, 0};
-    const int wgrid = ceil_div(n, 4 * WIDE_WAVES);
+    const int wgrid = ceil_div(n, 4 * wide_waves());
     if (mode == PT2Q_STAGE_FULL) {
       if (hipMemsetAsync(zero_rows, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
-      hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
+      hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
       PT2Q_LAUNCH_CHECK();
       WA.pass = 1;
     }
-    hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * WIDE_WAVES), 0, st, WA);
+    hipLaunchKernelGGL(atq_wide_stage_kernel, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }

@@ -159,7 +159,9 @@ PT2Q_DEV void ef_read(uint32_t baseA, uint32_t baseB, float (&a)[2], float (&b)[
   b[1] = ef_ld<S * 2 * EF_ROWB + 128>(baseB);
 }
 
-struct EfAcc {
+// KS k rows per LDS stage (EF_KH for ef_gemm_kernel's two K halves, E2_KS for ef2_gemm_kernel)
+template <int KS>
+struct EfAccT {
   f32x16 acc[2][2];  // [rm][rn], transposed MFMA: lane <-> e row, registers <-> i columns
 
   // k-pair S: its operands are in set S % 4; the reads of pair S+2 go to set (S+2) % 4, whose
@@ -171,7 +173,7 @@ struct EfAcc {
   // wait is pinned.
   template <int S, class IO>
   PT2Q_DEV void run(uint32_t bA, uint32_t bB, float (&a)[4][2], float (&b)[4][2], IO& io) {
-    constexpr int NP = EF_KH / 2;
+    constexpr int NP = KS / 2;
     if constexpr (S < NP) {
       constexpr int c = S % 4;
       if constexpr (S + 2 < NP) ef_read<S + 2>(bA, bB, a[(S + 2) % 4], b[(S + 2) % 4]);
@@ -206,13 +208,13 @@ struct EfAcc {
     }
   }
 
-  // the 32 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
+  // the KS / 2 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
   template <class IO>
   PT2Q_DEV void half(uint32_t stg, IO& io) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
     const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
-    const uint32_t bB = stg + EF_PANEL + lk * EF_ROWB + (wc * 64 + li) * 4;
+    const uint32_t bB = stg + KS * EF_ROWB + lk * EF_ROWB + (wc * 64 + li) * 4;
     float a[4][2], b[4][2];
     ef_read<0>(bA, bB, a[0], b[0]);
     ef_read<1>(bA, bB, a[1], b[1]);
@@ -220,6 +222,7 @@ struct EfAcc {
     run<0>(bA, bB, a, b, io);
   }
 };
+using EfAcc = EfAccT<EF_KH>;
 
 PT2Q_DEV int ef_row(int e0, int rm) {
   const int lane = threadIdx.x & 63, wr = (threadIdx.x >> 6) >> 1;
@@ -571,6 +574,223 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
   }
 }
 
+// ---- ef2_gemm_kernel: the same product with two workgroups per CU ----------------------------
+// ef_gemm_kernel holds ONE workgroup per CU (two 64-row K stages = 128 KiB of LDS, 336 registers):
+// each SIMD runs a single wave, so every stall of that wave -- an LDS-read wait, a barrier, a DMA
+// still landing -- idles the MFMA pipe (MFMA busy 0.48 in the 7B step).  Here a workgroup keeps
+// a ring of two 32-row K stages (32 KiB each; 66 KiB with the w-bar scratch) and at most 256
+// registers per lane, so two workgroups share every CU and each SIMD interleaves two waves: one
+// issues MFMAs while the other waits.  Per tile: the old Wt values are loaded at the top (their
+// latency hides under the tile's MFMAs), the K stages stream through the ring (the stage after
+// next is fetched into the slot just consumed, running on into the next tile's first two stages),
+// and the epilogue subtracts, stores, and forms the tile's own w-bar partials.  The k-pairs are
+// issued in ascending order into the same accumulators, the product is subtracted once, and the
+// w-bar is the same CHUNK128 tree: bit-identical to ef_gemm_kernel.
+constexpr int E2_KS = 32;                  // k rows per stage (16 k-pairs)
+constexpr int E2_PANEL = E2_KS * EF_ROWB;  // 16 KiB
+constexpr int E2_STAGE = 2 * E2_PANEL;     // A + B: 32 KiB
+
+// One 16-B chunk q (< 4) of stage s of tile (e0, i0) by per-lane addresses (ragged stages); the
+// conventions of ef_stage_q (zero chunk past bs, in-range garbage in dropped rows / columns).
+PT2Q_DEV void e2_stage_q(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, int q, bool withB) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  typedef __attribute__((address_space(3))) void* lptr;
+  const int kr = (wave * 4 + q) * 2 + (lane >> 5);
+  const int k = s * E2_KS + kr;
+  const int d = 4 * (lane & 31);
+  const bool kin = k < a.bs;
+  const int e = e0 + d, i = i0 + d;
+  const void* sa = kin ? (const void*)(a.Ck + (e < a.nr ? (long)k * a.ldk + e : 0)) : (const void*)&ef_zero16;
+  const void* sb = kin ? (const void*)(a.Et + (i < a.ldw ? (long)k * a.ldw + i : 0)) : (const void*)&ef_zero16;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  __builtin_amdgcn_global_load_lds(sa, (lptr)(stg + (wv * 4 + q) * 1024), 16, 0, 0);
+  if (withB) __builtin_amdgcn_global_load_lds(sb, (lptr)(stg + E2_PANEL + (wv * 4 + q) * 1024), 16, 0, 0);
+}
+
+struct E2Vo {
+  uint32_t a[4], b[4];
+};
+
+PT2Q_DEV void e2_voff(const EfArgs& a, E2Vo& v) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int kr = (wave * 4 + q) * 2 + (lane >> 5), d = 4 * (lane & 31);
+    v.a[q] = (uint32_t)(((long)kr * a.ldk + d) * 4);
+    v.b[q] = (uint32_t)(((long)kr * a.ldw + d) * 4);
+  }
+}
+
+// stage s of tile (e0, i0) into slot `stg`: scalar-base DMAs when whole (ef_stage_any), else per
+// lane; returns the DMA instructions issued per wave (8, or 4 without the B panel)
+PT2Q_DEV int e2_stage(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, uint32_t stg_lds, const E2Vo& v,
+                      bool withB) {
+  const bool fast = (s + 1) * E2_KS <= a.bs && e0 + EF_T <= a.nr && i0 + EF_T <= a.ldw;
+  if (!fast) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e2_stage_q(a, e0, i0, s, stg, q, withB);
+    return withB ? 8 : 4;
+  }
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const char* ba = (const char*)(a.Ck + (long)s * E2_KS * a.ldk + e0);
+  const char* bb = (const char*)(a.Et + (long)s * E2_KS * a.ldw + i0);
+  const uint32_t mA = stg_lds + (uint32_t)(wv * 4 * 1024), mB = mA + E2_PANEL;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ef_dma_asm(ba, v.a[q], mA + q * 1024);
+    if (withB) ef_dma_asm(bb, v.b[q], mB + q * 1024);
+  }
+  return withB ? 8 : 4;
+}
+
+// s_waitcnt vmcnt(n), n < 64 (immediate operand)
+PT2Q_DEV void e2_vmcnt(int n) {
+  switch (n) {
+#define E2_W(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    E2_W(0) E2_W(1) E2_W(2) E2_W(3) E2_W(4) E2_W(5) E2_W(6) E2_W(7) E2_W(8) E2_W(9) E2_W(10) E2_W(11) E2_W(12)
+    E2_W(13) E2_W(14) E2_W(15) E2_W(16) E2_W(17) E2_W(18) E2_W(19) E2_W(20) E2_W(21) E2_W(22) E2_W(23) E2_W(24)
+    E2_W(25) E2_W(26) E2_W(27) E2_W(28) E2_W(29) E2_W(30) E2_W(31) E2_W(32) E2_W(33) E2_W(34) E2_W(35) E2_W(36)
+    E2_W(37) E2_W(38) E2_W(39) E2_W(40) E2_W(41) E2_W(42) E2_W(43) E2_W(44) E2_W(45) E2_W(46) E2_W(47) E2_W(48)
+    E2_W(49) E2_W(50) E2_W(51) E2_W(52) E2_W(53) E2_W(54) E2_W(55) E2_W(56) E2_W(57) E2_W(58) E2_W(59) E2_W(60)
+    E2_W(61) E2_W(62)
+#undef E2_W
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int J, int JE>
+PT2Q_DEV void ef_wbar_span(const int (&prow)[2], const u32x4 (&pend)[EF_CV], float* red) {
+  if constexpr (J < JE) {
+    ef_wbar_step<J>(prow, pend, red);
+    ef_wbar_span<J + 1, JE>(prow, pend, red);
+  }
+}
+
+// old values of column group rn (c[j], j = (rm * 2 + rn) * 4 + q: 8 loads), or their results
+template <int RN>
+PT2Q_DEV void e2_load(u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2]) {
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      c[(rm * 2 + RN) * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
+}
+
+template <int RN, int KS>
+PT2Q_DEV void e2_sub_store(u32x4 (&c)[EF_CV], const EfAccT<KS>& F, __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2]) {
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (rm * 2 + RN) * 4 + q;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c[j][u] = __float_as_uint(__uint_as_float(c[j][u]) - F.acc[rm][RN][4 * q + u]);
+      __builtin_amdgcn_raw_buffer_store_b128(c[j], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
+    }
+}
+
+// NST = K stages per tile (2: bs <= 64, 4: bs <= 128; stages past bs are zero chunks: no-op pairs).
+// Issue order per tile, for the hand-counted vmcnt waits: [next rows: 2] [stage s + 2 after each
+// compute s (the last two: the next tile's stages 0 and 1)] with [old values, column group 0: 8]
+// just before the last stage's compute; the epilogue then [waits for group 0] [stores it: 8]
+// [loads group 1: 8] [waits for everything] [stores it: 8] [w-bar partials: P].  So at the next
+// tile's top only that tile's last stores (SP) may still be in flight beside its stages.
+template <int NST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void ef2_gemm_kernel(
+    EfArgs a0, long wt_bytes, long part_bytes) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * E2_STAGE];
+  __shared__ __attribute__((aligned(16))) float red[EF_RED];  // w-bar wave sums (ef_wbar_step)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  const int total = a0.ntile * a0.nz;
+  int t = blockIdx.x;
+  if (t >= total) return;
+  auto corner = [&](int t, EfArgs& a, int& e0, int& i0) {
+    const int z = t / a0.ntile, tl = t - z * a0.ntile;
+    a = ef_linear(a0, z);
+    e0 = (tl / a0.ti) * EF_T;
+    i0 = (tl % a0.ti) * EF_T;
+  };
+  auto rsrc = [&](const EfArgs& a) { return __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000); };
+  auto prsrc = [&](const EfArgs& x) { return __builtin_amdgcn_make_buffer_rsrc(x.part, 0, (int)part_bytes, 0x00020000); };
+  const int P = a0.part ? EF_PS : 0;  // w-bar partial stores per wave per tile
+  EfArgs a;
+  int e0, i0, wrow[2];
+  corner(t, a, e0, i0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  ef_rows(a, e0, wrow);
+  E2Vo vo;
+  e2_voff(a0, vo);
+  e2_stage(a, e0, i0, 0, smem, lds0, vo, true);
+  int Dn1 = e2_stage(a, e0, i0, 1, smem + E2_STAGE, lds0 + E2_STAGE, vo, true);
+  int SP = 0;
+  for (;;) {
+    const int tn = t + (int)gridDim.x;
+    const bool more = tn < total;
+    int en = e0, in = i0, nrow[2];
+    EfArgs an = a;
+    if (more) corner(tn, an, en, in);
+    // the next tile's stage j lands in the slot that held this tile's stage NST - 2 + j: its E
+    // panel is still there only when that is the same stage (NST == 2), same linear, same i0
+    const bool newB = NST != 2 || !(more && an.Et == a.Et && in == i0);
+    const __amdgpu_buffer_rsrc_t rc = rsrc(a);
+    uint32_t rb[2];
+    ef_rowbase(a, wrow, i0, rb);
+    ef_rows(an, en, nrow);  // 2 loads, issued by every wave whether or not a next tile exists
+    EfAccT<E2_KS> F;
+#pragma unroll
+    for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+      for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
+    u32x4 c[EF_CV];
+    int X[NST];  // DMAs issued after compute s (into the slot it freed)
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      // this stage landed: everything younger than it may still be in flight
+      const int young = s == 0 ? Dn1 + SP + 2 : s == 1 ? SP + 2 + X[0] : X[s - 1];
+      e2_vmcnt(young);
+      asm volatile("s_barrier" ::: "memory");
+      if (s == NST - 1) e2_load<0>(c, rc, rb);  // their latency hides under the last stage
+      EfNoIO nio;
+      F.half(lds0 + (s & 1) * E2_STAGE, nio);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slot
+      uint8_t* slot = smem + (s & 1) * E2_STAGE;
+      const uint32_t slot_lds = lds0 + (s & 1) * E2_STAGE;
+      if (s + 2 < NST) {
+        X[s] = e2_stage(a, e0, i0, s + 2, slot, slot_lds, vo, true);
+      } else if (more) {
+        X[s] = e2_stage(an, en, in, s + 2 - NST, slot, slot_lds, vo, newB);
+        if (s == NST - 1) Dn1 = X[s];
+      } else {
+        X[s] = 0;
+      }
+    }
+    e2_vmcnt(X[NST - 1]);  // column group 0's old values landed
+    e2_sub_store<0>(c, F, rc, rb);
+    if (P) {  // this tile's w-bar partials (the next block's SSR mean, DESIGN.md §3 CHUNK128)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red free (last readers done)
+      ef_wbar_span<0, 16>(wrow, c, red);
+    }
+    e2_load<1>(c, rc, rb);
+    e2_vmcnt(0);
+    e2_sub_store<1>(c, F, rc, rb);
+    if (P) {
+      ef_wbar_span<16, 32>(wrow, c, red);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      ef_wbar_store(a0.n, prsrc(a), true, e0, i0, red);
+    }
+    SP = EF_CV / 2 + P;
+    if (!more) break;
+    t = tn;
+    a = an;
+    e0 = en;
+    i0 = in;
+    wrow[0] = nrow[0];
+    wrow[1] = nrow[1];
+  }
+}
+
 }  // namespace
 
 // Wt[crow[e]][i] -= sum_k Ck[k][e] * Et[k][i] for e < nr, i < ldw (the padding columns of Wt
@@ -590,6 +810,15 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (pt2q_tuning().ef_v2) {  // two workgroups per CU (ef2_gemm_kernel)
+    const int grid2 = std::min(a.ntile * a.nz, 2 * cus);
+    if (bs <= 2 * E2_KS)
+      hipLaunchKernelGGL(ef2_gemm_kernel<2>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
+    else
+      hipLaunchKernelGGL(ef2_gemm_kernel<4>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   const int grid = std::min(a.ntile * a.nz, cus);
   hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes, part_bytes);
   PT2Q_LAUNCH_CHECK();

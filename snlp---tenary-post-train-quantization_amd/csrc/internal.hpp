@@ -26,6 +26,10 @@ inline Grp grp_or_none(const Grp* g) {
 }
 
 // ---- ATQ (atq.hip)
+// per-channel block (b = m > 512) on the caller's row-major W, outputs in place (atq.hip)
+int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, const float* S1, const float* d,
+                            int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
+                            int* counters, hipStream_t st);
 int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
