@@ -96,6 +96,9 @@ def parse(argv=None):
     p.add_argument("--inv-streams", type=int, default=1,
                    help="model workload, grams-first: streams the batched inverse chunks spread over "
                         "(sharding.GramsFirst inv_streams)")
+    p.add_argument("--inv-chunk", type=str, default="32",
+                   help="model workload, grams-first: items per batched-inverse launch sequence, N or "
+                        "m:N,m:N (sharding.GramsFirst chunk)")
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
@@ -109,6 +112,13 @@ def parse(argv=None):
                    help="skip extra.h2d (the transfer-inclusive step: inputs from pinned host memory, "
                         "packed results back to the host)")
     return p.parse_args(argv)
+
+
+def parse_chunk(v):
+    """--inv-chunk: "32" -> 32; "11008:16,4096:32" -> {11008: 16, 4096: 32}."""
+    if ":" not in v:
+        return int(v)
+    return {int(k): int(c) for k, c in (x.split(":") for x in v.split(","))}
 
 
 def resolve(a):
@@ -400,7 +410,7 @@ class ModelStep:
         self.schedule = a.schedule
         self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group,
                                        overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams,
-                                       inv_streams=a.inv_streams)
+                                       inv_streams=a.inv_streams, chunk=parse_chunk(a.inv_chunk))
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.xi = {}  # unit -> which of its width's activation tensors it reads

@@ -372,6 +372,7 @@ class GramsFirst:
         # step 1 batched: the Grams of each (m, N) group in data-parallel launches
         # (pt2q_gram_batched) instead of one stream-K launch per unit
         self.batch_grams, self.pending = batch_grams, {}
+        # chunk: items per batched-inverse launch sequence, an int or {m: items} (others: 32)
         self.batched, self.chunk = batched, chunk
         # step 3 grouped: the block loops of up to `group` same-shape linears (across units) per
         # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
@@ -401,6 +402,11 @@ class GramsFirst:
     @property
     def percdamp(self):
         return self.pipe.percdamp
+
+    def _chunk(self, m: int) -> int:
+        if isinstance(self.chunk, dict):
+            return int(self.chunk.get(m, 32))
+        return int(self.chunk)
 
     def needs_inverse(self, m: int) -> bool:
         return self.engine.needs_inverse(m, self.pipe.bs)
@@ -478,8 +484,8 @@ class GramsFirst:
             jobs = []
             for g in live:
                 c = self.groups[g]["G"].shape[0]
-                jobs += [(float(g[0]) ** 3 * min(self.chunk, c - z0), g, z0, min(self.chunk, c - z0))
-                         for z0 in range(0, c, self.chunk)]
+                ch = self._chunk(g[0])
+                jobs += [(float(g[0]) ** 3 * min(ch, c - z0), g, z0, min(ch, c - z0)) for z0 in range(0, c, ch)]
             jobs.sort(key=lambda j: (-j[0], j[1], j[2]))
             while len(self._istreams) < min(self.inv_streams, len(jobs)):
                 self._istreams.append(torch.cuda.Stream(self.dev))
@@ -502,14 +508,14 @@ class GramsFirst:
             for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
-                                                    info=grp["info"], scratch=self.scratch, chunk=self.chunk)
+                                                    info=grp["info"], scratch=self.scratch, chunk=self._chunk(g[0]))
             return
         self.inv_stream.wait_stream(caller)  # the Grams
         with torch.cuda.stream(self.inv_stream):
             for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
-                                                    info=grp["info"], scratch=self.scratch, chunk=self.chunk)
+                                                    info=grp["info"], scratch=self.scratch, chunk=self._chunk(g[0]))
                 ev = torch.cuda.Event()
                 ev.record(self.inv_stream)
                 self.inv_done[g] = ev
