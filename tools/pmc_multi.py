@@ -53,6 +53,8 @@ def main():
                 out.append(f"lds_insts {c['SQ_INSTS_LDS']:.3g}")
                 if "SQ_LDS_BANK_CONFLICT" in c:
                     out.append(f"lds_conflict_cyc {c['SQ_LDS_BANK_CONFLICT']:.3g}")
+                if c.get("SQ_LDS_IDX_ACTIVE"):
+                    out.append(f"lds_conflict_share {c.get('SQ_LDS_BANK_CONFLICT', 0) / c['SQ_LDS_IDX_ACTIVE']:.3f}")
             print("  " + "  ".join(out))
 
 
