@@ -117,6 +117,8 @@ struct Pt2qTuning {
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
   bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM
   bool ef_v2 = false;          // PT2Q_EF_V2=1: ef2_gemm_kernel (two workgroups per CU)
+  int ef2_stagger = 0;         // PT2Q_EF2_STAGGER: ef2 start de-phasing (0: off)
+  int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
   // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
   // seconds, before they give up and report PT2Q_E_STALL.  PT2Q_DEBUG_SPIN_CAP overrides both

@@ -52,6 +52,9 @@ struct EfArgs {
   int nz;           // linears; the work line is nz * ntile tiles, linear-major
   float* part;      // nullable: w-bar chunk partials part[c][i] of the updated rows, i < n
   int n;
+  int stagger;      // ef2: workgroup w first sleeps (w * 7 % stagger) x 4K cycles (PT2Q_EF2_STAGGER)
+  int probe;        // ef2 development knock-outs (PT2Q_EF2_PROBE, tools only; results garbage):
+                    // 1 = Wt traffic dropped, 2 = operand DMAs from one hot chunk, 4 = no MFMAs
 };
 
 // The arguments of linear z (its workspace slice).
@@ -625,6 +628,16 @@ PT2Q_DEV void e2_voff(const EfArgs& a, E2Vo& v) {
 // lane; returns the DMA instructions issued per wave (8, or 4 without the B panel)
 PT2Q_DEV int e2_stage(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, uint32_t stg_lds, const E2Vo& v,
                       bool withB) {
+  if (a.probe & 2) {  // knock-out: every DMA from the one zero chunk (L2-hot)
+    typedef __attribute__((address_space(3))) void* lptr;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_global_load_lds(&ef_zero16, (lptr)(stg + (wv * 4 + q) * 1024), 16, 0, 0);
+      if (withB) __builtin_amdgcn_global_load_lds(&ef_zero16, (lptr)(stg + E2_PANEL + (wv * 4 + q) * 1024), 16, 0, 0);
+    }
+    return withB ? 8 : 4;
+  }
   const bool fast = (s + 1) * E2_KS <= a.bs && e0 + EF_T <= a.nr && i0 + EF_T <= a.ldw;
   if (!fast) {
 #pragma unroll
@@ -678,7 +691,7 @@ PT2Q_DEV void e2_load(u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const uint32
 }
 
 template <int RN, int KS>
-PT2Q_DEV void e2_sub_store(u32x4 (&c)[EF_CV], const EfAccT<KS>& F, __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2]) {
+PT2Q_DEV void e2_sub(u32x4 (&c)[EF_CV], const EfAccT<KS>& F) {
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
@@ -686,16 +699,24 @@ PT2Q_DEV void e2_sub_store(u32x4 (&c)[EF_CV], const EfAccT<KS>& F, __amdgpu_buff
       const int j = (rm * 2 + RN) * 4 + q;
 #pragma unroll
       for (int u = 0; u < 4; ++u) c[j][u] = __float_as_uint(__uint_as_float(c[j][u]) - F.acc[rm][RN][4 * q + u]);
-      __builtin_amdgcn_raw_buffer_store_b128(c[j], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
     }
+}
+
+template <int RN>
+PT2Q_DEV void e2_store(const u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2]) {
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(c[(rm * 2 + RN) * 4 + q], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
 }
 
 // NST = K stages per tile (2: bs <= 64, 4: bs <= 128; stages past bs are zero chunks: no-op pairs).
 // Issue order per tile, for the hand-counted vmcnt waits: [next rows: 2] [stage s + 2 after each
 // compute s (the last two: the next tile's stages 0 and 1)] with [old values, column group 0: 8]
-// just before the last stage's compute; the epilogue then [waits for group 0] [stores it: 8]
-// [loads group 1: 8] [waits for everything] [stores it: 8] [w-bar partials: P].  So at the next
-// tile's top only that tile's last stores (SP) may still be in flight beside its stages.
+// just before the last stage's compute; the epilogue then [waits for group 0] [loads group 1: 8]
+// [stores group 0: 8] [waits for group 1] [stores it: 8] [w-bar partials: P].  So at the next
+// tile's top only that tile's stores (SP) may still be in flight beside its stages.
 template <int NST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void ef2_gemm_kernel(
     EfArgs a0, long wt_bytes, long part_bytes) {
@@ -722,6 +743,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   ef_rows(a, e0, wrow);
   E2Vo vo;
   e2_voff(a0, vo);
+  if (a0.stagger > 1)  // de-phase the workgroups: identical tiles keep them in lock step otherwise,
+    for (int z = (int)((blockIdx.x * 7u) % (unsigned)a0.stagger); z > 0; --z)  // bursting memory at once
+      __builtin_amdgcn_s_sleep(64);
   e2_stage(a, e0, i0, 0, smem, lds0, vo, true);
   int Dn1 = e2_stage(a, e0, i0, 1, smem + E2_STAGE, lds0 + E2_STAGE, vo, true);
   int SP = 0;
@@ -737,6 +761,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const __amdgpu_buffer_rsrc_t rc = rsrc(a);
     uint32_t rb[2];
     ef_rowbase(a, wrow, i0, rb);
+    if (a0.probe & 1) rb[0] = rb[1] = EF_DROP;
     ef_rows(an, en, nrow);  // 2 loads, issued by every wave whether or not a next tile exists
     EfAccT<E2_KS> F;
 #pragma unroll
@@ -753,7 +778,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       asm volatile("s_barrier" ::: "memory");
       if (s == NST - 1) e2_load<0>(c, rc, rb);  // their latency hides under the last stage
       EfNoIO nio;
-      F.half(lds0 + (s & 1) * E2_STAGE, nio);
+      if (!(a0.probe & 4)) F.half(lds0 + (s & 1) * E2_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slot
       uint8_t* slot = smem + (s & 1) * E2_STAGE;
       const uint32_t slot_lds = lds0 + (s & 1) * E2_STAGE;
@@ -767,20 +792,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
     e2_vmcnt(X[NST - 1]);  // column group 0's old values landed
-    e2_sub_store<0>(c, F, rc, rb);
+    e2_sub<0>(c, F);
+    e2_load<1>(c, rc, rb);  // before group 0's stores: waiting for it then leaves those in flight
+    e2_store<0>(c, rc, rb);
     if (P) {  // this tile's w-bar partials (the next block's SSR mean, DESIGN.md §3 CHUNK128)
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red free (last readers done)
       ef_wbar_span<0, 16>(wrow, c, red);
     }
-    e2_load<1>(c, rc, rb);
-    e2_vmcnt(0);
-    e2_sub_store<1>(c, F, rc, rb);
+    e2_vmcnt(EF_CV / 2);  // group 1 landed (younger: group 0's stores)
+    e2_sub<1>(c, F);
+    e2_store<1>(c, rc, rb);
     if (P) {
       ef_wbar_span<16, 32>(wrow, c, red);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       ef_wbar_store(a0.n, prsrc(a), true, e0, i0, red);
     }
-    SP = EF_CV / 2 + P;
+    SP = EF_CV + P;
     if (!more) break;
     t = tn;
     a = an;
@@ -806,7 +833,7 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   if (part && (n <= 0 || n % 4 || n > ldw || (uintptr_t)part % 16 || part_bytes >= (long)EF_DROP))
     return PT2Q_E_UNSUPPORTED;
   EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1,
-           grp ? grp->ws : 0l, (int)grp_z(grp), part, n};
+           grp ? grp->ws : 0l, (int)grp_z(grp), part, n, pt2q_tuning().ef2_stagger, pt2q_tuning().ef2_probe};
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
