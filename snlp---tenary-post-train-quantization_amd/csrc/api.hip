@@ -41,7 +41,7 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);
   geti("PT2Q_WIDE_WAVES", t.wide_waves);
-  getb("PT2Q_EF_V2", t.ef_v2);
+  geti("PT2Q_EF_V2", t.ef_v2);
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   if (t.wide_waves != 8) t.wide_waves = 4;
