@@ -818,282 +818,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-// ---- ef3_gemm_kernel: warp-specialised (one workgroup of 8 waves per CU) --------------------
-// ef_gemm_kernel / ef2_gemm_kernel run every wave through the same phases, so a tile's memory work
-// (operand staging, the Wt read-modify-write, the w-bar partials) and its MFMAs overlap only in
-// part: knock-outs of ef2 put memory alone at ~8.5 ms and MFMA alone at ~7.1 ms of a 13.3 ms
-// 16-linear 4096^2 loop.  Here the roles are split across the waves of ONE
-// workgroup (two waves per SIMD):
-//   waves 0-3  (C): the 64 x 64 accumulators of the 128 x 128 tile (as ef_gemm_kernel): LDS reads
-//                   and MFMAs only; each tile's results go to an LDS result buffer;
-//   waves 4, 5 (D): LDS-DMA of the A (coefficient) / B (error) panels into a ring of E3_S slots of
-//                   16 k rows, up to E3_S stages ahead of the C waves;
-//   waves 6, 7 (R): rows [64r, 64r + 64) of every tile: load the old Wt values (the next column
-//                   groups while the current one is processed), subtract the results read back
-//                   from LDS, store, and form the w-bar partials; wave 6 adds the two row halves.
-// Roles hand off through monotonic LDS counters (filled / consumed per stage, results written /
-// read per tile), polled with s_sleep; nothing waits on a barrier after the prologue.  The MFMA
-// chain (k-ascending pairs into the same accumulators), the one subtraction and the CHUNK128
-// w-bar tree are those of ef_gemm_kernel: bit-identical.
-constexpr int E3_KS = 16;                          // k rows per stage (8 k-pairs)
-constexpr int E3_PANEL = E3_KS * EF_ROWB;          // 8 KiB
-constexpr int E3_SLOT = 2 * E3_PANEL;              // A + B: 16 KiB
-constexpr int E3_S = 4;                            // ring slots
-constexpr int E3_RS = EF_T + 4;                    // result buffer row stride (floats; 2-way conflicts)
-constexpr int E3_RES = EF_T * E3_RS * 4;           // 67,584 B
-constexpr int E3_RED = 2 * 256 + 128;              // w-bar sums: two tile buffers + per-lane spare slots
-enum : int { E3_FA = 0, E3_FB = 1, E3_CONS = 2, E3_RDONE = 6, E3_RFREE = 10, E3_WREADY = 12, E3_WDONE = 14,
-             E3_NFLAG = 16 };
-constexpr int E3_LDS = E3_S * E3_SLOT + E3_RES + E3_RED * 4 + E3_NFLAG * 4;
-
-PT2Q_DEV int e3_ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-PT2Q_DEV void e3_st(int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-// wait (one wave) until min(p[0..n)) >= v.  Bounded: a legitimate wait is one tile (~10 us); after
-// ~2^24 polls (~0.5 s) the wave gives up rather than hang the device (the results are then wrong,
-// which every parity test catches).
-PT2Q_DEV void e3_wait_min(const int* p, int n, int v) {
-  for (int spin = 0; spin < (1 << 24); ++spin) {
-    int m = e3_ld(p);
-    for (int j = 1; j < n; ++j) m = min(m, e3_ld(p + j));
-    if (m >= v) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");
-}
-
-PT2Q_DEV void e3_corner(const EfArgs& a0, int t, EfArgs& a, int& e0, int& i0) {
-  const int z = t / a0.ntile, tl = t - z * a0.ntile;
-  a = ef_linear(a0, z);
-  e0 = (tl / a0.ti) * EF_T;
-  i0 = (tl % a0.ti) * EF_T;
-}
-
-// --- D waves: panel P (0: A = C[k][e0..], 1: B = E[k][i0..]) of stage s of a tile into slot `dst`
-PT2Q_DEV void e3_dma(const EfArgs& a, int P, int e0, int i0, int s, uint8_t* dst, uint32_t dst_lds,
-                     const uint32_t (&vo)[8]) {
-  const int lane = threadIdx.x & 63;
-  const long ld = P ? a.ldw : a.ldk;
-  const float* base = P ? a.Et : a.Ck;
-  const int c0 = P ? i0 : e0, lim = P ? (int)a.ldw : a.nr;
-  const bool fast = (s + 1) * E3_KS <= a.bs && c0 + EF_T <= lim;
-  if (fast) {
-    const char* sb = (const char*)(base + (long)s * E3_KS * ld + c0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) ef_dma_asm(sb, vo[q], dst_lds + q * 1024);
-    return;
-  }
-  typedef __attribute__((address_space(3))) void* lptr;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int k = s * E3_KS + 2 * q + (lane >> 5), c = c0 + 4 * (lane & 31);
-    const void* src = k < a.bs ? (const void*)(base + (c < lim ? (long)k * ld + c : 0)) : (const void*)&ef_zero16;
-    __builtin_amdgcn_global_load_lds(src, (lptr)(dst + q * 1024), 16, 0, 0);
-  }
-}
-
-template <int NST>
-PT2Q_DEV void e3_dma_wave(const EfArgs& a0, int P, uint8_t* smem, uint32_t lds0, int* fl) {
-  const int lane = threadIdx.x & 63, total = a0.ntile * a0.nz;
-  const long ld = P ? a0.ldw : a0.ldk;
-  uint32_t vo[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) vo[q] = (uint32_t)(((long)(2 * q + (lane >> 5)) * ld + 4 * (lane & 31)) * 4);
-  int g = 0;
-  for (int t = blockIdx.x; t < total; t += gridDim.x) {
-    EfArgs a;
-    int e0, i0;
-    e3_corner(a0, t, a, e0, i0);
-#pragma unroll
-    for (int s = 0; s < NST; ++s, ++g) {
-      if (g >= E3_S) e3_wait_min(fl + E3_CONS, 4, g - E3_S + 1);  // the slot's previous stage consumed
-      const int off = (g % E3_S) * E3_SLOT + P * E3_PANEL;
-      e3_dma(a, P, e0, i0, s, smem + off, lds0 + off, vo);
-      if (g >= E3_S - 1) {  // stage g - (E3_S - 1) landed: 8 DMAs per younger stage may be in flight
-        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        e3_st(fl + P, g - E3_S + 2);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  e3_st(fl + P, g);
-}
-
-// --- C waves
-template <int NST>
-PT2Q_DEV void e3_mfma_wave(const EfArgs& a0, uint32_t lds0, float* res, int* fl) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, total = a0.ntile * a0.nz;
-  const int wr = w >> 1, wc = w & 1, li = lane & 31, h = lane >> 5;
-  int g = 0, seq = 0;
-  for (int t = blockIdx.x; t < total; t += gridDim.x, ++seq) {
-    EfAccT<E3_KS> F;
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < 2; ++rn) F.acc[rm][rn] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < NST; ++s, ++g) {
-      e3_wait_min(fl + E3_FA, 2, g + 1);  // both panels of stage g landed
-      EfNoIO nio;
-      if (!(a0.probe & 4)) F.half(lds0 + (g % E3_S) * E3_SLOT, nio);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the slot returned
-      e3_st(fl + E3_CONS + w, g + 1);
-    }
-    e3_wait_min(fl + E3_RFREE, 2, seq);  // the previous tile's results were read out
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int rn = 0; rn < 2; ++rn)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = wr * 64 + rm * 32 + li, col = wc * 64 + rn * 32 + 8 * q + 4 * h;
-          f32x4 v;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = F.acc[rm][rn][4 * q + u];
-          *(f32x4*)(res + e * E3_RS + col) = v;
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    e3_st(fl + E3_RDONE + w, seq + 1);
-  }
-}
-
-// --- R waves: row half r of every tile
-template <int G>  // column group G = wc * 2 + rn: c[rm * 4 + q] <- old values of rows (li, li + 32)
-PT2Q_DEV void e3_load(u32x4 (&c)[8], __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2][2]) {
-  constexpr int wc = G >> 1, rn = G & 1;
-#pragma unroll
-  for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      c[rm * 4 + q] = __builtin_amdgcn_raw_buffer_load_b128(rc, rb[rm][wc] + 4 * (32 * rn + 8 * q), 0, 0);
-}
-
-template <int G>
-PT2Q_DEV void e3_rmw(u32x4 (&c)[8], __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2][2], const float* res,
-                     int r, const int (&wrow)[2], float* red) {
-  constexpr int wc = G >> 1, rn = G & 1;
-  const int lane = threadIdx.x & 63, li = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = r * 64 + rm * 32 + li, col = wc * 64 + rn * 32 + 8 * q + 4 * h;
-      const f32x4 v = *(const f32x4*)(res + e * E3_RS + col);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) c[rm * 4 + q][u] = __float_as_uint(__uint_as_float(c[rm * 4 + q][u]) - v[u]);
-    }
-#pragma unroll
-  for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(c[rm * 4 + q], rc, rb[rm][wc] + 4 * (32 * rn + 8 * q), 0, 0);
-  if (!red) return;
-  // w-bar of the group's 16 columns (q, u): rows li + li+32 in the lane, bfly16, row_bcast:15 --
-  // ef_wbar_step's tree; lanes 16 / 48 hold the 64-row sum of column (wc, rn, q, h, u)
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float v0 = wrow[0] >= 0 ? __uint_as_float(c[q][u]) : 0.0f;
-      const float v1 = wrow[1] >= 0 ? __uint_as_float(c[4 + q][u]) : 0.0f;
-      float x = bfly16(v0 + v1);
-      x = x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));
-      const bool sel = (lane & 31) == 16;
-      red[sel ? r * 128 + wc * 64 + h * 32 + rn * 16 + q * 4 + u : 512 + r * 64 + lane] = x;
-    }
-}
-
-template <int NST>
-PT2Q_DEV void e3_rmw_wave(const EfArgs& a0, long wt_bytes, long part_bytes, const float* res, float* red, int* fl) {
-  const int lane = threadIdx.x & 63, r = (threadIdx.x >> 6) - 6, total = a0.ntile * a0.nz;
-  const int li = lane & 31, h = lane >> 5;
-  const bool P = a0.part != nullptr;
-  auto rows = [&](const EfArgs& a, int e0, int (&wr_)[2]) {
-    int v[2];
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm) {
-      const int e = e0 + r * 64 + rm * 32 + li;
-      v[rm] = a.crow[e < a.nr ? e : 0];
-    }
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm) wr_[rm] = e0 + r * 64 + rm * 32 + li < a.nr ? v[rm] : -1;
-  };
-  int t = blockIdx.x, seq = 0;
-  if (t >= total) return;
-  EfArgs a;
-  int e0, i0, wrow[2];
-  e3_corner(a0, t, a, e0, i0);
-  rows(a, e0, wrow);
-  for (; t < total; t += gridDim.x, ++seq) {
-    const int tn = t + (int)gridDim.x;
-    EfArgs an = a;
-    int en = e0, in = i0, nrow[2];
-    if (tn < total) e3_corner(a0, tn, an, en, in);
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.Wt, 0, (int)wt_bytes, 0x00020000);
-    uint32_t rb[2][2];
-#pragma unroll
-    for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-      for (int wc = 0; wc < 2; ++wc)
-        rb[rm][wc] = (wrow[rm] < 0 || i0 + wc * 64 >= a.ldw || (a0.probe & 1))
-                         ? EF_DROP
-                         : (uint32_t)(((long)wrow[rm] * a.ldw + i0 + wc * 64 + 4 * h) * 4);
-    u32x4 c0[8], c1[8];
-    e3_load<0>(c0, rc, rb);
-    e3_load<1>(c1, rc, rb);
-    rows(an, en, nrow);  // the next tile's rows, under this tile's work
-    float* rd = red + (seq & 1) * 256;
-    if (P && r == 1 && seq >= 2) e3_wait_min(fl + E3_WDONE, 1, seq - 1);  // wave 6 added this buffer's last sums
-    e3_wait_min(fl + E3_RDONE, 4, seq + 1);  // the tile's results are in LDS
-    float* rdp = P ? rd : nullptr;
-    e3_rmw<0>(c0, rc, rb, res, r, wrow, rdp);
-    e3_load<2>(c0, rc, rb);
-    e3_rmw<1>(c1, rc, rb, res, r, wrow, rdp);
-    e3_load<3>(c1, rc, rb);
-    e3_rmw<2>(c0, rc, rb, res, r, wrow, rdp);
-    e3_rmw<3>(c1, rc, rb, res, r, wrow, rdp);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every result read (and w-bar sum written)
-    e3_st(fl + E3_RFREE + r, seq + 1);
-    if (P) {
-      e3_st(fl + E3_WREADY + r, seq + 1);
-      if (r == 0) {  // part[c][i] = X + Y (the two row halves' sums), 128 columns, lanes 0..31
-        e3_wait_min(fl + E3_WREADY + 1, 1, seq + 1);
-        const int wc = li >> 4, hh = (li >> 3) & 1, rn = (li >> 2) & 1, q = li & 3;
-        const f32x4 x = *(const f32x4*)(rd + wc * 64 + hh * 32 + rn * 16 + q * 4);
-        const f32x4 y = *(const f32x4*)(rd + 128 + wc * 64 + hh * 32 + rn * 16 + q * 4);
-        const int i = i0 + wc * 64 + rn * 32 + 8 * q + 4 * hh;
-        const f32x4 o = x + y;
-        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(a.part, 0, (int)part_bytes, 0x00020000);
-        const unsigned off = (h == 0 && i < a0.n) ? (unsigned)(((long)(e0 / EF_T) * a0.n + i) * 4) : EF_DROP;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rp, off, 0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        e3_st(fl + E3_WDONE, seq + 1);
-      }
-    }
-    a = an;
-    e0 = en;
-    i0 = in;
-    wrow[0] = nrow[0];
-    wrow[1] = nrow[1];
-  }
-}
-
-template <int NST>
-__global__ __launch_bounds__(512) void ef3_gemm_kernel(EfArgs a0, long wt_bytes, long part_bytes) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[E3_LDS];
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
-  float* res = (float*)(smem + E3_S * E3_SLOT);
-  float* red = res + EF_T * E3_RS;
-  int* fl = (int*)(red + E3_RED);
-  if ((int)blockIdx.x >= a0.ntile * a0.nz) return;
-  if (threadIdx.x < E3_NFLAG) fl[threadIdx.x] = 0;
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w < 4) e3_mfma_wave<NST>(a0, lds0, res, fl);
-  else if (w < 6) e3_dma_wave<NST>(a0, w - 4, smem, lds0, fl);
-  else e3_rmw_wave<NST>(a0, wt_bytes, part_bytes, res, red, fl);
-}
-
 }  // namespace
 
 // Wt[crow[e]][i] -= sum_k Ck[k][e] * Et[k][i] for e < nr, i < ldw (the padding columns of Wt
@@ -1113,15 +837,6 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (pt2q_tuning().ef_v2 == 2) {  // warp-specialised, one workgroup of 8 waves per CU (ef3_gemm_kernel)
-    const int grid3 = std::min(a.ntile * a.nz, cus);
-    if (bs <= 4 * E3_KS)
-      hipLaunchKernelGGL(ef3_gemm_kernel<4>, dim3(grid3), dim3(512), 0, st, a, wt_bytes, part_bytes);
-    else
-      hipLaunchKernelGGL(ef3_gemm_kernel<8>, dim3(grid3), dim3(512), 0, st, a, wt_bytes, part_bytes);
-    PT2Q_LAUNCH_CHECK();
-    return PT2Q_OK;
-  }
   if (pt2q_tuning().ef_v2 == 1) {  // two workgroups per CU (ef2_gemm_kernel)
     const int grid2 = std::min(a.ntile * a.nz, 2 * cus);
     if (bs <= 2 * E2_KS)

@@ -3,7 +3,7 @@
 # block loop (16 fp16 4096 x 4096 linears, kern_workloads group) per PT2Q_EF2_PROBE mask
 # (1 = no Wt traffic, 2 = operand DMAs from one hot chunk, 4 = no MFMAs; results garbage), and
 # ef_gemm_kernel for reference.   bash tools/ef2_knock.sh TAG [mask ...]
-# masks: N (ef2 knock-out N), sN (ef2, stagger N), e3[N] (ef3 [knock-out N]), nV (PT2Q_EF_V2=V, no w-bar)
+# masks: N (ef2 knock-out N), sN (ef2, stagger N), nV (PT2Q_EF_V2=V, no w-bar)
 set -o pipefail
 TAG=${1:-ef2k}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,7 +14,6 @@ for M in v1 ${@:-0 1 2 4 3 7}; do
   # M: a knock-out mask, or sN = no knock-out with PT2Q_EF2_STAGGER=N
   export PT2Q_EF2_STAGGER=0 PT2Q_EF_WBAR=1
   if [ "$M" = v1 ]; then export PT2Q_EF_V2=0 PT2Q_EF2_PROBE=0;
-  elif [ "${M:0:2}" = e3 ]; then export PT2Q_EF_V2=2 PT2Q_EF2_PROBE=${M:2}; [ -z "${M:2}" ] && export PT2Q_EF2_PROBE=0;
   elif [ "${M:0:1}" = n ]; then export PT2Q_EF_V2=${M:1} PT2Q_EF2_PROBE=0 PT2Q_EF_WBAR=0;
   elif [ "${M:0:1}" = s ]; then export PT2Q_EF_V2=1 PT2Q_EF2_PROBE=0 PT2Q_EF2_STAGGER=${M:1};
   else export PT2Q_EF_V2=1 PT2Q_EF2_PROBE=$M; fi
