@@ -16,7 +16,7 @@ timeout -k 10 500 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || exit
 python3 -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline']['value'], d['roofline']['stages']['step'])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/bench_trace -o run --output-format csv -- \
-  python3 $R/bench.py --no-cpu-baseline --no-configs > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit 1
+  python3 $R/bench.py --no-cpu-baseline --no-configs --no-h2d > $OUT/bench_prof.json 2> $OUT/bench_prof.err || exit 1
 f=$(find $OUT/bench_trace -name "*kernel_trace.csv" | head -1)
 python3 $R/tools/kstats.py $f > $OUT/bench_kstats.txt 2>&1 && head -30 $OUT/bench_kstats.txt
 gzip -f $f
