@@ -117,3 +117,47 @@ def test_reference_surface_fails_loudly_without_gpu(pt2q):
         pt2q.AsymmetricTernaryQuantizer().quantize(torch.zeros(4, 128))
     with pytest.raises(pt2q._lib.Pt2qError):
         pt2q.select_next_block_ssr(torch.zeros(4, 300), torch.arange(300), 128)
+
+
+def test_group_support_query_and_block_workspace(pt2q):
+    """pt2q_quantize_blocks_group_supported restates every E_UNSUPPORTED condition of the grouped
+    entry (host only), and engine.group_supported asks it rather than restating them."""
+    lib = pt2q._lib.lib()
+    ACT, SSR, HESS = pt2q._lib.AGA_ACT, pt2q._lib.FLAG_SSR, pt2q._lib.AGA_HESS
+    ok = lib.pt2q_quantize_blocks_group_supported
+    assert ok(4096, 4096, 128, SSR | ACT) == 1
+    assert ok(11008, 4096, 128, SSR | ACT) == 1 and ok(4096, 11008, 128, SSR | ACT) == 1
+    assert ok(4096, 4096, 256, SSR | ACT) == 0       # blocks > 128 columns
+    assert ok(4096, 128, 128, SSR | ACT) == 0        # one block: no error feedback to group
+    assert ok(4096, 4096, 128, SSR | HESS) == 0      # variant G (H_bb AGA) per linear
+    assert ok(4098, 4096, 128, SSR | ACT) == 0       # n % 4
+    assert ok(4096, 4098, 128, SSR | ACT) == 0       # m % 4: EF coefficient rows 16-byte aligned
+    assert ok(16384, 40000, 128, SSR | ACT) == 0     # Wt >= 2 GiB: past the EF buffer range
+    assert pt2q.engine.group_supported(4096, 4096, 128) and not pt2q.engine.group_supported(4096, 4098, 128)
+    # the per-linear block loop's own workspace: status word + loop buffers, far below the
+    # layer figure (which adds the Gram, Hessian, inverse and their scratch)
+    n, m = 5120, 13824
+    b = lib.pt2q_blocks_workspace_bytes(n, m, 1 << 14, SSR | ACT)
+    assert pt2q._lib.STATUS_BYTES + m * 5120 * 5 < b < lib.pt2q_layer_workspace_bytes(n, m, 1 << 14, SSR | ACT)
+    assert lib.pt2q_blocks_workspace_bytes(0, m, 128, 0) == 0
+
+
+def test_stage_timing_host_side(pt2q):
+    """pt2q_stage_timing with no bracketed launches: enabling clears the log, reading sums
+    nothing and makes no device call (so it runs here without a GPU)."""
+    lib = pt2q._lib
+    lib.stage_timing(True)
+    lib.stage_timing(False)
+    t = lib.stage_timing_read()
+    assert t["records"] == 0 and all(t[k] == 0.0 for k in lib.TIMERS)
+    assert lib.TIMERS.index("ef") == 3 and lib.TIMERS.index("inverse") == 6  # PT2Q_TIMER_* order
+
+
+def test_quantize_blocks_hinv_optional_only_per_channel(pt2q):
+    """Hinv may be NULL only for one block (b >= m: nothing reads it); with several blocks the
+    call is refused before any device work (fake non-null pointers are never touched)."""
+    lib = pt2q._lib.lib()
+    p = ctypes.c_void_p(4096)
+    E_ARG, I8 = 1, 3
+    assert lib.pt2q_quantize_blocks(p, 0, 64, 16, 64, 32, 0x11, p, 64, None, 64, 100, p, p, p, I8, p,
+                                    None, p, 1 << 30, None) == E_ARG

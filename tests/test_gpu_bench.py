@@ -1,0 +1,49 @@
+"""bench.py's measured paths on a small model (GPU): the transfer-inclusive step (extra.h2d,
+bench.H2DStep: inputs from pinned host memory, packed results back to pinned host memory) must
+produce exactly the resident step's results, and the live stage timing must bracket every stage
+of the step it measures."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_step():
+    import bench
+    a = bench.parse(["--model", "llama-2-7b", "--layers", "2", "--hidden", "512", "--inter", "768",
+                     "--tokens", "2048", "--no-cpu-baseline"])
+    bench._load_runtime(False)
+    bench.resolve(a)
+    return bench, bench.ModelStep(a, 0, 1, torch.device("cuda", 0), torch.float16)
+
+
+def test_h2d_step_equals_resident_step():
+    bench, ms = _small_step()
+    want = ms.step()  # {unit.linear: {T2, alpha, mu, perm, shape}} on the device
+    h = bench.H2DStep(ms)
+    manifest = h.step()
+    got = bench.sharding._unflatten(manifest, h.host_res[:h.d2h_bytes])
+    assert sorted(got) == sorted(want) and len(got) == 14
+    for k, r in want.items():
+        for f in ("T2", "alpha", "mu", "perm"):
+            assert torch.equal(got[k][f], r[f].cpu()), (k, f)
+    assert h.h2d_bytes > 0 and got[next(iter(got))]["T2"].device.type == "cpu"
+
+
+def test_stage_busy_brackets_every_stage():
+    bench, ms = _small_step()
+    ms.step()
+    busy = ms.stage_busy()
+    for k in ("gram", "inverse", "ssr", "atq", "ef", "setup", "out"):
+        assert busy[k] > 0, (k, busy)
+    assert busy["records"] > 0
+    # one lane: the busy times of the tail phase fit inside its wall
+    tails = sum(busy[k] for k in ("setup", "ssr", "atq", "ef", "out"))
+    assert tails <= busy["phase_wall_ms"]["tails"] * 1.02 + 0.5
+    assert len(ms.gf.pipe.lanes) == 3  # restored after the one-lane measurement
