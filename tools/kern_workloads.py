@@ -2,7 +2,8 @@
 python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT} [reps]
 inverse: engine.hessian_inverse_batched on BATCH synthetic Grams of order M (N = 262144 scale);
 group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M);
-grams:   engine.gram_batched over COUNT Grams of one resident fp16 N x M activation (as the bench)."""
+grams:   engine.gram_batched over COUNT Grams of DISTINCT (env, default 4) resident fp16 N x M
+         activations rotated over the items (as the bench)."""
 import os
 import sys
 import torch
@@ -21,11 +22,13 @@ if kind == "inverse":
     torch.cuda.synchronize()
     print("inverse done", int(info.max()))
 elif kind == "grams":
+    # DISTINCT (env, default 4) activation tensors rotated over the items, as bench.py's step
     n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
-    X = pt2q.fill_synthetic((n, m), 79, outliers=True).half()
-    G = torch.empty(count, m, m, device=X.device)
+    nd = int(os.environ.get("DISTINCT", "4"))
+    Xs = [pt2q.fill_synthetic((n, m), 79 + 7919 * k, outliers=True).half() for k in range(nd)]
+    G = torch.empty(count, m, m, device=Xs[0].device)
     for _ in range(reps):
-        pt2q.engine.gram_batched([X] * count, G)
+        pt2q.engine.gram_batched([Xs[z % nd] for z in range(count)], G)
     torch.cuda.synchronize()
     print("grams done", float(G[0, 0, 0]))
 else:
