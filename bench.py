@@ -59,6 +59,9 @@ def parse(argv=None):
                         "them itself; default: WORLD_SIZE or 1")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU plumbing check: gloo ranks, stub units (no GPU, no libpt2q)")
+    p.add_argument("--share-gpu", action="store_true",
+                   help="TESTING ONLY: every rank on cuda:0 with the gloo backend (the real kernels and the "
+                        "sharded step's gather on a one-GPU box; not a scaling measurement)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--workload", choices=["model", "layer", "split"], default="model",
@@ -446,6 +449,7 @@ class ModelStep:
         gf = self.gf if self.schedule == "grams-first" and self.pipe is not None else None
         res, _ = sharding.quantize_units_sharded(self.units, self.provider, run_unit=self.run_unit,
                                                  pack=True, dst=0, grams_first=gf)
+        self.gathered = None if res is None else len(res)  # linears whose results reached rank 0
         return res
 
     def phase_step(self):
@@ -823,14 +827,19 @@ def main(argv=None):
         if world > 1:
             dist.init_process_group("gloo")
     else:
-        if world > torch.cuda.device_count():
+        if a.share_gpu:
+            local = 0
+        elif world > torch.cuda.device_count():
             print(f"[bench] refusing: {world} ranks but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
             return 2
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         sync = torch.cuda.synchronize
         if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
+            if a.share_gpu:
+                dist.init_process_group("gloo")  # RCCL refuses two ranks on one device
+            else:
+                dist.init_process_group("nccl", device_id=dev)
     if world > 1:
         world, rank = dist.get_world_size(), dist.get_rank()
     io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[a.io_dtype]
@@ -1029,7 +1038,8 @@ def main(argv=None):
                        "block_size": bs,
                        "parallelism": ({"model": f"LPT unit sharding x{world}", "layer": f"layer per rank x{world}",
                                         "split": f"Gram rows x{world}, rank-ordered fold on rank 0"}[a.workload])
-                                  + (", rccl gather" if world > 1 else "")
+                                  + ((", gloo gather, TEST ONLY: every rank shares cuda:0" if a.share_gpu else
+                                      ", rccl gather") if world > 1 else "")
                                   + ((f", every Gram first then the tails on {a.lanes} unit lanes"
                                       if a.schedule == "grams-first" else
                                       f", {a.lanes} unit lanes (Grams chained, tails overlapped)")
@@ -1038,6 +1048,7 @@ def main(argv=None):
         if a.workload == "model":
             res["s_model"] = ms_per_step / 1e3
             res["ranks"] = ranks
+            res["gathered_linears"] = getattr(work, "gathered", None)
         if roof is not None:
             res["roofline"] = roof
         if (a.workload == "model" and world == 1 and not a.no_extra and not a.no_h2d and work.gf is not None

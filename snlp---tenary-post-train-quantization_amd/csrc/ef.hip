@@ -52,7 +52,7 @@ struct EfArgs {
   int nz;           // linears; the work line is nz * ntile tiles, linear-major
   float* part;      // nullable: w-bar chunk partials part[c][i] of the updated rows, i < n
   int n;
-  int stagger;      // ef2: workgroup w first sleeps (w * 7 % stagger) x 4K cycles (PT2Q_EF2_STAGGER)
+  int stagger;      // ef2: the grid's second half first sleeps stagger x 4K cycles (PT2Q_EF2_STAGGER)
   int probe;        // ef2 development knock-outs (PT2Q_EF2_PROBE, tools only; results garbage):
                     // 1 = Wt traffic dropped, 2 = operand DMAs from one hot chunk, 4 = no MFMAs
 };
@@ -743,9 +743,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   ef_rows(a, e0, wrow);
   E2Vo vo;
   e2_voff(a0, vo);
-  if (a0.stagger > 1)  // de-phase the workgroups: identical tiles keep them in lock step otherwise,
-    for (int z = (int)((blockIdx.x * 7u) % (unsigned)a0.stagger); z > 0; --z)  // bursting memory at once
-      __builtin_amdgcn_s_sleep(64);
+  // de-phase the two workgroups of a CU (the second half of the grid lands on CUs already holding
+  // one): identical tiles would keep them in lock step, both in their MFMA stages or both in their
+  // epilogues at once (PT2Q_EF2_STAGGER = sleeps of ~4K cycles; development knob)
+  if (a0.stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
+    for (int z = a0.stagger; z > 0; --z) __builtin_amdgcn_s_sleep(64);
   e2_stage(a, e0, i0, 0, smem, lds0, vo, true);
   int Dn1 = e2_stage(a, e0, i0, 1, smem + E2_STAGE, lds0 + E2_STAGE, vo, true);
   int SP = 0;

@@ -176,9 +176,10 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
         return _unflatten(manifest, flat)
     manifests = [None] * world if rank == dst else None
     dist.gather_object(manifest, manifests, dst=dst, group=group)
+    host = dist.get_backend(group) == "gloo"  # gloo moves host memory only: device bytes go via the CPU
     if rank != dst:
         if flat.numel():
-            dist.send(flat, dst=dst, group=group)
+            dist.send(flat.cpu() if host else flat, dst=dst, group=group)
         return None
     merged = _unflatten(manifest, flat)
     dev = device
@@ -195,13 +196,13 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
             continue
         nbytes = sum(e[4] for e in manifests[r])
         if nbytes:
-            bufs[r] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            bufs[r] = torch.empty(nbytes, dtype=torch.uint8, device="cpu" if host else dev)
             ops.append(dist.P2POp(dist.irecv, bufs[r], r, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     for r, buf in bufs.items():
-        merged.update(_unflatten(manifests[r], buf))
+        merged.update(_unflatten(manifests[r], buf.to(dev) if host else buf))
     return merged
 
 
