@@ -44,6 +44,8 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_EF_V2", t.ef_v2);
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
+  geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
+  if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;
   if (t.wide_waves != 8) t.wide_waves = 4;
   if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
     const long c = std::atol(e);

@@ -840,7 +840,9 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (pt2q_tuning().ef_v2 == 1) {  // two workgroups per CU (ef2_gemm_kernel)
-    const int grid2 = std::min(a.ntile * a.nz, 2 * cus);
+    // workgroups per CU (PT2Q_EF2_PER_CU, 1 or 2): with one, another lane's latency-bound
+    // kernels (SSR, ATQ) find registers and LDS beside the error feedback on every CU
+    const int grid2 = std::min(a.ntile * a.nz, pt2q_tuning().ef2_per_cu * cus);
     if (bs <= 2 * E2_KS)
       hipLaunchKernelGGL(ef2_gemm_kernel<2>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
     else
