@@ -24,6 +24,7 @@ Pt2qTuning load_tuning() {
   };
   geti("PT2Q_GRAM_SUPER", t.gram_super);
   geti("PT2Q_GRAM_GROUPS", t.gram_groups);
+  geti("PT2Q_GRAM_CUS", t.gram_cus);
   getb("PT2Q_GRAM_STREAMK", t.gram_split);
   getb("PT2Q_GRAM_PAIR", t.gram_pair);
   getb("PT2Q_GRAM_DP", t.gram_dp);

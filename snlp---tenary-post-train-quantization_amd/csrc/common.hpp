@@ -98,6 +98,7 @@ static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 struct Pt2qTuning {
   int gram_super = 0;          // PT2Q_GRAM_SUPER: 16-bit Gram super-block side (0: by m)
   int gram_groups = 8;         // PT2Q_GRAM_GROUPS: XCD groups of the 16-bit Gram split
+  int gram_cus = 0;            // PT2Q_GRAM_CUS: CUs the batched Gram may hold (0: all)
   bool gram_split = true;      // PT2Q_GRAM_STREAMK=0: one chain per tile, no split
   bool gram_pair = true;       // PT2Q_GRAM_PAIR=0: no tile-pair teams
   bool gram_dp = true;         // PT2Q_GRAM_DP=0: no data-parallel waves

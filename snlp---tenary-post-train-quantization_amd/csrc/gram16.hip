@@ -926,7 +926,9 @@ int pt2q_launch_gram16_batched(const void* const* X, int dtype, long N, int m, l
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   b.NG = std::max(1, tu.gram_groups);
-  b.R = std::max(1, cus / b.NG);
+  // PT2Q_GRAM_CUS (development knob): CUs the batched Gram may hold (one workgroup each)
+  const int use = tu.gram_cus > 0 ? std::min(tu.gram_cus, cus) : cus;
+  b.R = std::max(1, use / b.NG);
   const long grid = std::min<long>(b.total, (long)b.NG * b.R);
   if (grid < (long)b.NG * b.R) {  // fewer tiles than workgroups: one tile each, no team order
     b.NG = 1;
