@@ -62,6 +62,7 @@ def lib():
             "orc_rowsum_seq": (None, [f32p, L, I, I, f32p]),
             "orc_set_threads": (None, [I]),
             "orc_get_threads": (I, []),
+            "orc_fp_rule_mismatches": (L, [I, L, ctypes.c_uint64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(h, name)
@@ -84,6 +85,13 @@ def get_threads():
 
 
 # ------------------------------------------------------------------ ATQ (quantizer.py)
+
+def fp_rule_mismatches(rule, count, seed=1):
+    """Mismatches of a GPU arithmetic shortcut against the oracle's own operation (C, fmaf):
+    rule 0 = the division-free ITF round (atq.hip round_code), rule 1 = the reciprocal-corrected
+    division of the SSR similarity (ssr.hip div_rcp)."""
+    return int(lib().orc_fp_rule_mismatches(rule, count, seed))
+
 
 def ternary_init(W):
     """quantizer.py:32-69. Returns alpha (n,1), mu (n,1), T (n,b) float32."""

@@ -765,3 +765,56 @@ int orc_get_threads(void) {
   return 1;
 #endif
 }
+
+/* ---- checks of the GPU path's arithmetic shortcuts (test infrastructure, not the reference) ----
+ * rule 0: atq.hip round_code -- sign(d) iff |d| - as/2 > as * 2^-25  ==  the ±0.5 test on RN(d/as)
+ * rule 1: ssr.hip div_rcp    -- fma(fma(-b, q, a), y, q), q = a*y, y = RN(1/b)  ==  RN(a/b)
+ *         for |a| >= 2^-80 and b in [1e-8, 2^64]
+ * Returns the number of mismatching pairs out of `count` pseudo-random pairs (xorshift64 from
+ * `seed`), drawn near the thresholds / midpoints as well as across the ranges. */
+static uint64_t orc_xs(uint64_t* s) {
+  *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17;
+  return *s;
+}
+static float orc_uf(uint64_t* s) { return (float)(orc_xs(s) >> 40) * (1.0f / 16777216.0f); }
+
+long orc_fp_rule_mismatches(int rule, long count, uint64_t seed) {
+  uint64_t st = seed ? seed : 88172645463325252ull;
+  long bad = 0;
+  for (long it = 0; it < count; ++it) {
+    if (rule == 0) {
+      float as = expf(logf(1e-8f) + orc_uf(&st) * (logf(1e4f) - logf(1e-8f)));
+      float d = as * 0.5f;
+      int k = (int)(orc_xs(&st) % 81) - 40;
+      for (int j = 0; j < (k < 0 ? -k : k); ++j) d = nextafterf(d, k > 0 ? INFINITY : -INFINITY);
+      if (it & 1) d = -d;
+      if ((it & 7) == 7) d = (orc_uf(&st) * 4.0f - 2.0f) * as;
+      const float q = d / as;
+      const float ref = q > 0.5f ? 1.0f : (q < -0.5f ? -1.0f : 0.0f);
+      const float got = (fabsf(d) - as * 0.5f > as * 0x1p-25f) ? copysignf(1.0f, d) : 0.0f;
+      bad += got != ref;
+    } else {
+      float b = expf((orc_uf(&st) * 2.0f - 1.0f) * 20.0f);
+      if (b < 1e-8f) b = 1e-8f;
+      float a;
+      switch (it & 3) {
+        case 0: a = (orc_uf(&st) * 2.0f - 1.0f) * b; break;
+        case 1: a = b * (orc_uf(&st) * 2.0f - 1.0f) * expf(-orc_uf(&st) * 30.0f); break;
+        case 2: {
+          uint32_t u = (uint32_t)orc_xs(&st);
+          memcpy(&a, &u, 4);
+          if (!isfinite(a)) a = 1.0f;
+          if (fabsf(a) > b) a = fmodf(a, b);
+          break;
+        }
+        default: { a = (orc_uf(&st) * 2.0f - 1.0f) * b; uint32_t u; memcpy(&u, &a, 4);
+                   u += (uint32_t)((int)(orc_xs(&st) % 5) - 2); memcpy(&a, &u, 4); }
+      }
+      if (!(fabsf(a) >= 0x1p-80f)) continue;
+      const float y = 1.0f / b, q = a * y;
+      const float got = fmaf(fmaf(-b, q, a), y, q), ref = a / b;
+      bad += memcmp(&got, &ref, 4) != 0;
+    }
+  }
+  return bad;
+}

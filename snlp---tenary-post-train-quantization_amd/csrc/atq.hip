@@ -22,19 +22,21 @@ constexpr int ROWS_PER_WAVE = 4;
 constexpr int WAVES = 4;
 constexpr int ROWS_PER_WG = ROWS_PER_WAVE * WAVES;
 
-// flexible_round's code of RN((w - mu) / as) at the ±0.5 thresholds (quantizer.py:127-131),
-// without a division in the common case: qa = d * rcp(as) is within 2^-21 (relative) of the
-// exact quotient, so whenever qa is farther than 2^-20 from a threshold the exact quotient, and
-// its correctly rounded value (rounding is monotonic), lie on the same side.  Near a threshold,
-// or if the reciprocal is unreliable, the correctly rounded division decides, exactly as before.
-PT2Q_DEV float round_code(float d, float as, float ras, bool ras_ok) {
-  float q = d * ras;
-  const float aq = fabsf(q);
-  if (!ras_ok || !(fabsf(aq - 0.5f) > aq * 0x1p-20f)) q = d / as;
-  return (q > 0.5f) ? 1.0f : ((q < -0.5f) ? -1.0f : 0.0f);
+// flexible_round's code of RN(d / as) at the ±0.5 thresholds (quantizer.py:127-131), decided
+// exactly with no division.  RN(x) > 0.5 iff x > 0.5 + 2^-25 (that midpoint to the next float
+// rounds to even, i.e. to 0.5), so the code is sign(d) iff |d| - as/2 > as * 2^-25 in exact
+// arithmetic.  as/2 and as * 2^-25 are exact (as >= 1e-8 by the clamp); the float |d| - as/2 is
+// exact whenever as/4 <= |d| <= as (Sterbenz), and outside that range its rounding cannot cross
+// as * 2^-25.  NaN / inf operands give the division's codes (0 for a NaN quotient).  Checked
+// against the correctly rounded division on 1.2e8 pairs within 40 ulp of the thresholds
+// (tests/test_oracle.py::test_round_threshold_rule).
+struct RoundTh {
+  float hs, eps;
+};
+PT2Q_DEV RoundTh round_th(float as) { return {as * 0.5f, as * 0x1p-25f}; }
+PT2Q_DEV float round_code(float d, RoundTh th) {
+  return (fabsf(d) - th.hs > th.eps) ? copysignf(1.0f, d) : 0.0f;
 }
-PT2Q_DEV float rcp_approx(float as) { return __builtin_amdgcn_rcpf(as); }
-PT2Q_DEV bool rcp_ok(float as) { return as < 1e30f; }  // as >= 1e-8 by the clamp
 
 // FULL: b == 16 * NS (every lane holds NS elements; no per-element range checks)
 template <int NS, bool FULL = false>
@@ -71,7 +73,7 @@ PT2Q_DEV bool row_init(Row<NS, F>& R, float wsum, float* alpha0, float* mu0) {
     if (R.has(s)) {
       float wc = R.w[s] - mu;
       t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
-      pn = pn + t * wc;
+      pn = fmaf(t, wc, pn);  // t * wc exact
       pd = pd + fabsf(t);
     }
     R.t[s] = t;
@@ -83,53 +85,36 @@ PT2Q_DEV bool row_init(Row<NS, F>& R, float wsum, float* alpha0, float* mu0) {
   return cnt == 0.0f;
 }
 
-// build_optimal_grid, quantizer.py:71-108.
+// build_optimal_grid, quantizer.py:71-108.  sum(w t) is the SUM16 of fmaf(w, t, p) (w * t is
+// exact for t in {-1, 0, 1}, so each step is the same rounding of p + w * t).  sum(t) and sum(t^2)
+// are integers <= 128 in any order: one exact SUM16 of 512 t^2 + t carries both.
 template <int NS, bool F>
 PT2Q_DEV void row_grid(const Row<NS, F>& R, float wsum, float* a, float* m) {
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (R.has(s)) {
-      pwt = pwt + R.w[s] * R.t[s];
+      pwt = fmaf(R.w[s], R.t[s], pwt);
       pt = pt + R.t[s];
-      pt2 = pt2 + R.t[s] * R.t[s];
+      pt2 = fmaf(R.t[s], R.t[s], pt2);
     }
-  float swt = bfly16(pwt), ts = bfly16(pt), t2 = bfly16(pt2);
+  const float swt = bfly16(pwt), v = bfly16(fmaf(pt2, 512.0f, pt));
+  const float t2 = rintf(v * 0x1p-9f), ts = fmaf(-512.0f, t2, v);
   const float fb = (float)R.b;
   float den = clampmin(fb * t2 - ts * ts);
   *a = (fb * swt - ts * wsum) / den;
   *m = (t2 * wsum - ts * swt) / den;
 }
 
-// flexible_round, quantizer.py:110-134. Returns true if this lane changed a code.  The quotients
-// come from the reciprocal first (straight-line code); only when some lane of the wave has one
-// near a threshold (round_code's test) does the wave take the correctly rounded divisions.
+// flexible_round, quantizer.py:110-134 (round_code). Returns true if this lane changed a code.
 template <int NS, bool F>
 PT2Q_DEV bool row_round(Row<NS, F>& R, float a, float m) {
-  float as = clampmin(a);
-  const float ras = rcp_approx(as);
-  const bool rok = rcp_ok(as);
-  float d[NS], q[NS];
-  bool near = !rok;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    d[s] = R.w[s] - m;
-    q[s] = d[s] * ras;
-    const float aq = fabsf(q[s]);
-    near |= R.has(s) && !(fabsf(aq - 0.5f) > aq * 0x1p-20f);
-  }
-  if (__any(near)) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float aq = fabsf(q[s]);
-      if (!rok || !(fabsf(aq - 0.5f) > aq * 0x1p-20f)) q[s] = d[s] / as;
-    }
-  }
+  const RoundTh th = round_th(clampmin(a));
   bool changed = false;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
     if (R.has(s)) {
-      const float nt = (q[s] > 0.5f) ? 1.0f : ((q[s] < -0.5f) ? -1.0f : 0.0f);
+      const float nt = round_code(R.w[s] - m, th);
       changed |= (nt != R.t[s]);
       R.t[s] = nt;
     }
@@ -698,11 +683,11 @@ PT2Q_DEV bool wide_init(const WideRow<L>& R, float wsum, float* a, float* m, flo
     const float wc = w - mu;
     const float t = (wc > delta) ? 1.0f : ((wc < -delta) ? -1.0f : 0.0f);
     R.set_t(c, t);
-    pn = pn + t * wc;
+    pn = fmaf(t, wc, pn);  // t * wc exact
     pd = pd + fabsf(t);
-    pwt = pwt + w * t;
+    pwt = fmaf(w, t, pwt);
     pt = pt + t;
-    pt2 = pt2 + t * t;
+    pt2 = fmaf(t, t, pt2);
   });
   const float num = bfly16(pn), cnt = bfly16(pd);
   g[0] = bfly16(pwt);
@@ -725,9 +710,9 @@ template <class L>
 PT2Q_DEV void wide_grid_pass(const WideRow<L>& R, float* g) {
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
   R.template pass<true>([&](int, long, float w, float t) {
-    pwt = pwt + w * t;
+    pwt = fmaf(w, t, pwt);
     pt = pt + t;
-    pt2 = pt2 + t * t;
+    pt2 = fmaf(t, t, pt2);
   });
   g[0] = bfly16(pwt);
   g[1] = bfly16(pt);
@@ -738,20 +723,18 @@ PT2Q_DEV void wide_grid_pass(const WideRow<L>& R, float* g) {
 // next grid's sums into g.  Returns whether this lane changed a code.
 template <class L>
 PT2Q_DEV bool wide_round_pass(const WideRow<L>& R, float a, float m, float* g) {
-  const float as = clampmin(a);
-  const float ras = rcp_approx(as);
-  const bool rok = rcp_ok(as);
+  const RoundTh th = round_th(clampmin(a));
   bool changed = false;
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
   R.template pass<true>([&](int, long c, float w, float old) {
-    const float nt = round_code(w - m, as, ras, rok);
+    const float nt = round_code(w - m, th);
     if (nt != old) {
       changed = true;
       R.set_t(c, nt);
     }
-    pwt = pwt + w * nt;
+    pwt = fmaf(w, nt, pwt);  // exact product (row_grid)
     pt = pt + nt;
-    pt2 = pt2 + nt * nt;
+    pt2 = fmaf(nt, nt, pt2);
   });
   g[0] = bfly16(pwt);
   g[1] = bfly16(pt);

@@ -24,11 +24,11 @@ PT2Q_DEV float xor_lane(float p) {
   const int v = __float_as_int(p);
   int r;
   if constexpr (K == 1) {
-    r = __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    r = __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
   } else if constexpr (K == 2) {
-    r = __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    r = __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
   } else if constexpr (K == 8) {
-    r = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    r = __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, true);  // row_ror:8
   } else {
     static_assert(K == 4, "xor_lane: K in {1, 2, 4, 8}");
     r = __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0x5, false);  // banks 0, 2: row_shl:4
@@ -38,9 +38,11 @@ PT2Q_DEV float xor_lane(float p) {
 }
 
 // Butterfly over the 16 lanes of a lane group (xor 8,4,2,1): every lane ends with the same sum.
+// After the xor-8 step p[l] == p[l ^ 8], so the row rotation by 4 (lane (l + 4) mod 16) delivers
+// the value of lane l ^ 4: one DPP move instead of the two bank-masked shifts of xor_lane<4>.
 PT2Q_DEV float bfly16(float p) {
   p = p + xor_lane<8>(p);
-  p = p + xor_lane<4>(p);
+  p = p + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(p), 0x124, 0xF, 0xF, true));
   p = p + xor_lane<2>(p);
   p = p + xor_lane<1>(p);
   return p;

@@ -226,6 +226,18 @@ __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) 
   for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = wn[i] / nw;
 }
 
+// RN(x / nj) from one correctly rounded reciprocal y = RN(1 / nj) and a Markstein correction:
+// q = RN(x y) is within an ulp of x / nj, r = fma(-nj, q, x) is exact, and RN(q + r y) is then
+// RN(x / nj) -- provided nothing underflows, which |x| >= 2^-80 guarantees for nj in
+// [1e-8, 2^64] (a finite column norm).  A column with a smaller |x| (zeros included) or a
+// non-finite norm takes the division (wave-uniform branch).  Checked against the division on
+// 4e8 pairs (tests/test_oracle_golden.py::test_rcp_division_rule).
+PT2Q_DEV float div_rcp(float x, float nj, float y) {
+  const float q = x * y;
+  return fmaf(fmaf(-nj, q, x), y, q);
+}
+PT2Q_DEV bool rcp_column_ok(float minabs, float nj) { return minabs >= 0x1p-80f && nj <= 0x1p64f; }
+
 // One wave per remaining column: nj = clamp(sqrt(SUMN fma x^2)); s = SUMN fma (x/nj) * wn.
 // NV > 0 (n % 4 == 0, n <= 256 NV): one pass over the column, its NV float4 per lane kept in
 // registers for both chains; NV == 0: the generic two-pass paths.
@@ -261,26 +273,38 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
         if (base < n) w[u] = *(const f4*)(wn + base);
       }
     }
-    float ss = 0.0f;
+    float ss = 0.0f, mn = 0x1p64f;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       if (4 * t + 256 * u < n) {
-        ss = fmaf(v[u][0], v[u][0], ss);
-        ss = fmaf(v[u][1], v[u][1], ss);
-        ss = fmaf(v[u][2], v[u][2], ss);
-        ss = fmaf(v[u][3], v[u][3], ss);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ss = fmaf(v[u][q], v[u][q], ss);
+          mn = fminf(mn, fabsf(v[u][q]));
+        }
       }
     }
     const float nj = clampmin(sqrtf(bfly64(ss)));
+    if (__all(rcp_column_ok(mn, nj))) {
+      const float y = 1.0f / nj;
 #pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const long base = 4 * t + 256 * u;
-      if (base < n) {
-        const f4 wu = PRE ? w[PRE ? u : 0] : *(const f4*)(wn + base);
-        p = fmaf(v[u][0] / nj, wu[0], p);
-        p = fmaf(v[u][1] / nj, wu[1], p);
-        p = fmaf(v[u][2] / nj, wu[2], p);
-        p = fmaf(v[u][3] / nj, wu[3], p);
+      for (int u = 0; u < NV; ++u) {
+        const long base = 4 * t + 256 * u;
+        if (base < n) {
+          const f4 wu = PRE ? w[PRE ? u : 0] : *(const f4*)(wn + base);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p = fmaf(div_rcp(v[u][q], nj, y), wu[q], p);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const long base = 4 * t + 256 * u;
+        if (base < n) {
+          const f4 wu = PRE ? w[PRE ? u : 0] : *(const f4*)(wn + base);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p = fmaf(v[u][q] / nj, wu[q], p);
+        }
       }
     }
   } else if ((n & 3) == 0 && (ldw & 3) == 0) {
@@ -328,6 +352,7 @@ __global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, 
                                                                int r, const float* wn, float* sim, long zs) {
   __shared__ float part[64];
   __shared__ float njs;
+  __shared__ bool okw[S];
   Wt = zws(Wt, zs);
   rem = zws(rem, zs);
   wn = zws(wn, zs);
@@ -347,7 +372,13 @@ __global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, 
     const long base = 4 * t + 256 * (16 * s + u);
     if (base < n) w[u] = *(const f4*)(wn + base);
   }
-  float ss = 0.0f;
+  float ss = 0.0f, mn = 0x1p64f;
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (4 * t + 256 * (16 * s + u) < n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mn = fminf(mn, fabsf(v[u][q]));
+    }
   for (int q = 0; q < S; ++q) {
     if (s == q) {
       if (q > 0) ss = part[t];
@@ -363,24 +394,36 @@ __global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, 
     }
     __syncthreads();
   }
+  const bool wave_ok = __all(mn >= 0x1p-80f);
+  if (t == 0) okw[s] = wave_ok;
   if (s == S - 1) {
     const float tot = bfly64(ss);
     if (t == 0) njs = clampmin(sqrtf(tot));
   }
   __syncthreads();
   const float nj = njs;
+  bool fast = nj <= 0x1p64f;
+  for (int q = 0; q < S; ++q) fast = fast && okw[q];  // workgroup-uniform
+  const float y = 1.0f / nj;
   float p = 0.0f;
   for (int q = 0; q < S; ++q) {
     if (s == q) {
       if (q > 0) p = part[t];
+      if (fast) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (4 * t + 256 * (16 * s + u) < n) {
-          p = fmaf(v[u][0] / nj, w[u][0], p);
-          p = fmaf(v[u][1] / nj, w[u][1], p);
-          p = fmaf(v[u][2] / nj, w[u][2], p);
-          p = fmaf(v[u][3] / nj, w[u][3], p);
-        }
+        for (int u = 0; u < 16; ++u)
+          if (4 * t + 256 * (16 * s + u) < n) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) p = fmaf(div_rcp(v[u][c], nj, y), w[u][c], p);
+          }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (4 * t + 256 * (16 * s + u) < n) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) p = fmaf(v[u][c] / nj, w[u][c], p);
+          }
+      }
       if (q < S - 1) part[t] = p;
     }
     __syncthreads();

@@ -203,6 +203,29 @@ def test_atq_edges_vs_reference(pt2q):
     np.testing.assert_array_equal(host(T).astype(np.int8), g["round_T"])
 
 
+@pytest.mark.parametrize("b", [128, 1000])
+def test_atq_round_at_thresholds(pt2q, b):
+    """flexible_round (quantizer.py:127-131) on quotients within 40 ulp of ±0.5: the HIP round
+    decides RN(d / as) against ±0.5 with no division (atq.hip round_code); every code must equal
+    the oracle's correctly rounded division.  b = 128: the row kernel; b = 1000: the wide one."""
+    rng = np.random.default_rng(b)
+    n = 256
+    alpha = np.exp(rng.uniform(np.log(1e-6), np.log(10.0), n)).astype(np.float32)
+    mu = np.where(np.arange(n) % 2 == 0, 0.0, rng.standard_normal(n) * 0.01).astype(np.float32)
+    d = np.repeat((alpha * np.float32(0.5))[:, None], b, axis=1)
+    k = rng.integers(-40, 41, (n, b))
+    for step in range(1, 41):
+        sel = np.abs(k) >= step
+        d[sel] = np.nextafter(d[sel], np.where(k[sel] > 0, np.inf, -np.inf).astype(np.float32))
+    d *= np.where(rng.random((n, b)) < 0.5, -1, 1).astype(np.float32)
+    W = (d + mu[:, None]).astype(np.float32)
+    q = pt2q.AsymmetricTernaryQuantizer()
+    T = q.flexible_round(cuda(W), cuda(alpha[:, None]), cuda(mu[:, None]))
+    ref = orc.flexible_round(W, alpha[:, None], mu[:, None])
+    assert np.array_equal(host(T), ref)
+    assert 0.2 < (ref == 0).mean() < 0.8  # both sides of the thresholds are exercised
+
+
 def test_atq_per_channel_b1000_vs_reference(pt2q):
     """b = 1000 > 512: the streaming one-lane-per-row kernel (atq_wide_*), per-method stages
     and the fused quantize, vs the oracle (bit-exact) and the reference's fixture."""

@@ -407,3 +407,46 @@ def test_oracle_model_layer1_teacher_forced():
         np.testing.assert_array_equal(o["T"], unpack2(g[f"T2_{i}"], m), err_msg=name)
         assert np.array_equal(o["alpha"], g[f"alpha{i}"]) and np.array_equal(o["mu"], g[f"mu{i}"]), name
         check_vs_unmodified_reference(g, i, name, o["perm"], o["T"], o["alpha"], o["mu"])
+
+
+def test_round_threshold_rule():
+    """The HIP ITF round (csrc/atq.hip round_code) decides RN(d / as) against ±0.5 with no
+    division: sign(d) iff |d| - as/2 > as * 2^-25.  Pin it to the correctly rounded float32
+    division (quantizer.py:127-131, oracle flexible_round) within 40 ulp of both thresholds, on
+    random quotients, and on NaN / inf / zero operands."""
+    rng = np.random.default_rng(7)
+    n = 2_000_000
+
+    def by_division(d, a):
+        with np.errstate(all="ignore"):
+            q = (d / a).astype(np.float32)
+        return np.where(q > 0.5, 1, np.where(q < -0.5, -1, 0))
+
+    def by_rule(d, a):
+        with np.errstate(all="ignore"):
+            hs = (a * np.float32(0.5)).astype(np.float32)
+            eps = (a * np.float32(2.0 ** -25)).astype(np.float32)
+            r = (np.abs(d) - hs).astype(np.float32)
+        return np.where(r > eps, np.where(d > 0, 1, -1), 0)
+
+    a = np.exp(rng.uniform(np.log(1e-8), np.log(1e4), n)).astype(np.float32)
+    k = rng.integers(-40, 41, n)
+    d = (a * np.float32(0.5)).astype(np.float32)
+    for step in range(1, 41):
+        m = np.abs(k) >= step
+        d[m] = np.nextafter(d[m], np.where(k[m] > 0, np.inf, -np.inf).astype(np.float32))
+    d = d * np.where(rng.random(n) < 0.5, -1, 1).astype(np.float32)
+    np.testing.assert_array_equal(by_rule(d, a), by_division(d, a))
+    d2 = (rng.standard_normal(n) * a * 2).astype(np.float32)
+    np.testing.assert_array_equal(by_rule(d2, a), by_division(d2, a))
+    sp = np.array([0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 3e38], np.float32)
+    A = np.array([1e-8, 1.0, np.inf, np.nan, 3e38, 1e30], np.float32)
+    D, AA = np.meshgrid(sp, A)
+    np.testing.assert_array_equal(by_rule(D, AA), by_division(D, AA))
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_fp_shortcut_rules_in_c(rule):
+    """The same two GPU shortcuts checked in C with hardware fmaf (oracle/pt2q_oracle.c
+    orc_fp_rule_mismatches): rule 0 the ITF round, rule 1 the SSR similarity's x / nj."""
+    assert orc.fp_rule_mismatches(rule, 20_000_000, 12345) == 0
