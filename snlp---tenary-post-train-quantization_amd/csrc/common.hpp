@@ -37,12 +37,17 @@ PT2Q_DEV float xor_lane(float p) {
   return __int_as_float(r);
 }
 
+// xor_lane<4> for a value already symmetric under xor 8 (p[l] == p[l ^ 8], as after a butterfly's
+// xor-8 step): the row rotation by 4 (lane (l + 4) mod 16) then delivers the value of lane l ^ 4,
+// one DPP move instead of two bank-masked shifts.
+PT2Q_DEV float xor4_sym8(float p) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(p), 0x124, 0xF, 0xF, true));  // row_ror:4
+}
+
 // Butterfly over the 16 lanes of a lane group (xor 8,4,2,1): every lane ends with the same sum.
-// After the xor-8 step p[l] == p[l ^ 8], so the row rotation by 4 (lane (l + 4) mod 16) delivers
-// the value of lane l ^ 4: one DPP move instead of the two bank-masked shifts of xor_lane<4>.
 PT2Q_DEV float bfly16(float p) {
   p = p + xor_lane<8>(p);
-  p = p + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(p), 0x124, 0xF, 0xF, true));
+  p = p + xor4_sym8(p);
   p = p + xor_lane<2>(p);
   p = p + xor_lane<1>(p);
   return p;

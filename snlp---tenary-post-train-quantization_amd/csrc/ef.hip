@@ -326,7 +326,7 @@ PT2Q_DEV void ef_wb_b(EfWb2& w) {
   const float s0 = xor_lane<8>(w.x0), s1 = xor_lane<8>(w.x1);
   w.x0 = w.x0 + s0;
   w.x1 = w.x1 + s1;
-  const float t0 = xor_lane<4>(w.x0), t1 = xor_lane<4>(w.x1);
+  const float t0 = xor4_sym8(w.x0), t1 = xor4_sym8(w.x1);  // after the xor-8 step
   w.x0 = w.x0 + t0;
   w.x1 = w.x1 + t1;
 }
