@@ -42,12 +42,14 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);
   geti("PT2Q_WIDE_WAVES", t.wide_waves);
+  geti("PT2Q_ATQ_OCC", t.atq_occ);
   geti("PT2Q_EF_V2", t.ef_v2);
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
   if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;
   if (t.wide_waves != 8) t.wide_waves = 4;
+  if (t.atq_occ != 0) t.atq_occ = 6;
   if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
     const long c = std::atol(e);
     if (c >= 0) t.spin_cap_long = t.spin_cap_short = t.spin_cap_fallback = c;

@@ -404,7 +404,18 @@ PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
 }
 
 template <int NS, bool F>
-__global__ __launch_bounds__(256) void atq_block_kernel(BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
+PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid);
+
+// OCC: 0 = the compiler's register budget (85 VGPRs at NS = 8, 5 waves per SIMD); 6 = at least
+// six waves per SIMD (76 VGPRs, no spills) to hide more of the row gathers (PT2Q_ATQ_OCC).
+template <int NS, bool F, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8))) void atq_block_kernel(
+    BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
+  atq_block_body<NS, F>(A0, g, K, rowgrid);
+}
+
+template <int NS, bool F>
+PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid) {
   const BlockArgs A = at_linear(A0, g);
   if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
     atq_s1_part(A);
@@ -905,12 +916,17 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   const int cgrid = per_k * b;
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
-    if (b == 16 * NS)
-      hipLaunchKernelGGL((atq_block_kernel<NS, true>), dim3(nS1 + grid + cgrid, 1, nz), dim3(256), 0, st, A, g, K,
-                         grid);
-    else
-      hipLaunchKernelGGL((atq_block_kernel<NS, false>), dim3(nS1 + grid + cgrid, 1, nz), dim3(256), 0, st, A, g, K,
-                         grid);
+    const dim3 gd(nS1 + grid + cgrid, 1, nz);
+    // the six-wave variant only where it costs no spills: full 128-column blocks
+    constexpr int OCC = NS == 8 ? 6 : 0;
+    if (b == 16 * NS) {
+      if (OCC && pt2q_tuning().atq_occ == 6)
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, OCC>), gd, dim3(256), 0, st, A, g, K, grid);
+      else
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0>), gd, dim3(256), 0, st, A, g, K, grid);
+    } else {
+      hipLaunchKernelGGL((atq_block_kernel<NS, false, 0>), gd, dim3(256), 0, st, A, g, K, grid);
+    }
     PT2Q_LAUNCH_CHECK();
     hipLaunchKernelGGL(atq_finish_kernel<NS>, dim3(1, 1, nz), dim3(256), 0, st, A, grid, g);
     PT2Q_LAUNCH_CHECK();

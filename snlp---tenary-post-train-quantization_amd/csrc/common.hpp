@@ -129,6 +129,7 @@ struct Pt2qTuning {
   int ef2_stagger = 0;         // PT2Q_EF2_STAGGER: ef2 start de-phasing (0: off)
   int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
+  int atq_occ = 6;             // PT2Q_ATQ_OCC: block-ATQ waves per SIMD floor (6, or 0: compiler's)
   // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
   // seconds, before they give up and report PT2Q_E_STALL.  PT2Q_DEBUG_SPIN_CAP overrides both
   // (0: every hand-off reports a stall -- tests force the reporting path with it).

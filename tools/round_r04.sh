@@ -20,3 +20,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/bench_trace -o run --
 f=$(find $OUT/bench_trace -name "*kernel_trace.csv" | head -1)
 python3 $R/tools/kstats.py $f > $OUT/bench_kstats.txt 2>&1 && head -30 $OUT/bench_kstats.txt
 gzip -f $f
+# live stage busy with the block-ATQ occupancy floor off and on (PT2Q_ATQ_OCC)
+cd $R
+for occ in 0 6; do
+  PT2Q_ATQ_OCC=$occ timeout -k 10 200 python -u tools/stage_busy.py > $OUT/busy_occ$occ.json 2> $OUT/busy_occ$occ.err || exit 1
+  echo "occ=$occ $(cat $OUT/busy_occ$occ.json)"
+done
