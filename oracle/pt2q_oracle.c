@@ -768,7 +768,8 @@ int orc_get_threads(void) {
 
 /* ---- checks of the GPU path's arithmetic shortcuts (test infrastructure, not the reference) ----
  * rule 0: atq.hip round_code -- sign(d) iff |d| - as/2 > as * 2^-25  ==  the ±0.5 test on RN(d/as)
- * rule 1: ssr.hip div_rcp    -- fma(fma(-b, q, a), y, q), q = a*y, y = RN(1/b)  ==  RN(a/b)
+ * rule 1: ssr.hip div_rcp    -- two corrections q' = fma(fma(-b, q, a), y, q) from q = a*y,
+ *         y = RN(1/b)  ==  RN(a/b)
  *         for |a| >= 2^-80 and b in [1e-8, 2^64]
  * Returns the number of mismatching pairs out of `count` pseudo-random pairs (xorshift64 from
  * `seed`), drawn near the thresholds / midpoints as well as across the ranges. */
@@ -811,8 +812,9 @@ long orc_fp_rule_mismatches(int rule, long count, uint64_t seed) {
                    u += (uint32_t)((int)(orc_xs(&st) % 5) - 2); memcpy(&a, &u, 4); }
       }
       if (!(fabsf(a) >= 0x1p-80f)) continue;
-      const float y = 1.0f / b, q = a * y;
-      const float got = fmaf(fmaf(-b, q, a), y, q), ref = a / b;
+      const float y = 1.0f / b, q0 = a * y;
+      const float q1 = fmaf(fmaf(-b, q0, a), y, q0);
+      const float got = fmaf(fmaf(-b, q1, a), y, q1), ref = a / b;
       bad += memcmp(&got, &ref, 4) != 0;
     }
   }

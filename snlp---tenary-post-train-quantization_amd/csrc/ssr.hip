@@ -226,15 +226,17 @@ __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) 
   for (int i = threadIdx.x; i < n; i += blockDim.x) wn[i] = wn[i] / nw;
 }
 
-// RN(x / nj) from one correctly rounded reciprocal y = RN(1 / nj) and a Markstein correction:
-// q = RN(x y) is within an ulp of x / nj, r = fma(-nj, q, x) is exact, and RN(q + r y) is then
-// RN(x / nj) -- provided nothing underflows, which |x| >= 2^-80 guarantees for nj in
-// [1e-8, 2^64] (a finite column norm).  A column with a smaller |x| (zeros included) or a
-// non-finite norm takes the division (wave-uniform branch).  Checked against the division on
-// 4e8 pairs (tests/test_oracle_golden.py::test_rcp_division_rule).
+// RN(x / nj) from one correctly rounded reciprocal y = RN(1 / nj) (Markstein): with r = x - nj q
+// exact (fma), RN(q + r y) = RN(x / nj) whenever q is within one ulp of x / nj and nothing
+// underflows.  q0 = RN(x y) can be 1.5 ulp off, so one correction first brings it within
+// 0.5 ulp + 2^-23 ulp, and the second is exact.  No underflow: |x| >= 2^-80 with nj in
+// [1e-8, 2^64] (a finite column norm); a column with a smaller |x| (zeros included) or a
+// non-finite norm takes the division (wave-uniform branch).  5 VALU instead of the division's
+// scaled Newton sequence; pinned against the division by orc_fp_rule_mismatches (rule 1).
 PT2Q_DEV float div_rcp(float x, float nj, float y) {
-  const float q = x * y;
-  return fmaf(fmaf(-nj, q, x), y, q);
+  const float q0 = x * y;
+  const float q1 = fmaf(fmaf(-nj, q0, x), y, q0);
+  return fmaf(fmaf(-nj, q1, x), y, q1);
 }
 PT2Q_DEV bool rcp_column_ok(float minabs, float nj) { return minabs >= 0x1p-80f && nj <= 0x1p64f; }
 
