@@ -346,6 +346,39 @@ def cpu_baseline(units, N, block_size, use_ssr, hidden):
                        "sample": (f"1 thread: Gram over {rows1} rows ({tg1:.2f}s), Cholesky inverse "
                                   f"of order {cm1} ({tc1:.2f}s, x(m/{cm1})^3), block loop on {br1} "
                                   f"of {d} rows ({tb1:.2f}s, x n/{br1}); same work-law scaling")}
+    # The reference's own CPU path is faster than this port: its Gram and Cholesky are torch /
+    # MKL calls (main.py:128, 136-139), and its block loop ran in 0.47-0.61x the port's time on
+    # identical layers (profiles/cpu_ref_vs_oracle.json, build container).  So a GPU / port ratio
+    # overstates GPU / reference: estimate the reference on this host from the same torch ops,
+    # timed live on the same samples, and the measured block-loop ratio.
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_ref_vs_oracle.json")) as f:
+            rows_ref = json.load(f)["rows"]
+        r44 = [r for r in rows_ref if r["m"] == 4096 and r["threads"] == 8]
+        ratio = float(r44[0]["reference_over_oracle"]) if r44 else None
+    except (OSError, KeyError, ValueError):
+        ratio = None
+    if ratio is not None:
+        torch.set_num_threads(cores)
+        Xt, Ht = torch.from_numpy(X), torch.from_numpy(H)
+
+        def tbest(fn):
+            dt = float("inf")
+            for _ in range(2):
+                t0 = time.perf_counter()
+                fn()
+                dt = min(dt, time.perf_counter() - t0)
+            return dt
+        tgt = tbest(lambda: Xt.T @ Xt)
+        tct = tbest(lambda: torch.cholesky_inverse(torch.linalg.cholesky(Ht)))
+        tot_t, _ = scaled(tgt, rows, tct, d, tb * ratio, d)
+        res["torch_ref_over_port"] = ratio
+        res["reference_estimate"] = {
+            "value": cols / tot_t, "unit": "cols/s", "cores": cores, "s_workload": tot_t,
+            "how": (f"the reference's CPU ops timed live with torch on {cores} threads: X.T @ X over {rows} rows "
+                    f"({tgt:.3f}s, main.py:128), cholesky + cholesky_inverse at {d} ({tct:.3f}s, main.py:136-139); "
+                    f"the block loop = the port's x {ratio:.3f} (reference / port time on a {d}x{d} layer, "
+                    "profiles/cpu_ref_vs_oracle.json); same work-law scaling")}
     return res
 
 
@@ -538,7 +571,7 @@ def model_work(units, bs, io_bytes=2, ssr=True):
 
 STAGE_KERNELS = {"gram": "gram16b_kernel / gram_streamk_kernel", "inverse": "chol_* + rank_update2 + gemmx_kernel",
                  "setup": "transpose_to_f32 + group_init", "ssr": "ssr_wbar_* + ssr_sim* + ssr_topk",
-                 "atq": "atq_block_kernel / atq_wide_* + atq_post", "ef": "ef_gemm_kernel",
+                 "atq": "atq_block_kernel / atq_wide_* + atq_finish", "ef": "ef2_gemm_kernel (ef_gemm_kernel with PT2Q_EF_V2=0)",
                  "out": "transpose_i8 / transpose_f32"}
 
 
@@ -613,7 +646,8 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
     return st
 
 
-TAIL_STAGE = (("ef_gemm", "ef"), ("ssr_", "ssr"), ("atq_", "atq"))
+# kernel-name prefixes of the tail stages (ef_gemm_kernel, ef2_gemm_kernel<4>, ...)
+TAIL_STAGE = (("ef_gemm", "ef"), ("ef2_gemm", "ef"), ("ef3_gemm", "ef"), ("ssr_", "ssr"), ("atq_", "atq"))
 
 
 def load_committed_stages():
@@ -796,6 +830,7 @@ class DryStep:
             self.ran.append(f"{name}.{p}")
             g = torch.Generator().manual_seed(zlib.crc32(f"{name}.{p}".encode()))
             B = -(-m // self.bs)
+            n = min(n, 8)  # 8-row stand-ins: full-size shapes (a 7B / 13B unit list) stay cheap on gloo
             outs.append(SimpleNamespace(alpha=torch.rand((n, B), generator=g), mu=torch.rand((n, B), generator=g),
                                         T=(torch.randint(0, 3, (n, m), generator=g) - 1).to(torch.int8),
                                         perm=torch.randperm(m, generator=g)))
@@ -889,6 +924,9 @@ def main(argv=None):
               if step_ms else None}
         if a.dry_run:
             me["ran"] = sorted(set(work.ran))
+        # the LPT cost model's seconds for this shard (sharding.unit_cost), beside the measured ms,
+        # so a first multi-GPU run shows a modelled-vs-measured imbalance at once
+        me["predicted_cost_s"] = sum(sharding.unit_cost(work.units[i], a.block_size) for i in mine)
         if world > 1:
             ranks = [None] * world
             dist.all_gather_object(ranks, me)
@@ -896,6 +934,13 @@ def main(argv=None):
             ranks = [me]
     ms_per_step = 1e3 * elapsed / max(a.steps, 1)
     cols = {"model": sharding.units_cols(work.units), "layer": world * a.m, "split": a.m}[a.workload]
+    balance = None
+    if ranks:
+        pc = [r["predicted_cost_s"] for r in ranks]
+        mc = [r["ms_per_step"] for r in ranks]
+        balance = {"predicted_max_over_mean": max(pc) / (sum(pc) / len(pc)) if sum(pc) > 0 else None,
+                   "measured_max_over_mean": max(mc) / (sum(mc) / len(mc)) if sum(mc) > 0 else None,
+                   "model": "sharding.unit_cost (Gram N*m^2, inverse m^3, block loop n*r), LPT over the ranks"}
     log(rank, f"timed {a.steps} steps: {ms_per_step:.1f} ms/step")
     if a.dry_run:
         if rank == 0:
@@ -904,7 +949,7 @@ def main(argv=None):
                    "value": cols / (ms_per_step * 1e-3), "unit": "cols/s", "n_gpus": world,
                    "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms_per_step,
                    "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "none",
-                   "data": "dry run (no kernels)", "ranks": ranks,
+                   "data": "dry run (no kernels)", "ranks": ranks, "lpt_balance": balance,
                    "gathered_linears": sorted(got) if got is not None else None,
                    "config": {"workload": "dry run", "weight_columns_per_step": cols}}
             print(json.dumps(res), flush=True)
@@ -1031,7 +1076,8 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": f"{a.io_dtype}->f32" if a.io_dtype != "fp32" else "f32",
             "data": (f"synthetic (counter-hash {a.io_dtype} weights std 0.02; {a.io_dtype} activations, unit "
-                     "variance, 1% x20 outlier channels; one resident activation tensor per input width per rank)"),
+                     f"variance, 1% x20 outlier channels; {X_DISTINCT} distinct resident activation tensors per "
+                     "input width per rank, rotated over that width's units)"),
             "config": {"workload": f"{model_desc}, N={N} calibration rows, variant M, "
                                    f"{'SSR' if use_ssr else 'sequential'}+ATQ(ITF,AGA), block {bs}",
                        "weight_columns_per_step": cols, "tokens": N, "io_dtype": a.io_dtype,
@@ -1048,6 +1094,7 @@ def main(argv=None):
         if a.workload == "model":
             res["s_model"] = ms_per_step / 1e3
             res["ranks"] = ranks
+            res["lpt_balance"] = balance
             res["gathered_linears"] = getattr(work, "gathered", None)
         if roof is not None:
             res["roofline"] = roof

@@ -770,7 +770,8 @@ int orc_get_threads(void) {
  * rule 0: atq.hip round_code -- sign(d) iff |d| - as/2 > as * 2^-25  ==  the ±0.5 test on RN(d/as)
  * rule 1: ssr.hip div_rcp    -- two corrections q' = fma(fma(-b, q, a), y, q) from q = a*y,
  *         y = RN(1/b)  ==  RN(a/b)
- *         for |a| >= 2^-80 and b in [1e-8, 2^64]
+ *         for a == 0 (equal up to the sign of zero, which the similarity chain cannot see) or
+ *         |a| >= 2^-80, and b in [1e-8, 2^40] with |a| <= b (the kernel's gate)
  * Returns the number of mismatching pairs out of `count` pseudo-random pairs (xorshift64 from
  * `seed`), drawn near the thresholds / midpoints as well as across the ranges. */
 static uint64_t orc_xs(uint64_t* s) {
@@ -798,8 +799,8 @@ long orc_fp_rule_mismatches(int rule, long count, uint64_t seed) {
       float b = expf((orc_uf(&st) * 2.0f - 1.0f) * 20.0f);
       if (b < 1e-8f) b = 1e-8f;
       float a;
-      switch (it & 3) {
-        case 0: a = (orc_uf(&st) * 2.0f - 1.0f) * b; break;
+      switch (it & 7) {
+        case 0: case 4: a = (orc_uf(&st) * 2.0f - 1.0f) * b; break;
         case 1: a = b * (orc_uf(&st) * 2.0f - 1.0f) * expf(-orc_uf(&st) * 30.0f); break;
         case 2: {
           uint32_t u = (uint32_t)orc_xs(&st);
@@ -808,14 +809,20 @@ long orc_fp_rule_mismatches(int rule, long count, uint64_t seed) {
           if (fabsf(a) > b) a = fmodf(a, b);
           break;
         }
+        case 5:  /* the gate's corner: |a| just above 2^-80, b up to 2^40 (q down to 2^-120) */
+          a = ldexpf(1.0f + orc_uf(&st), -80 + (int)(orc_xs(&st) % 8)) * ((it & 8) ? -1.0f : 1.0f);
+          b = ldexpf(1.0f + orc_uf(&st), 24 + (int)(orc_xs(&st) % 16));
+          break;
+        case 6: a = (it & 8) ? -0.0f : 0.0f; break;
         default: { a = (orc_uf(&st) * 2.0f - 1.0f) * b; uint32_t u; memcpy(&u, &a, 4);
                    u += (uint32_t)((int)(orc_xs(&st) % 5) - 2); memcpy(&a, &u, 4); }
       }
-      if (!(fabsf(a) >= 0x1p-80f)) continue;
+      if (!(a == 0.0f || fabsf(a) >= 0x1p-80f) || !(b <= 0x1p40f) || fabsf(a) > b) continue;
       const float y = 1.0f / b, q0 = a * y;
       const float q1 = fmaf(fmaf(-b, q0, a), y, q0);
       const float got = fmaf(fmaf(-b, q1, a), y, q1), ref = a / b;
-      bad += memcmp(&got, &ref, 4) != 0;
+      if (a == 0.0f) bad += got != 0.0f;
+      else bad += memcmp(&got, &ref, 4) != 0;
     }
   }
   return bad;

@@ -44,7 +44,11 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_WIDE_WAVES", t.wide_waves);
   geti("PT2Q_ATQ_OCC", t.atq_occ);
   geti("PT2Q_EF_V2", t.ef_v2);
+#ifdef PT2Q_DEV_PROBES
+  // ef2 knock-outs (tools/ef2_knock.sh; results garbage): only a development build
+  // (make DEV_PROBES=1) reads this, so a stray variable cannot corrupt a release library's results
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
+#endif
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
   if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;

@@ -85,21 +85,42 @@ PT2Q_DEV bool row_init(Row<NS, F>& R, float wsum, float* alpha0, float* mu0) {
   return cnt == 0.0f;
 }
 
-// build_optimal_grid, quantizer.py:71-108.  sum(w t) is the SUM16 of fmaf(w, t, p) (w * t is
-// exact for t in {-1, 0, 1}, so each step is the same rounding of p + w * t).  sum(t) and sum(t^2)
-// are integers <= 128 in any order: one exact SUM16 of 512 t^2 + t carries both.
-template <int NS, bool F>
+// build_optimal_grid, quantizer.py:71-108.  TERN (codes known to be in {-1, 0, 1}: every grid of
+// the ITF loop): sum(w t) is the SUM16 of fmaf(w, t, p) (w * t is exact, so each step is the same
+// rounding of p + w * t), and sum(t), sum(t^2) are integers with |sum t| <= sum t^2 <= b <= 512:
+// one SUM16 of 1024 t^2 + t carries both exactly (every partial < 2^24; |sum t| / 1024 <= 0.5 and
+// the tie at |sum t| = 512 -- all codes of one sign, sum t^2 = 512 -- rounds to the even 512).
+// !TERN (the per-method GRID / ITF stages read the caller's T, any values): three separate
+// SUM16 chains of the plain products, as the oracle (grid_row).
+template <bool TERN, int NS, bool F>
 PT2Q_DEV void row_grid(const Row<NS, F>& R, float wsum, float* a, float* m) {
+  static_assert(16 * NS <= 512, "packed grid counts need b <= 512");
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
+  float swt, ts, t2;
+  if constexpr (TERN) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if (R.has(s)) {
-      pwt = fmaf(R.w[s], R.t[s], pwt);
-      pt = pt + R.t[s];
-      pt2 = fmaf(R.t[s], R.t[s], pt2);
-    }
-  const float swt = bfly16(pwt), v = bfly16(fmaf(pt2, 512.0f, pt));
-  const float t2 = rintf(v * 0x1p-9f), ts = fmaf(-512.0f, t2, v);
+    for (int s = 0; s < NS; ++s)
+      if (R.has(s)) {
+        pwt = fmaf(R.w[s], R.t[s], pwt);
+        pt = pt + R.t[s];
+        pt2 = fmaf(R.t[s], R.t[s], pt2);
+      }
+    const float v = bfly16(fmaf(pt2, 1024.0f, pt));
+    swt = bfly16(pwt);
+    t2 = rintf(v * 0x1p-10f);
+    ts = fmaf(-1024.0f, t2, v);
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (R.has(s)) {
+        pwt = pwt + R.w[s] * R.t[s];
+        pt = pt + R.t[s];
+        pt2 = pt2 + R.t[s] * R.t[s];
+      }
+    swt = bfly16(pwt);
+    ts = bfly16(pt);
+    t2 = bfly16(pt2);
+  }
   const float fb = (float)R.b;
   float den = clampmin(fb * t2 - ts * ts);
   *a = (fb * swt - ts * wsum) / den;
@@ -122,14 +143,21 @@ PT2Q_DEV bool row_round(Row<NS, F>& R, float a, float m) {
 }
 
 // iterative_ternary_fitting, quantizer.py:136-175, wave-level stop (see file header).
-// Assumes the block is not all-zero at init (iteration 0 never stops).
-template <int NS, bool F>
+// Assumes the block is not all-zero at init (iteration 0 never stops).  TERN: the codes on entry
+// are ternary (from row_init); the stage entry passes the caller's T, so its first grid is the
+// general one (every later grid sees round's codes).
+template <bool TERN, int NS, bool F>
 PT2Q_DEV int row_itf(Row<NS, F>& R, float wsum, int max_iter, float* a, float* m) {
   int it = 0;
   bool any = true;
+  if (!TERN && max_iter > 0) {
+    row_grid<false>(R, wsum, a, m);
+    any = __any(row_round(R, *a, *m));
+    it = 1;
+  }
   for (; it < max_iter; ++it) {
     if (!any) break;
-    row_grid(R, wsum, a, m);
+    row_grid<true>(R, wsum, a, m);
     bool ch = row_round(R, *a, *m);
     any = __any(ch);
   }
@@ -285,7 +313,7 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   bool zero = row_init(R, wsum, &a, &m);
   if (count_zero && valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
   int it = 0;
-  if (!skip_itf) it = row_itf(R, wsum, A.max_iter, &a, &m);
+  if (!skip_itf) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
   if (A.S1 && A.nS1 > 0) {  // S1 / d from this launch's leading workgroups (write-through)
     int ready = 1;
     if ((threadIdx.x & 63) == 0) ready = wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, nullptr, 0);
@@ -521,7 +549,7 @@ __global__ __launch_bounds__(256) void atq_stage_kernel(StageArgs A) {
       row_init(R, wsum, &a, &m);
       break;
     case PT2Q_STAGE_GRID:
-      row_grid(R, wsum, &a, &m);
+      row_grid<false>(R, wsum, &a, &m);
       write_t = false;
       break;
     case PT2Q_STAGE_ROUND:
@@ -530,7 +558,7 @@ __global__ __launch_bounds__(256) void atq_stage_kernel(StageArgs A) {
     case PT2Q_STAGE_ITF: {
       // Caller passes init (alpha, mu, T); zero_rows[0] holds the count of all-zero T rows.
       bool block_zero = (*A.zero_rows == A.n);
-      if (!block_zero) it = row_itf(R, wsum, A.max_iter, &a, &m);
+      if (!block_zero) it = row_itf<false>(R, wsum, A.max_iter, &a, &m);
       break;
     }
     case PT2Q_STAGE_AGA:
@@ -544,7 +572,7 @@ __global__ __launch_bounds__(256) void atq_stage_kernel(StageArgs A) {
         return;
       }
       bool block_zero = (*A.zero_rows == A.n);
-      if (!block_zero) it = row_itf(R, wsum, A.max_iter, &a, &m);
+      if (!block_zero) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
       if (A.S1) row_aga(R, S1, *A.d, &a, &m);
       break;
     }
@@ -716,14 +744,16 @@ PT2Q_DEV void wide_grid(const float* g, float fb, float wsum, float* a, float* m
   *m = (g[2] * wsum - g[1] * g[0]) / den;
 }
 
-// grid partials over the codes in T (the ITF stage entry without a preceding init pass)
+// grid partials over the caller's T (the GRID / ITF stage entries, no preceding init pass): any
+// values, so the plain rounded products of the oracle's grid_row (the fmaf form of the passes
+// below is the same only for ternary codes)
 template <class L>
 PT2Q_DEV void wide_grid_pass(const WideRow<L>& R, float* g) {
   float pwt = 0.0f, pt = 0.0f, pt2 = 0.0f;
   R.template pass<true>([&](int, long, float w, float t) {
-    pwt = fmaf(w, t, pwt);
+    pwt = pwt + w * t;
     pt = pt + t;
-    pt2 = fmaf(t, t, pt2);
+    pt2 = pt2 + t * t;
   });
   g[0] = bfly16(pwt);
   g[1] = bfly16(pt);

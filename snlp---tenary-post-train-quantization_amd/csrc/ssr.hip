@@ -229,16 +229,34 @@ __global__ __launch_bounds__(1024) void ssr_wbar_final_kernel(float* wn, int n) 
 // RN(x / nj) from one correctly rounded reciprocal y = RN(1 / nj) (Markstein): with r = x - nj q
 // exact (fma), RN(q + r y) = RN(x / nj) whenever q is within one ulp of x / nj and nothing
 // underflows.  q0 = RN(x y) can be 1.5 ulp off, so one correction first brings it within
-// 0.5 ulp + 2^-23 ulp, and the second is exact.  No underflow: |x| >= 2^-80 with nj in
-// [1e-8, 2^64] (a finite column norm); a column with a smaller |x| (zeros included) or a
-// non-finite norm takes the division (wave-uniform branch).  5 VALU instead of the division's
+// 0.5 ulp + 2^-23 ulp, and the second is exact.  No underflow: every nonzero |x| >= 2^-80 and
+// nj in [1e-8, 2^40] (nj >= |x|: the clamped norm of the column holding x), so |q| >= 2^-120 is
+// normal and r (about 2^-24 |x|) is too.  x = 0 gives a zero quotient (its sign may differ from
+// the division's: q0 = -0, the corrections +0), and a signed zero cannot change the similarity
+// chain p = fma(q, w, p) -- p starts at +0 and an exactly-zero fma result is -0 only if both
+// addends are, so p is never -0 and fma(+-0, w, p) = p.  A column with a nonzero |x| < 2^-80 or
+// a norm above 2^40 takes the division (wave-uniform branch).  5 VALU instead of the division's
 // scaled Newton sequence; pinned against the division by orc_fp_rule_mismatches (rule 1).
+constexpr float RCP_X_MIN = 0x1p-80f, RCP_NJ_MAX = 0x1p40f;
 PT2Q_DEV float div_rcp(float x, float nj, float y) {
   const float q0 = x * y;
   const float q1 = fmaf(fmaf(-nj, q0, x), y, q0);
   return fmaf(fmaf(-nj, q1, x), y, q1);
 }
-PT2Q_DEV bool rcp_column_ok(float minabs, float nj) { return minabs >= 0x1p-80f && nj <= 0x1p64f; }
+PT2Q_DEV bool rcp_column_ok(float minabs, float nj) { return minabs >= RCP_X_MIN && nj <= RCP_NJ_MAX; }
+// The gate's re-check when a lane's min |x| failed it: the smallest NONZERO |x| of its registers
+// (zeros -- pruned or padded weights -- keep the fast path; rare, so off the common path).
+template <int U, typename V>
+PT2Q_DEV float min_nonzero_abs(const V (&v)[U], int n, int t, int u0) {
+  float mz = 0x1p64f;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (4 * t + 256 * (u0 + u) < n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mz = fminf(mz, v[u][q] == 0.0f ? 0x1p64f : fabsf(v[u][q]));
+    }
+  return mz;
+}
 
 // One wave per remaining column: nj = clamp(sqrt(SUMN fma x^2)); s = SUMN fma (x/nj) * wn.
 // NV > 0 (n % 4 == 0, n <= 256 NV): one pass over the column, its NV float4 per lane kept in
@@ -287,7 +305,9 @@ __global__ __launch_bounds__(256) void ssr_sim_kernel(const float* Wt, long ldw,
       }
     }
     const float nj = clampmin(sqrtf(bfly64(ss)));
-    if (__all(rcp_column_ok(mn, nj))) {
+    bool fast = __all(rcp_column_ok(mn, nj));
+    if (!fast && nj <= RCP_NJ_MAX) fast = __all(min_nonzero_abs(v, n, t, 0) >= RCP_X_MIN);
+    if (fast) {
       const float y = 1.0f / nj;
 #pragma unroll
       for (int u = 0; u < NV; ++u) {
@@ -396,7 +416,8 @@ __global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, 
     }
     __syncthreads();
   }
-  const bool wave_ok = __all(mn >= 0x1p-80f);
+  bool wave_ok = __all(mn >= RCP_X_MIN);
+  if (!wave_ok) wave_ok = __all(min_nonzero_abs(v, n, t, 16 * s) >= RCP_X_MIN);
   if (t == 0) okw[s] = wave_ok;
   if (s == S - 1) {
     const float tot = bfly64(ss);
@@ -404,31 +425,50 @@ __global__ __launch_bounds__(64 * S) void ssr_sim_split_kernel(const float* Wt, 
   }
   __syncthreads();
   const float nj = njs;
-  bool fast = nj <= 0x1p64f;
+  bool fast = nj <= RCP_NJ_MAX;
   for (int q = 0; q < S; ++q) fast = fast && okw[q];  // workgroup-uniform
-  const float y = 1.0f / nj;
+  // chain p = fma(x / nj, w, p) over this wave's elements, continued across the waves in order.
   float p = 0.0f;
-  for (int q = 0; q < S; ++q) {
-    if (s == q) {
-      if (q > 0) p = part[t];
-      if (fast) {
+  if (fast) {  // workgroup-uniform
+    // the quotients in place first, every wave at once: only the chain is serial over the waves
+    const float y = 1.0f / nj;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[u][c] = div_rcp(v[u][c], nj, y);
+    for (int q = 0; q < S; ++q) {
+      if (s == q) {
+        if (q > 0) p = part[t];
 #pragma unroll
         for (int u = 0; u < 16; ++u)
           if (4 * t + 256 * (16 * s + u) < n) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) p = fmaf(div_rcp(v[u][c], nj, y), w[u][c], p);
+            for (int c = 0; c < 4; ++c) p = fmaf(v[u][c], w[u][c], p);
           }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (4 * t + 256 * (16 * s + u) < n) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) p = fmaf(v[u][c] / nj, w[u][c], p);
-          }
+        if (q < S - 1) part[t] = p;
       }
-      if (q < S - 1) part[t] = p;
+      __syncthreads();
     }
-    __syncthreads();
+  } else {
+    // the division (rare columns): a rolled loop re-reading the column and the mean (L2 hits),
+    // so its register image stays small -- unrolled beside the fast path, the two need 200 VGPRs
+    // (two waves per SIMD instead of three)
+    for (int q = 0; q < S; ++q) {
+      if (s == q) {
+        if (q > 0) p = part[t];
+#pragma unroll 1
+        for (int u = 0; u < 16; ++u) {
+          const long base = 4 * t + 256 * (16 * s + u);
+          if (base < n) {
+            const f4 xv = *(const f4*)(x + base), wv = *(const f4*)(wn + base);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) p = fmaf(xv[c] / nj, wv[c], p);
+          }
+        }
+        if (q < S - 1) part[t] = p;
+      }
+      __syncthreads();
+    }
   }
   if (s == S - 1) {
     p = bfly64(p);

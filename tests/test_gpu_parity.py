@@ -226,6 +226,40 @@ def test_atq_round_at_thresholds(pt2q, b):
     assert 0.2 < (ref == 0).mean() < 0.8  # both sides of the thresholds are exercised
 
 
+@pytest.mark.parametrize("b", [128, 300, 512, 1000])
+def test_atq_one_signed_codes_and_general_t(pt2q, b):
+    """Grid counts at their extremes: an ITF whose second grid sees codes almost all of one sign
+    (|sum t| near b, past the 256 a 512-multiplier packing could carry), and build_optimal_grid
+    on a caller T that is not ternary (quantizer.py:71-108 accepts any T): both vs the oracle,
+    bit-exact."""
+    n = 96
+    rng = np.random.default_rng(b)
+    W = rng.uniform(1.0, 1.1, (n, b)).astype(np.float32)
+    T0 = np.ones((n, b), np.float32)
+    zc = rng.choice(b, 6, replace=False)
+    W[:, zc] = 0.0
+    T0[:, zc] = -1.0
+    T0[(rng.random((n, b)) < 0.1) & (T0 > 0)] = 0.0  # the first round makes these +1 as well
+    W[: n // 2] *= -1.0  # half the rows one-signed the other way
+    T0[: n // 2] *= -1.0
+    q = pt2q.AsymmetricTernaryQuantizer()
+    Wd = cuda(W)
+    ga, gm = q.build_optimal_grid(Wd, cuda(T0))
+    rga, rgm = orc.build_optimal_grid(W, T0)
+    assert bits_equal(host(ga), rga) and bits_equal(host(gm), rgm)
+    _, _, rTa, _ = orc.iterative_ternary_fitting(W, rga, rgm, T0, max_iter=1)
+    assert np.abs(rTa.sum(axis=1)).min() > 0.8 * b  # what the second (packed) grid must carry
+    a1, m1, T1 = q.iterative_ternary_fitting(Wd, ga, gm, cuda(T0))
+    ra1, rm1, rT1, rit = orc.iterative_ternary_fitting(W, rga, rgm, T0)
+    assert np.array_equal(host(T1), rT1)
+    assert bits_equal(host(a1), ra1) and bits_equal(host(m1), rm1)
+    assert int(q.last_itf_iters.item()) == rit >= 2
+    Tg = rng.standard_normal((n, b)).astype(np.float32)  # not ternary
+    ga, gm = q.build_optimal_grid(Wd, cuda(Tg))
+    rga, rgm = orc.build_optimal_grid(W, Tg)
+    assert bits_equal(host(ga), rga) and bits_equal(host(gm), rgm)
+
+
 def test_atq_per_channel_b1000_vs_reference(pt2q):
     """b = 1000 > 512: the streaming one-lane-per-row kernel (atq_wide_*), per-method stages
     and the fused quantize, vs the oracle (bit-exact) and the reference's fixture."""
@@ -339,6 +373,11 @@ def test_ssr_similarity_quotient_paths(pt2q, n, m):
     W[:5, 20] = 1e-20         # a few tiny elements in an otherwise normal column
     W[:, 30] = 0.0            # an all-zero column (norm clamped to 1e-8)
     W[:, 40] *= 1e-12         # small norm, elements still in range
+    W[::2, 50:90] = 0.0       # pruned columns: zeros keep the reciprocal path (nonzero-min gate)
+    W[1, 60] = 1e-30          # ... except beside a tiny nonzero element
+    W[:, 95] *= 1e13          # norm above 2^40: the division
+    W[:, 96] = 0.0
+    W[5, 96] = 1e-30          # a lone tiny element: quotient ~1, division path
     rem = np.arange(m, dtype=np.int64)[(np.arange(m) % 7) != 2]
     rem = np.concatenate([rem, np.array([2, 9], dtype=np.int64)])
     rem.sort()

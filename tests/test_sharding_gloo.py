@@ -323,6 +323,34 @@ def test_bench_gpus2_launches_two_ranks_dry_run():
     assert d["config"]["weight_columns_per_step"] == sh.units_cols(units)
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("model,linears", [("llama-2-7b", 224), ("llama-2-13b", 280)])
+def test_bench_gpus8_dry_run_full_models(model, linears):
+    """The driver's 8-GPU run, rehearsed on CPU: `bench.py --gpus 8 --model M --dry-run` with the
+    model's full unit list (C4: 128 units / 224 linears; C5: 160 / 280).  Every rank runs its LPT
+    shard, rank 0 gathers every linear, and the modelled makespan (max / mean rank cost) is <= 1.10."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = ["--model", model, "--steps", "1", "--warmup", "0", "--dry-run"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"] + args,
+                       capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _last_json(p.stdout)
+    sh = _sharding()
+    units = sh.model_units(model)
+    bs = sh.MODELS[model]["block_size"]
+    assert d["n_gpus"] == 8 and len(d["ranks"]) == 8
+    assert len(d["gathered_linears"]) == linears == sum(len(u[1]) for u in units)
+    assert d["gathered_linears"] == sorted(f"{n}.{p}" for n, lins, _ in units for p, _, _ in lins)
+    shards = sh.assign_lpt([sh.unit_cost(u, bs) for u in units], 8)
+    for r in d["ranks"]:
+        assert r["units"] == len(shards[r["rank"]])
+        want = sum(sh.unit_cost(units[i], bs) for i in shards[r["rank"]])
+        assert abs(r["predicted_cost_s"] - want) <= 1e-9 * want
+    assert d["lpt_balance"]["predicted_max_over_mean"] <= 1.10
+
+
 def test_bench_refuses_gpus_world_size_mismatch():
     import subprocess
     import sys

@@ -4,6 +4,8 @@
 # (1 = no Wt traffic, 2 = operand DMAs from one hot chunk, 4 = no MFMAs; results garbage), and
 # ef_gemm_kernel for reference.   bash tools/ef2_knock.sh TAG [mask ...]
 # masks: N (ef2 knock-out N), sN (ef2, stagger N), nV (PT2Q_EF_V2=V, no w-bar)
+# The knock-out masks need a development library: make -C <pkg> clean && make -C <pkg> DEV_PROBES=1
+# (the release build ignores PT2Q_EF2_PROBE).
 set -o pipefail
 TAG=${1:-ef2k}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
