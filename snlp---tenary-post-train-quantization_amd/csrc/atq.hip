@@ -22,22 +22,6 @@ constexpr int ROWS_PER_WAVE = 4;
 constexpr int WAVES = 4;
 constexpr int ROWS_PER_WG = ROWS_PER_WAVE * WAVES;
 
-// flexible_round's code of RN(d / as) at the ±0.5 thresholds (quantizer.py:127-131), decided
-// exactly with no division.  RN(x) > 0.5 iff x > 0.5 + 2^-25 (that midpoint to the next float
-// rounds to even, i.e. to 0.5), so the code is sign(d) iff |d| - as/2 > as * 2^-25 in exact
-// arithmetic.  as/2 and as * 2^-25 are exact (as >= 1e-8 by the clamp); the float |d| - as/2 is
-// exact whenever as/4 <= |d| <= as (Sterbenz), and outside that range its rounding cannot cross
-// as * 2^-25.  NaN / inf operands give the division's codes (0 for a NaN quotient).  Checked
-// against the correctly rounded division on 1.2e8 pairs within 40 ulp of the thresholds
-// (tests/test_oracle.py::test_round_threshold_rule).
-struct RoundTh {
-  float hs, eps;
-};
-PT2Q_DEV RoundTh round_th(float as) { return {as * 0.5f, as * 0x1p-25f}; }
-PT2Q_DEV float round_code(float d, RoundTh th) {
-  return (fabsf(d) - th.hs > th.eps) ? copysignf(1.0f, d) : 0.0f;
-}
-
 // FULL: b == 16 * NS (every lane holds NS elements; no per-element range checks)
 template <int NS, bool FULL = false>
 struct Row {
@@ -975,10 +959,17 @@ int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, c
   WideArgs WA{MODE_BLOCK, (const float*)W, ldw, n, b, nullptr, S1, d, max_iter, alpha, mu, T, ldt, nullptr, 0,
               iters, counters, 0};
   const int wgrid = ceil_div(n, 4 * wide_waves());
+  const bool pc = pt2q_atq_pc_supported(W, wdtype, ldw, b);  // codes held on-chip (atq_pc.hip)
   auto go = [&](auto lay) {
     typedef decltype(lay) L;
-    hipLaunchKernelGGL(atq_wide_block_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
-    PT2Q_LAUNCH_CHECK();
+    if (pc) {
+      const int rc = pt2q_launch_atq_pc(W, wdtype, ldw, n, b, S1, d, max_iter, alpha, mu, T, tdtype, ldt, iters,
+                                        counters, st);
+      if (rc != PT2Q_OK) return rc;
+    } else {
+      hipLaunchKernelGGL(atq_wide_block_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
+      PT2Q_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;

@@ -1,0 +1,362 @@
+// Per-channel ATQ rows (block = every column of the layer, b = m > 512): init -> ITF -> AGA on the
+// caller's row-major W, codes kept on-chip between the ITF passes.
+//
+// Reference: quantizer.py:32-248 (ternary_init, build_optimal_grid, flexible_round,
+// iterative_ternary_fitting, activation_aware_grid_alignment) at block_size = m (main.py:176-189
+// with one block; BASELINE config 5, Llama-2-13B per-channel).
+//
+// The arithmetic is atq.hip's wide path, term for term: a wave holds 4 rows, the 16 lanes of a row
+// own the columns k = l + 16 s (SUM16 partials, one chain per lane in s order, bfly16 folds), so
+// every value is bit-identical to atq_wide_block_kernel and to the oracle.  What changes is where
+// the data lives between the passes (sum w, sum |w - mu|, init, one per ITF iteration, AGA + the
+// code write):
+//  * W is streamed once per pass in chunks of 512 columns (1 KiB of a bf16 row): each lane loads
+//    16-byte pieces of its wave's 4 rows into registers one chunk ahead, stores them into a
+//    wave-private two-stage LDS ring (row stride 1056 B: rows 8 banks apart), and reads back its
+//    own strided elements (ds_read_u16 / b32 at 32 B steps) -- 16-byte global loads instead of one
+//    2-byte load per element, no code loads or stores at all;
+//  * the codes live as two bit masks per lane and chunk (Z: t != 0, S: t < 0 where Z), 2 bits per
+//    element in a wave-private LDS area, so an ITF pass writes nothing to global memory; sum t and
+//    sum t^2 (exact integers) come from popcounts of the masks; T is written once, in the last
+//    pass.
+// The codes of one pass are compared with the previous pass's masks for the wave-level ITF stop.
+#include "common.hpp"
+#include "internal.hpp"
+
+namespace {
+
+constexpr int PC_COLS = 512;   // columns per chunk: 32 per lane
+constexpr int PC_J = 32;       // elements per lane per chunk
+constexpr int PC_WAVES = 2;    // waves (4 rows each) per workgroup
+
+template <class T>
+using lds_t = __attribute__((address_space(3))) T;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef lds_t<char> lds_char;
+
+// storage type of W: element bytes and the exact conversion of its raw bits to fp32
+template <class TI>
+struct PcIn;
+template <>
+struct PcIn<uint16_t> {  // bf16 bits
+  static constexpr int E = 2;
+  PT2Q_DEV static float cvt(uint32_t raw) { return __uint_as_float(raw << 16); }
+};
+template <>
+struct PcIn<_Float16> {
+  static constexpr int E = 2;
+  PT2Q_DEV static float cvt(uint32_t raw) { return (float)__builtin_bit_cast(_Float16, (uint16_t)raw); }
+};
+template <>
+struct PcIn<float> {
+  static constexpr int E = 4;
+  PT2Q_DEV static float cvt(uint32_t raw) { return __uint_as_float(raw); }
+};
+
+template <class TI>
+struct PcGeom {
+  static constexpr int E = PcIn<TI>::E;
+  static constexpr int CHUNK_B = PC_COLS * E;          // bytes of one row's chunk
+  static constexpr int ROWB = CHUNK_B + 16 * E;        // LDS row stride: rows 8 (E=2) / 16 (E=4) banks apart
+  static constexpr int STAGE = 4 * ROWB;               // one chunk of the wave's 4 rows
+  static constexpr int PIECES = CHUNK_B / 16 / 64 * 4;  // 16-byte pieces per lane per chunk (4 or 8)
+  static_assert(CHUNK_B % 1024 == 0, "a row's chunk is whole 1 KiB wave loads");
+};
+
+struct PcArgs {
+  const void* W;     // n x m row-major (ldw elements)
+  long ldw;
+  int n, m;
+  const float* S1;   // m, or nullptr (no AGA)
+  const float* d;    // device scalar (AGA)
+  int max_iter;
+  float* alpha;      // n
+  float* mu;         // n
+  void* T;           // n x m row-major codes (ldt), int8 or fp32
+  long ldt;
+  int* iters;        // atomicMax of the wave iteration counts
+  int* counters;     // [0] rows whose init codes are all zero
+};
+
+__host__ __device__ inline size_t pc_wave_bytes(int stage, int nchunks) { return 2 * (size_t)stage + (size_t)nchunks * 64 * 8; }
+
+// One wave's 4 rows, streamed pass by pass.
+template <class TI>
+struct PcRows {
+  typedef PcGeom<TI> G;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const PcArgs& A;
+  int lane, l, r;       // lane, residue class (column k = l + 16 s), row of the wave (0..3)
+  int i;                // this lane's row (clamped to 0 when invalid: loads stay in range)
+  bool valid;
+  int nc;               // chunks per pass
+  const char* rowp[4];  // the wave's 4 rows (clamped)
+  lds_char* ring;       // wave-private: 2 stages, then the masks [chunk][lane] (Z, S)
+  lds_char* masks;
+  u32x4 stg[G::PIECES];  // next chunk's pieces (registers, one chunk ahead)
+
+  PT2Q_DEV void load_chunk(int c) {  // global -> registers: piece p = row (p % 4), 1 KiB part p / 4
+#pragma unroll
+    for (int p = 0; p < G::PIECES; ++p) {
+      const long off = (long)c * G::CHUNK_B + (p / 4) * 1024 + 16 * lane;
+      const long lim = (long)A.m * G::E;  // m % (16 / E) == 0: pieces never straddle the row end
+      stg[p] = *(const u32x4*)(rowp[p % 4] + (off < lim ? off : 0));
+    }
+  }
+  PT2Q_DEV void store_stage(int st) {  // registers -> LDS stage st
+#pragma unroll
+    for (int p = 0; p < G::PIECES; ++p)
+      *(lds_t<u32x4>*)(ring + st * G::STAGE + (p % 4) * G::ROWB + (p / 4) * 1024 + 16 * lane) = stg[p];
+  }
+  // this lane's 32 elements of the chunk in stage st (element j = column c*512 + l + 16 j)
+  PT2Q_DEV void read_stage(int st, float (&x)[PC_J]) const {
+    const lds_char* b = ring + st * G::STAGE + r * G::ROWB + G::E * l;
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j) {
+      uint32_t raw;
+      if constexpr (G::E == 2) raw = *(const lds_t<uint16_t>*)(b + 32 * j);
+      else raw = *(const lds_t<uint32_t>*)(b + 64 * j);
+      x[j] = PcIn<TI>::cvt(raw);
+    }
+  }
+  // One streamed pass: f.template chunk<TAIL>(c, x, jn) for every chunk in order (jn: this lane's
+  // elements in the chunk, < 32 only in the last chunk).  Prologue: chunk 0 in the stage, chunk 1
+  // in registers.  Every pass restarts the stream (the ring is wave-private: no barriers).
+  template <typename F>
+  PT2Q_DEV void pass(F&& f) {
+    load_chunk(0);
+    store_stage(0);
+    if (nc > 1) load_chunk(1);
+    for (int c = 0; c < nc; ++c) {
+      const int st = c & 1;
+      float x[PC_J];
+      read_stage(st, x);
+      if (c + 1 < nc) {
+        store_stage(st ^ 1);  // chunk c+1 (its stage was last read for chunk c-1: done)
+        if (c + 2 < nc) load_chunk(c + 2);
+      }
+      if ((c + 1) * PC_COLS <= A.m) {  // wave-uniform
+        f.template chunk<false>(c, x, PC_J);
+      } else {
+        const int rem = A.m - c * PC_COLS - l;  // columns of this residue class left (< 512)
+        f.template chunk<true>(c, x, rem > 0 ? (rem + 15) / 16 : 0);
+      }
+    }
+  }
+  PT2Q_DEV lds_t<u32x2>* mask_at(int c) const { return (lds_t<u32x2>*)masks + c * 64 + lane; }
+};
+
+// ---- the passes (each mirrors its atq.hip wide_* counterpart's per-element arithmetic)
+
+struct PcSumW {  // sum w (wide_sum_w)
+  float p = 0.0f;
+  template <bool TAIL>
+  PT2Q_DEV void chunk(int, const float (&x)[PC_J], int jn) {
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j)
+      if (!TAIL || j < jn) p = p + x[j];
+  }
+};
+
+struct PcSumAbs {  // sum |w - mu| (wide_init, first pass)
+  float mu, p = 0.0f;
+  template <bool TAIL>
+  PT2Q_DEV void chunk(int, const float (&x)[PC_J], int jn) {
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j)
+      if (!TAIL || j < jn) p = p + fabsf(x[j] - mu);
+  }
+};
+
+// ternary_init's codes (wide_init, second pass) with the first grid's partials; masks written
+template <class TI>
+struct PcInit {
+  const PcRows<TI>& R;
+  float mu, delta;
+  float pn = 0.0f, pwt = 0.0f;
+  int nz = 0, neg = 0;
+  template <bool TAIL>
+  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
+    uint32_t zn = 0, sn = 0;
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j) {
+      const float w = x[j];
+      const float wc = w - mu;
+      const bool cp = wc > delta, cq = wc < -delta;
+      const bool ok = !TAIL || j < jn;
+      const float t = (ok && cp) ? 1.0f : ((ok && cq) ? -1.0f : 0.0f);
+      pn = fmaf(t, wc, pn);  // t * wc exact; t = 0 adds +-0: p is never -0 (it starts at +0)
+      pwt = fmaf(w, t, pwt);
+      zn = (zn << 1) | (uint32_t)(t != 0.0f);
+      sn = (sn << 1) | (uint32_t)(t < 0.0f);
+    }
+    *R.mask_at(c) = u32x2{zn, sn};
+    nz += __builtin_popcount(zn);
+    neg += __builtin_popcount(sn);
+  }
+};
+
+// one ITF iteration: flexible_round against (a, m) and the next grid's partials (wide_round_pass)
+template <class TI>
+struct PcRound {
+  const PcRows<TI>& R;
+  float m;
+  RoundTh th;
+  float pwt = 0.0f;
+  int nz = 0, neg = 0;
+  bool changed = false;
+  template <bool TAIL>
+  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
+    lds_t<u32x2>* mp = R.mask_at(c);
+    const u32x2 old = *mp;
+    uint32_t zn = 0, sn = 0;
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j) {
+      const float w = x[j];
+      const float dd = w - m;
+      const bool cz = (fabsf(dd) - th.hs > th.eps) && (!TAIL || j < jn);
+      const float t = cz ? copysignf(1.0f, dd) : 0.0f;
+      pwt = fmaf(w, t, pwt);  // exact product (row_grid)
+      zn = (zn << 1) | (uint32_t)cz;
+      sn = __builtin_amdgcn_alignbit(sn, __float_as_uint(dd), 31);  // (sn << 1) | sign(dd)
+    }
+    sn &= zn;
+    changed |= ((zn ^ old.x) | (sn ^ old.y)) != 0u;
+    *mp = u32x2{zn, sn};
+    nz += __builtin_popcount(zn);
+    neg += __builtin_popcount(sn);
+  }
+};
+
+// activation_aware_grid_alignment (wide_aga) over the final codes, and the codes written to T
+template <class TI, class TO>
+struct PcAgaOut {
+  const PcRows<TI>& R;
+  const float* S1;  // nullable: codes only
+  float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
+  template <bool TAIL>
+  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
+    const u32x2 mk = *R.mask_at(c);
+    const PcArgs& A = R.A;
+    TO* trow = (TO*)A.T + (long)R.i * A.ldt + (long)c * PC_COLS + R.l;
+    const float* s1 = S1 ? S1 + (long)c * PC_COLS + R.l : nullptr;
+#pragma unroll
+    for (int j = 0; j < PC_J; ++j) {
+      if (TAIL && j >= jn) continue;
+      const uint32_t bit = 1u << (PC_J - 1 - j);
+      const float t = (mk.x & bit) ? ((mk.y & bit) ? -1.0f : 1.0f) : 0.0f;
+      if (s1) {
+        const float w = x[j], cv = s1[16 * j];
+        pv = fmaf(t, cv, pv);
+        pws = fmaf(w, cv, pws);
+        pwts = fmaf(w * t, cv, pwts);
+        pt2s = fmaf(t * t, cv, pt2s);
+      }
+      if (R.valid) trow[16 * j] = (TO)t;
+    }
+  }
+};
+
+template <class TI, class TO>
+__global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char pc_lds[];
+  typedef PcGeom<TI> G;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = (A.m + PC_COLS - 1) / PC_COLS;
+  PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr, {}};
+  const int row0 = ((int)blockIdx.x * PC_WAVES + wave) * 4;
+  R.i = row0 + R.r;
+  R.valid = R.i < A.n;
+  if (!R.valid) R.i = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int iq = row0 + q < A.n ? row0 + q : 0;
+    R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
+  }
+  R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
+  R.masks = R.ring + 2 * G::STAGE;
+  const float fb = (float)A.m;
+
+  PcSumW sw;
+  R.pass(sw);
+  const float wsum = bfly16(sw.p);
+  // ternary_init (quantizer.py:32-69)
+  const float mu0 = wsum / fb;
+  PcSumAbs sa{mu0};
+  R.pass(sa);
+  const float delta = 0.75f * (bfly16(sa.p) / fb);
+  PcInit<TI> in{R, mu0, delta};
+  R.pass(in);
+  const float num = bfly16(in.pn), cnt = bfly16((float)in.nz);
+  float g[3] = {bfly16(in.pwt), bfly16((float)(in.nz - 2 * in.neg)), cnt};
+  float a = num / clampmin(cnt), m = mu0;
+  if (R.valid && R.l == 0 && cnt == 0.0f) atomicAdd(&A.counters[0], 1);
+  // iterative_ternary_fitting (quantizer.py:136-175), wave-level stop (atq.hip wide_itf)
+  int it = 0;
+  bool any = true;
+  for (; it < A.max_iter; ++it) {
+    if (!any) break;
+    {
+      const float den = clampmin(fb * g[2] - g[1] * g[1]);
+      a = (fb * g[0] - g[1] * wsum) / den;
+      m = (g[2] * wsum - g[1] * g[0]) / den;
+    }
+    PcRound<TI> rd{R, m, round_th(clampmin(a))};
+    R.pass(rd);
+    g[0] = bfly16(rd.pwt);
+    g[1] = bfly16((float)(rd.nz - 2 * rd.neg));
+    g[2] = bfly16((float)rd.nz);
+    any = __any(rd.changed);
+  }
+  // AGA (quantizer.py:177-248) and the codes
+  PcAgaOut<TI, TO> ag{R, A.S1};
+  R.pass(ag);
+  if (A.S1) {
+    const float dv = *A.d;
+    const float v = bfly16(ag.pv), ws1 = bfly16(ag.pws), wts1 = bfly16(ag.pwts), t2s1 = bfly16(ag.pt2s);
+    const float v2 = v * v;
+    const float den = clampmin(dv * t2s1 - v2);
+    a = (dv * wts1 - v * ws1) / den;
+    m = (t2s1 * ws1 - v * wts1) / den;
+  }
+  if (A.iters && lane == 0) atomicMax(A.iters, it);
+  if (R.valid && R.l == 0) {
+    A.alpha[R.i] = a;
+    A.mu[R.i] = m;
+  }
+}
+
+}  // namespace
+
+// Whether the streamed per-channel kernel takes this call (else atq.hip's wide kernel): 16-byte
+// aligned rows whose length is whole 16-byte pieces, and the LDS the wave areas need.
+bool pt2q_atq_pc_supported(const void* W, int wdtype, long ldw, int m) {
+  if (!pt2q_tuning().atq_pc) return false;
+  const int E = wdtype == PT2Q_F32 ? 4 : 2;
+  if (wdtype != PT2Q_F32 && wdtype != PT2Q_F16 && wdtype != PT2Q_BF16) return false;
+  if (((uintptr_t)W & 15) != 0 || (ldw * E) % 16 != 0 || (m * E) % 16 != 0 || m <= 512) return false;
+  const int stage = 4 * (PC_COLS * E + 16 * E);
+  return PC_WAVES * pc_wave_bytes(stage, ceil_div(m, PC_COLS)) <= 160 * 1024;
+}
+
+int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const float* S1, const float* d,
+                       int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
+                       int* counters, hipStream_t st) {
+  PcArgs A{W, ldw, n, m, S1, d, max_iter, alpha, mu, T, ldt, iters, counters};
+  const int grid = ceil_div(n, 4 * PC_WAVES);
+  auto go = [&](auto ti, auto to) {
+    typedef decltype(ti) TI;
+    typedef decltype(to) TO;
+    const size_t lds = PC_WAVES * pc_wave_bytes(PcGeom<TI>::STAGE, ceil_div(m, PC_COLS));
+    hipLaunchKernelGGL((atq_pc_kernel<TI, TO>), dim3(grid), dim3(64 * PC_WAVES), lds, st, A);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  };
+  const bool i8 = tdtype == PT2Q_I8;
+  switch (wdtype) {
+    case PT2Q_F32: return i8 ? go(float{}, int8_t{}) : go(float{}, float{});
+    case PT2Q_F16: return i8 ? go(_Float16{}, int8_t{}) : go(_Float16{}, float{});
+    case PT2Q_BF16: return i8 ? go(uint16_t{}, int8_t{}) : go(uint16_t{}, float{});
+  }
+  return PT2Q_E_ARG;
+}

@@ -16,6 +16,22 @@
 // clamp(min=1e-8) with torch semantics (NaN propagates): quantizer.py:66,100,125,240.
 PT2Q_DEV float clampmin(float x) { return (x < 1e-8f) ? 1e-8f : x; }
 
+// flexible_round's code of RN(d / as) at the ±0.5 thresholds (quantizer.py:127-131), decided
+// exactly with no division.  RN(x) > 0.5 iff x > 0.5 + 2^-25 (that midpoint to the next float
+// rounds to even, i.e. to 0.5), so the code is sign(d) iff |d| - as/2 > as * 2^-25 in exact
+// arithmetic.  as/2 and as * 2^-25 are exact (as >= 1e-8 by the clamp); the float |d| - as/2 is
+// exact whenever as/4 <= |d| <= as (Sterbenz), and outside that range its rounding cannot cross
+// as * 2^-25.  NaN / inf operands give the division's codes (0 for a NaN quotient).  Checked
+// against the correctly rounded division on 1.2e8 pairs within 40 ulp of the thresholds
+// (tests/test_oracle.py::test_round_threshold_rule).
+struct RoundTh {
+  float hs, eps;
+};
+PT2Q_DEV RoundTh round_th(float as) { return {as * 0.5f, as * 0x1p-25f}; }
+PT2Q_DEV float round_code(float d, RoundTh th) {
+  return (fabsf(d) - th.hs > th.eps) ? copysignf(1.0f, d) : 0.0f;
+}
+
 // The value of lane (this lane ^ K), K in {1, 2, 4, 8}, by DPP inside a row of 16 lanes (no
 // trip through the LDS crossbar as ds_bpermute takes): xor 1 / 2 are quad permutations, xor 8 a
 // row rotation by 8, xor 4 two row shifts by 4 into alternate banks of 4 lanes.  All lanes active.
@@ -130,6 +146,7 @@ struct Pt2qTuning {
   int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
   int atq_occ = 6;             // PT2Q_ATQ_OCC: block-ATQ waves per SIMD floor (6, or 0: compiler's)
+  bool atq_pc = true;          // PT2Q_ATQ_PC=0: per-channel rows on the old streaming wide kernel
   // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
   // seconds, before they give up and report PT2Q_E_STALL.  PT2Q_DEBUG_SPIN_CAP overrides both
   // (0: every hand-off reports a stall -- tests force the reporting path with it).

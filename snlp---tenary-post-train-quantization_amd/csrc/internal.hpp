@@ -27,6 +27,11 @@ inline Grp grp_or_none(const Grp* g) {
 
 // ---- ATQ (atq.hip)
 // per-channel block (b = m > 512) on the caller's row-major W, outputs in place (atq.hip)
+// per-channel rows on the caller's row-major W, codes held on-chip (atq_pc.hip)
+bool pt2q_atq_pc_supported(const void* W, int wdtype, long ldw, int m);
+int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const float* S1, const float* d,
+                       int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
+                       int* counters, hipStream_t st);
 int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, const float* S1, const float* d,
                             int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
                             int* counters, hipStream_t st);
