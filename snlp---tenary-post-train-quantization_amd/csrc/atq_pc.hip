@@ -20,6 +20,9 @@
 //    sum t^2 (exact integers) come from popcounts of the masks; T is written once, in the last
 //    pass.
 // The codes of one pass are compared with the previous pass's masks for the wave-level ITF stop.
+#include <algorithm>
+#include <type_traits>
+
 #include "common.hpp"
 #include "internal.hpp"
 
@@ -28,6 +31,7 @@ namespace {
 constexpr int PC_COLS = 512;   // columns per chunk: 32 per lane
 constexpr int PC_J = 32;       // elements per lane per chunk
 constexpr int PC_WAVES = 2;    // waves (4 rows each) per workgroup
+constexpr int PCR_NW = 10;     // register-resident rows: m = 512 * PCR_NW (5120: Llama-2-13B)
 
 template <class T>
 using lds_t = __attribute__((address_space(3))) T;
@@ -135,23 +139,79 @@ struct PcRows {
         store_stage(st ^ 1);  // chunk c+1 (its stage was last read for chunk c-1: done)
         if (c + 2 < nc) load_chunk(c + 2);
       }
+      u32x2 mk = {0u, 0u};
+      if constexpr (std::decay_t<F>::MASKS_IN) mk = *mask_at(c);
       if ((c + 1) * PC_COLS <= A.m) {  // wave-uniform
-        f.template chunk<false>(c, x, PC_J);
+        f.template chunk<false>(*this, c, x, PC_J, mk);
       } else {
         const int rem = A.m - c * PC_COLS - l;  // columns of this residue class left (< 512)
-        f.template chunk<true>(c, x, rem > 0 ? (rem + 15) / 16 : 0);
+        f.template chunk<true>(*this, c, x, rem > 0 ? (rem + 15) / 16 : 0, mk);
       }
+      if constexpr (std::decay_t<F>::MASKS_OUT) *mask_at(c) = mk;
     }
   }
   PT2Q_DEV lds_t<u32x2>* mask_at(int c) const { return (lds_t<u32x2>*)masks + c * 64 + lane; }
 };
 
+// The register-resident rows (bf16 W, m = 512 NW: C5's 5120 columns at NW = 10): the
+// lane's 32 NW elements held as 16-bit pairs (element 2p in the low half of wr[p], 2p + 1 in the
+// high half), the masks in registers; the passes are fully unrolled, W is read from HBM once.
+template <class TI, int NW>
+struct PcRegs {
+  const PcArgs& A;
+  int lane, l, r, i;
+  bool valid;
+  uint32_t wr[16 * NW];
+  u32x2 M[NW];
+  PT2Q_DEV void load(const char* row) {
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    const uint16_t* w = (const uint16_t*)row + l;
+#pragma unroll
+    for (int p = 0; p < 16 * NW; ++p) {
+      const int s = 2 * p;  // columns l + 16 s and l + 16 (s + 1): 16-bit loads into the two halves
+      u16x2 v;
+      v.x = w[16 * s];
+      v.y = w[16 * s + 16];
+      wr[p] = __builtin_bit_cast(uint32_t, v);
+    }
+  }
+  // Makes a chunk's 16 packed registers opaque to the optimiser: without it, LLVM unpacks every
+  // element once (320 fp32 registers, spilled) -- at the load, and by hoisting a pass's unpacks out
+  // of the ITF loop.  No instruction is emitted.
+  PT2Q_DEV void opaque(int c) {
+    uint32_t* v = wr + 16 * c;
+    asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                 "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),
+                 "+v"(v[14]), "+v"(v[15]));
+  }
+  PT2Q_DEV float elem(int s) const {
+    const uint32_t v = wr[s >> 1];
+    if constexpr (std::is_same<TI, uint16_t>::value)
+      return __uint_as_float((s & 1) ? (v & 0xffff0000u) : (v << 16));
+    else
+      return (float)__builtin_bit_cast(_Float16, (uint16_t)((s & 1) ? (v >> 16) : v));
+  }
+  template <typename F>
+  PT2Q_DEV void pass(F&& f) {
+#pragma unroll
+    for (int c = 0; c < NW; ++c) {
+      opaque(c);
+      float x[PC_J];
+#pragma unroll
+      for (int j = 0; j < PC_J; ++j) x[j] = elem(32 * c + j);
+      f.template chunk<false>(*this, c, x, PC_J, M[c]);
+      asm volatile("" ::: "memory");  // one chunk's loads / stores at a time (register pressure)
+    }
+  }
+};
+
 // ---- the passes (each mirrors its atq.hip wide_* counterpart's per-element arithmetic)
 
 struct PcSumW {  // sum w (wide_sum_w)
+  static constexpr bool MASKS_IN = false, MASKS_OUT = false;
   float p = 0.0f;
-  template <bool TAIL>
-  PT2Q_DEV void chunk(int, const float (&x)[PC_J], int jn) {
+  template <bool TAIL, class R>
+  PT2Q_DEV void chunk(const R&, int, const float (&x)[PC_J], int jn, u32x2&) {
 #pragma unroll
     for (int j = 0; j < PC_J; ++j)
       if (!TAIL || j < jn) p = p + x[j];
@@ -159,9 +219,10 @@ struct PcSumW {  // sum w (wide_sum_w)
 };
 
 struct PcSumAbs {  // sum |w - mu| (wide_init, first pass)
+  static constexpr bool MASKS_IN = false, MASKS_OUT = false;
   float mu, p = 0.0f;
-  template <bool TAIL>
-  PT2Q_DEV void chunk(int, const float (&x)[PC_J], int jn) {
+  template <bool TAIL, class R>
+  PT2Q_DEV void chunk(const R&, int, const float (&x)[PC_J], int jn, u32x2&) {
 #pragma unroll
     for (int j = 0; j < PC_J; ++j)
       if (!TAIL || j < jn) p = p + fabsf(x[j] - mu);
@@ -169,14 +230,13 @@ struct PcSumAbs {  // sum |w - mu| (wide_init, first pass)
 };
 
 // ternary_init's codes (wide_init, second pass) with the first grid's partials; masks written
-template <class TI>
 struct PcInit {
-  const PcRows<TI>& R;
+  static constexpr bool MASKS_IN = false, MASKS_OUT = true;
   float mu, delta;
   float pn = 0.0f, pwt = 0.0f;
   int nz = 0, neg = 0;
-  template <bool TAIL>
-  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
+  template <bool TAIL, class R>
+  PT2Q_DEV void chunk(const R&, int, const float (&x)[PC_J], int jn, u32x2& mk) {
     uint32_t zn = 0, sn = 0;
 #pragma unroll
     for (int j = 0; j < PC_J; ++j) {
@@ -190,25 +250,23 @@ struct PcInit {
       zn = (zn << 1) | (uint32_t)(t != 0.0f);
       sn = (sn << 1) | (uint32_t)(t < 0.0f);
     }
-    *R.mask_at(c) = u32x2{zn, sn};
+    mk = u32x2{zn, sn};
     nz += __builtin_popcount(zn);
     neg += __builtin_popcount(sn);
   }
 };
 
 // one ITF iteration: flexible_round against (a, m) and the next grid's partials (wide_round_pass)
-template <class TI>
 struct PcRound {
-  const PcRows<TI>& R;
+  static constexpr bool MASKS_IN = true, MASKS_OUT = true;
   float m;
   RoundTh th;
   float pwt = 0.0f;
   int nz = 0, neg = 0;
   bool changed = false;
-  template <bool TAIL>
-  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
-    lds_t<u32x2>* mp = R.mask_at(c);
-    const u32x2 old = *mp;
+  template <bool TAIL, class R>
+  PT2Q_DEV void chunk(const R&, int, const float (&x)[PC_J], int jn, u32x2& mk) {
+    const u32x2 old = mk;
     uint32_t zn = 0, sn = 0;
 #pragma unroll
     for (int j = 0; j < PC_J; ++j) {
@@ -222,21 +280,20 @@ struct PcRound {
     }
     sn &= zn;
     changed |= ((zn ^ old.x) | (sn ^ old.y)) != 0u;
-    *mp = u32x2{zn, sn};
+    mk = u32x2{zn, sn};
     nz += __builtin_popcount(zn);
     neg += __builtin_popcount(sn);
   }
 };
 
 // activation_aware_grid_alignment (wide_aga) over the final codes, and the codes written to T
-template <class TI, class TO>
+template <class TO>
 struct PcAgaOut {
-  const PcRows<TI>& R;
+  static constexpr bool MASKS_IN = true, MASKS_OUT = false;
   const float* S1;  // nullable: codes only
   float pv = 0.0f, pws = 0.0f, pwts = 0.0f, pt2s = 0.0f;
-  template <bool TAIL>
-  PT2Q_DEV void chunk(int c, const float (&x)[PC_J], int jn) {
-    const u32x2 mk = *R.mask_at(c);
+  template <bool TAIL, class Rows>
+  PT2Q_DEV void chunk(const Rows& R, int c, const float (&x)[PC_J], int jn, u32x2& mk) {
     const PcArgs& A = R.A;
     TO* trow = (TO*)A.T + (long)R.i * A.ldt + (long)c * PC_COLS + R.l;
     const float* s1 = S1 ? S1 + (long)c * PC_COLS + R.l : nullptr;
@@ -257,40 +314,26 @@ struct PcAgaOut {
   }
 };
 
-template <class TI, class TO>
-__global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char pc_lds[];
-  typedef PcGeom<TI> G;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nc = (A.m + PC_COLS - 1) / PC_COLS;
-  PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr, {}};
-  const int row0 = ((int)blockIdx.x * PC_WAVES + wave) * 4;
-  R.i = row0 + R.r;
-  R.valid = R.i < A.n;
-  if (!R.valid) R.i = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int iq = row0 + q < A.n ? row0 + q : 0;
-    R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
-  }
-  R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
-  R.masks = R.ring + 2 * G::STAGE;
+// The row program on either data source R (PcRows: streamed, PcRegs: registers): sum w, sum
+// |w - mu|, init, ITF, AGA + codes; alpha / mu written by lane l = 0 of each row.
+template <class TO, class R>
+PT2Q_DEV void pc_rows(R& rows) {
+  const PcArgs& A = rows.A;
   const float fb = (float)A.m;
-
   PcSumW sw;
-  R.pass(sw);
+  rows.pass(sw);
   const float wsum = bfly16(sw.p);
   // ternary_init (quantizer.py:32-69)
   const float mu0 = wsum / fb;
   PcSumAbs sa{mu0};
-  R.pass(sa);
+  rows.pass(sa);
   const float delta = 0.75f * (bfly16(sa.p) / fb);
-  PcInit<TI> in{R, mu0, delta};
-  R.pass(in);
+  PcInit in{mu0, delta};
+  rows.pass(in);
   const float num = bfly16(in.pn), cnt = bfly16((float)in.nz);
   float g[3] = {bfly16(in.pwt), bfly16((float)(in.nz - 2 * in.neg)), cnt};
   float a = num / clampmin(cnt), m = mu0;
-  if (R.valid && R.l == 0 && cnt == 0.0f) atomicAdd(&A.counters[0], 1);
+  if (rows.valid && rows.l == 0 && cnt == 0.0f) atomicAdd(&A.counters[0], 1);
   // iterative_ternary_fitting (quantizer.py:136-175), wave-level stop (atq.hip wide_itf)
   int it = 0;
   bool any = true;
@@ -301,16 +344,16 @@ __global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
       a = (fb * g[0] - g[1] * wsum) / den;
       m = (g[2] * wsum - g[1] * g[0]) / den;
     }
-    PcRound<TI> rd{R, m, round_th(clampmin(a))};
-    R.pass(rd);
+    PcRound rd{m, round_th(clampmin(a))};
+    rows.pass(rd);
     g[0] = bfly16(rd.pwt);
     g[1] = bfly16((float)(rd.nz - 2 * rd.neg));
     g[2] = bfly16((float)rd.nz);
     any = __any(rd.changed);
   }
   // AGA (quantizer.py:177-248) and the codes
-  PcAgaOut<TI, TO> ag{R, A.S1};
-  R.pass(ag);
+  PcAgaOut<TO> ag{A.S1};
+  rows.pass(ag);
   if (A.S1) {
     const float dv = *A.d;
     const float v = bfly16(ag.pv), ws1 = bfly16(ag.pws), wts1 = bfly16(ag.pwts), t2s1 = bfly16(ag.pt2s);
@@ -319,11 +362,70 @@ __global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
     a = (dv * wts1 - v * ws1) / den;
     m = (t2s1 * ws1 - v * wts1) / den;
   }
-  if (A.iters && lane == 0) atomicMax(A.iters, it);
-  if (R.valid && R.l == 0) {
-    A.alpha[R.i] = a;
-    A.mu[R.i] = m;
+  if (A.iters && rows.lane == 0) atomicMax(A.iters, it);
+  if (rows.valid && rows.l == 0) {
+    A.alpha[rows.i] = a;
+    A.mu[rows.i] = m;
   }
+}
+
+// Row groups (4 consecutive rows, one wave) are claimed dynamically: the grid is what the chip
+// holds at once, and each wave takes the next group from a counter (counters[1], zeroed with
+// counters[0] by the caller) until none is left -- the ITF iteration counts of the groups vary
+// (5-11), so a static grid's last round of waves ran far emptier than its first.
+PT2Q_DEV int pc_claim(const PcArgs& A, int lane) {
+  int g = 0;
+  if (lane == 0) g = atomicAdd(&A.counters[1], 1);
+  return __builtin_amdgcn_readfirstlane(__shfl(g, 0));
+}
+
+template <class TI, class TO>
+__global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char pc_lds[];
+  typedef PcGeom<TI> G;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = (A.m + PC_COLS - 1) / PC_COLS;
+  const int groups = (A.n + 3) / 4;
+  for (int g = pc_claim(A, lane); g < groups; g = pc_claim(A, lane)) {
+    PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr, {}};
+    const int row0 = g * 4;
+    R.i = row0 + R.r;
+    R.valid = R.i < A.n;
+    if (!R.valid) R.i = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int iq = row0 + q < A.n ? row0 + q : 0;
+      R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
+    }
+    R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
+    R.masks = R.ring + 2 * G::STAGE;
+    pc_rows<TO>(R);
+  }
+}
+
+constexpr int PCR_WAVES = 4;
+template <class TI, class TO, int NW>
+__global__ __launch_bounds__(64 * PCR_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void atq_pcr_kernel(PcArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int groups = (A.n + 3) / 4;
+  for (int g = pc_claim(A, lane); g < groups; g = pc_claim(A, lane)) {
+    PcRegs<TI, NW> R{A, lane, lane & 15, lane >> 4, 0, false, {}, {}};
+    R.i = g * 4 + R.r;
+    R.valid = R.i < A.n;
+    if (!R.valid) R.i = 0;
+    R.load((const char*)A.W + (long)R.i * A.ldw * 2);
+    pc_rows<TO>(R);
+  }
+}
+
+// workgroups the chip holds at once (occupancy x CUs), at most `need`
+template <typename K>
+int pc_grid(K kern, int threads, size_t lds, int need) {
+  int dev = 0, cus = 256, per_cu = 1;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return std::max(1, std::min(need, per_cu * cus));
 }
 
 }  // namespace
@@ -343,12 +445,24 @@ int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const 
                        int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
                        int* counters, hipStream_t st) {
   PcArgs A{W, ldw, n, m, S1, d, max_iter, alpha, mu, T, ldt, iters, counters};
+  if (m == PC_COLS * PCR_NW && wdtype == PT2Q_BF16 && pt2q_tuning().atq_pc_regs) {
+    auto gor = [&](auto ti, auto to) {
+      auto kern = atq_pcr_kernel<decltype(ti), decltype(to), PCR_NW>;
+      const int grid = pc_grid(kern, 64 * PCR_WAVES, 0, ceil_div(n, 4 * PCR_WAVES));
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PCR_WAVES), 0, st, A);
+      PT2Q_LAUNCH_CHECK();
+      return PT2Q_OK;
+    };
+    const bool i8 = tdtype == PT2Q_I8;
+    return i8 ? gor(uint16_t{}, int8_t{}) : gor(uint16_t{}, float{});
+  }
   const int grid = ceil_div(n, 4 * PC_WAVES);
   auto go = [&](auto ti, auto to) {
     typedef decltype(ti) TI;
     typedef decltype(to) TO;
     const size_t lds = PC_WAVES * pc_wave_bytes(PcGeom<TI>::STAGE, ceil_div(m, PC_COLS));
-    hipLaunchKernelGGL((atq_pc_kernel<TI, TO>), dim3(grid), dim3(64 * PC_WAVES), lds, st, A);
+    auto kern = atq_pc_kernel<TI, TO>;
+    hipLaunchKernelGGL(kern, dim3(pc_grid(kern, 64 * PC_WAVES, lds, grid)), dim3(64 * PC_WAVES), lds, st, A);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };

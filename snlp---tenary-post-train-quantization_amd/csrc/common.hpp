@@ -147,6 +147,7 @@ struct Pt2qTuning {
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
   int atq_occ = 6;             // PT2Q_ATQ_OCC: block-ATQ waves per SIMD floor (6, or 0: compiler's)
   bool atq_pc = true;          // PT2Q_ATQ_PC=0: per-channel rows on the old streaming wide kernel
+  bool atq_pc_regs = true;     // PT2Q_ATQ_PC_REGS=0: m = 5120 rows streamed like the others
   // Cross-workgroup waits poll at most this many times (each poll sleeps ~64-128 cycles), i.e.
   // seconds, before they give up and report PT2Q_E_STALL.  PT2Q_DEBUG_SPIN_CAP overrides both
   // (0: every hand-off reports a stall -- tests force the reporting path with it).

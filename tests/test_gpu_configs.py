@@ -190,3 +190,42 @@ def test_block_loop_16bit_vs_reference(pt2q, name):
     np.testing.assert_array_equal(host(out.T), unpack2(g["T2"], W.shape[1]))
     check_scales(host(out.alpha), g["alpha"], "alpha")
     check_scales(host(out.mu), g["mu"], "mu")
+
+
+@pytest.mark.parametrize("n,m,dt,tdt", [(333, 5120, torch.bfloat16, torch.int8), (70, 5120, torch.bfloat16, torch.float32),
+                                        (77, 4104, torch.float16, torch.int8), (50, 1000, torch.float32, torch.int8),
+                                        (40, 13824, torch.bfloat16, torch.int8)])
+def test_per_channel_row_kernels_edges(pt2q, n, m, dt, tdt):
+    """The per-channel block loop (block_size = m) on both row kernels of atq_pc.hip -- 5120 bf16
+    columns: rows held in registers; otherwise streamed through the LDS ring (ragged last chunk
+    at m = 4104 / 1000, f16 / f32 W) -- with rows that are not a multiple of the workgroup's, an
+    all-zero row, one-signed rows and int8 / fp32 codes: every output vs the oracle, bit-exact,
+    and equal to the old streaming wide kernel (PT2Q_ATQ_PC=0 is read at load, so the oracle
+    stands in for it here)."""
+    Wd = pt2q.fill_synthetic((n, m), n + m, std=0.02)
+    Wd[3] = 0.0
+    Wd[5] = Wd[5].abs() + 0.01  # one-signed rows
+    Wd[6] = -Wd[6].abs() - 0.01
+    Wd = Wd.to(dt)
+    Xd = pt2q.fill_synthetic((512, m), n + m + 1, std=1.0, outliers=True).to(dt)
+    G = pt2q.gram(Xd)
+    out = pt2q.engine.quantize_blocks(Wd, G, None, block_size=m, t_dtype=tdt)
+    torch.cuda.synchronize()
+    orc.set_threads(16)
+    ref = orc.quantize_blocks(host(Wd.float()), host(G), np.zeros((1, 1), np.float32), m, True, 1)
+    np.testing.assert_array_equal(host(out.perm), np.arange(m))
+    np.testing.assert_array_equal(host(out.T.float()), ref["T"].astype(np.float32))
+    assert bits_equal(host(out.alpha), ref["alpha"]) and bits_equal(host(out.mu), ref["mu"])
+    np.testing.assert_array_equal(host(out.iters), ref["iters"])
+
+
+@pytest.mark.parametrize("m,dt", [(5120, torch.bfloat16), (2048, torch.float16)])
+def test_per_channel_zero_block(pt2q, m, dt):
+    """All-zero per-channel block: ITF stops at iteration 0 (quantizer.py:164); the init grid
+    (alpha = mu = 0, codes 0) is what every row returns, on both row kernels."""
+    Wd = torch.zeros((37, m), device=DEV, dtype=dt)
+    G = pt2q.gram(pt2q.fill_synthetic((256, m), 7, std=1.0).to(dt))
+    out = pt2q.engine.quantize_blocks(Wd, G, None, block_size=m)
+    torch.cuda.synchronize()
+    assert int(host(out.iters)[0]) == 0
+    assert not host(out.T).any() and not host(out.alpha).any() and not host(out.mu).any()

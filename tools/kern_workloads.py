@@ -1,7 +1,8 @@
 """PMC workloads (dev tool):
-python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT} [reps]
+python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT | pc N M COUNT} [reps]
 inverse: engine.hessian_inverse_batched on BATCH synthetic Grams of order M (N = 262144 scale);
 group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M);
+pc:      per-channel block loops (block_size = M, config C5) of COUNT bf16 N x M linears;
 grams:   engine.gram_batched over COUNT Grams of DISTINCT (env, default 4) resident fp16 N x M
          activations rotated over the items (as the bench)."""
 import os
@@ -31,6 +32,15 @@ elif kind == "grams":
         pt2q.engine.gram_batched([Xs[z % nd] for z in range(count)], G)
     torch.cuda.synchronize()
     print("grams done", float(G[0, 0, 0]))
+elif kind == "pc":
+    n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    X = pt2q.fill_synthetic((4096, m), 78, outliers=True).bfloat16()
+    G = pt2q.gram(X)
+    Ws = [pt2q.fill_synthetic((n, m), 900 + z, std=0.02).bfloat16() for z in range(count)]
+    for _ in range(reps):
+        outs = [pt2q.engine.quantize_blocks(W, G, None, block_size=m) for W in Ws]
+    torch.cuda.synchronize()
+    print("pc done", int(outs[0].iters[0]))
 else:
     n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     X = pt2q.fill_synthetic((4 * m, m), 78, outliers=True).half()

@@ -49,6 +49,13 @@ def main():
                 for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                     if n in c:
                         out.append(f"{n[3:].lower()} {c[n] / w:.2f}")
+            if c.get("SQ_INSTS_VALU") and cyc:
+                # a SIMD-32 issues one wave64 VALU instruction per 2 cycles: 1024 SIMDs x cycles / 2
+                out.append(f"valu_insts {c['SQ_INSTS_VALU']:.3g} valu_issue_frac "
+                           f"{c['SQ_INSTS_VALU'] / (cyc * 1024 / 2):.3f}")
+                for n in ("SQ_INSTS_VMEM", "SQ_ACTIVE_INST_VALU"):
+                    if n in c:
+                        out.append(f"{n[3:].lower()} {c[n]:.3g}")
             if c.get("SQ_INSTS_LDS"):
                 out.append(f"lds_insts {c['SQ_INSTS_LDS']:.3g}")
                 if "SQ_LDS_BANK_CONFLICT" in c:
