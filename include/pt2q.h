@@ -58,6 +58,8 @@ extern "C" {
 
 /* quantize flags */
 #define PT2Q_FLAG_SSR 0x1          /* SSR block selection (reorder.py:107) instead of sequential */
+#define PT2Q_FLAG_S1_GIVEN 0x2     /* one block (b >= m), PT2Q_AGA_ACT: A holds S1 (m floats) then d,
+                                      from pt2q_s1_from_gram[_batched], instead of the Gram */
 #define PT2Q_AGA_NONE 0x0          /* ATQ without activations (quantizer.py:274 X is None) */
 #define PT2Q_AGA_ACT 0x10          /* variant M: S = X_bᵀX_b from the raw Gram (main.py:177) */
 #define PT2Q_AGA_HESS 0x20         /* variant G: S = H_bbᵀH_bb from the damped Hessian (gptq.py:147) */
@@ -209,6 +211,13 @@ int pt2q_atq_stage(int mode, const float* W, int64_t ldw, int n, int b, float* a
 
 /* S1 = S·1 and d = 1ᵀS1 for a symmetric b x b matrix S (quantizer.py:215-218). */
 int pt2q_s1_from_gram(const float* S, int64_t lds, int b, float* S1, float* d_dev, void* stream);
+/* The same for `batch` whole m x m Grams (item z at S + z * item_stride, leading dim lds) in one
+ * launch pair: S1d[z * (m + 1) + j] = S1[j] of item z, S1d[z * (m + 1) + m] = its d; bit-identical
+ * to pt2q_s1_from_gram per item.  Per-channel quantisation (block_size >= m, quantizer.py:215-218
+ * on the whole Gram) feeds S1d rows to pt2q_quantize_blocks with PT2Q_FLAG_S1_GIVEN, once per
+ * Gram instead of once per linear (q/k/v and gate/up share one, main.py:289-299). */
+int pt2q_s1_from_gram_batched(const float* S, int64_t lds, int m, int batch, int64_t item_stride, float* S1d,
+                              void* stream);
 
 /* compute_column_similarity_to_mean + select_next_block_ssr (reorder.py:36-61,107-143) on W
  * (n x m row-major fp32).  rem: r int64 ascending.  Writes min(b,r) entries of blk (selection

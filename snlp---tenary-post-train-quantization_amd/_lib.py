@@ -18,6 +18,7 @@ STATUS_BYTES = 256  # the status word at the head of a workspace (include/pt2q.h
 STALL_BITS = {0x1: "Gram partial-tile hand-off", 0x2: "ATQ S1/d hand-off", 0x4: "top-k pick hand-off"}
 F32, F16, BF16, I8 = 0, 1, 2, 3
 FLAG_SSR = 0x1
+FLAG_S1_GIVEN = 0x2
 AGA_NONE, AGA_ACT, AGA_HESS = 0x0, 0x10, 0x20
 AGA_MASK = 0x30
 STAGE_INIT, STAGE_GRID, STAGE_ROUND, STAGE_ITF, STAGE_AGA, STAGE_FULL = range(6)
@@ -69,6 +70,7 @@ _SIGS = {
                                 P, SZ, P]),
     "pt2q_atq_stage": (I, [I, P, I64, I, I, P, P, P, I64, P, P, I, P, P, SZ, P]),
     "pt2q_s1_from_gram": (I, [P, I64, I, P, P, P]),
+    "pt2q_s1_from_gram_batched": (I, [P, I64, I, I, I64, P, P]),
     "pt2q_ssr_select": (I, [P, I64, I, I, P, I, I, P, P, P, P, SZ, P]),
     "pt2q_dequantize": (I, [P, P, P, I, P, I, I, I, P, P]),
     "pt2q_error_feedback_workspace_bytes": (SZ, [I, I, I]),

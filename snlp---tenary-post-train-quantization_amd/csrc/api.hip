@@ -266,8 +266,12 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     }
     StageScope ts_atq(PT2Q_TIMER_ATQ, st);
     const bool act = aga == PT2Q_AGA_ACT;
-    if (act && (rc = pt2q_launch_aga_s1(1, A, lda, nullptr, m, w.S1, w.d, st)) != PT2Q_OK) return rc;
-    return pt2q_launch_atq_wide_rm(W, wdtype, ldw_in, n, m, act ? w.S1 : nullptr, w.d, max_iter, alpha, mu, T,
+    // S1 / d given (PT2Q_FLAG_S1_GIVEN: A = S1 then d, formed once per Gram) or formed here
+    const bool given = act && (flags & PT2Q_FLAG_S1_GIVEN) != 0;
+    if (act && !given && (rc = pt2q_launch_aga_s1(1, A, lda, nullptr, m, w.S1, w.d, st)) != PT2Q_OK) return rc;
+    const float* S1 = given ? A : w.S1;
+    const float* dv = given ? A + m : w.d;
+    return pt2q_launch_atq_wide_rm(W, wdtype, ldw_in, n, m, act ? S1 : nullptr, dv, max_iter, alpha, mu, T,
                                    tdtype, m, iters, w.counters, st);
   }
   {
@@ -652,7 +656,11 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
       (Hinv && ldhi < m))
     return PT2Q_E_ARG;
   int aga = flags & PT2Q_AGA_MASK;
-  if (aga != PT2Q_AGA_NONE && (!A || lda < m)) return PT2Q_E_ARG;
+  if (flags & PT2Q_FLAG_S1_GIVEN) {  // A = S1 (m) then d: only the per-channel path reads it so
+    if (aga != PT2Q_AGA_ACT || b < m || m <= 512 || !A) return PT2Q_E_ARG;
+  } else if (aga != PT2Q_AGA_NONE && (!A || lda < m)) {
+    return PT2Q_E_ARG;
+  }
   Carve c{(char*)workspace, workspace_bytes};
   BlockWs w;
   int rc;
@@ -676,6 +684,7 @@ extern "C" int pt2q_quantize_blocks_group(int count, const void* const* W, int w
                                           size_t workspace_bytes, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int aga = flags & PT2Q_AGA_MASK;
+  if (flags & PT2Q_FLAG_S1_GIVEN) return PT2Q_E_ARG;  // per-channel blocks only (pt2q_quantize_blocks)
   if (count <= 0 || count > PT2Q_GROUP_MAX || !W || !Hinv || !alpha || !mu || !T || !perm || n <= 0 ||
       m <= 0 || b <= 0 || !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0 ||
       ldw < m || ldhi < m)
@@ -711,7 +720,7 @@ extern "C" int pt2q_quantize_layer(const void* W, int wdtype, int64_t ldw, int n
                                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (!W || !X || !info_dev || N <= 0 || N > INT_MAX || m <= 0 || n <= 0 || b <= 0 ||
-      !dtype_ok(xdtype) || !dtype_ok(wdtype) || ldx < m || ldw < m)
+      !dtype_ok(xdtype) || !dtype_ok(wdtype) || ldx < m || ldw < m || (flags & PT2Q_FLAG_S1_GIVEN))
     return PT2Q_E_ARG;
   Carve c{(char*)workspace, workspace_bytes};
   int rc;
@@ -761,6 +770,14 @@ extern "C" int pt2q_s1_from_gram(const float* S, int64_t lds, int b, float* S1, 
                                  void* stream) {
   if (!S || !S1 || !d_dev || b <= 0) return PT2Q_E_ARG;
   return pt2q_launch_aga_s1(1, S, lds, nullptr, b, S1, d_dev, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_s1_from_gram_batched(const float* S, int64_t lds, int m, int batch, int64_t item_stride,
+                                         float* S1d, void* stream) {
+  if (!S || !S1d || m <= 0 || batch < 0 || lds < m || (batch > 1 && item_stride < lds * m)) return PT2Q_E_ARG;
+  if (batch == 0) return PT2Q_OK;
+  StageScope ts(PT2Q_TIMER_ATQ, (hipStream_t)stream);  // the AGA's S1 / d (quantizer.py:215-218)
+  return pt2q_launch_s1_batched(S, lds, m, batch, item_stride, S1d, (hipStream_t)stream);
 }
 
 extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const int64_t* rem, int r,

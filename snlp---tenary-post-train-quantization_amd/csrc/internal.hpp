@@ -61,6 +61,7 @@ int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* bl
                          int* status = nullptr, const Grp* grp = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
                            int* newrem, int64_t* perm_out, hipStream_t st, const Grp* grp = nullptr);
+int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st);
 int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, const int* rem,

@@ -887,8 +887,10 @@ __global__ __launch_bounds__(256) void aga_s1_kernel(int src, const float* A, lo
 // striding over whole rows read 64 rows per instruction and ran 3.3 ms at b = 13824).
 constexpr int S1W_ROWS = 32, S1W_COLS = 256;
 __global__ __launch_bounds__(256) void s1_rows_kernel(const float* A, long lda, const int* blk,
-                                                      int b, float* S1) {
+                                                      int b, float* S1, long sA, long sS) {
   __shared__ float tile[2][S1W_ROWS][S1W_COLS + 1];
+  A += blockIdx.y * sA;  // batched: item blockIdx.y (strides 0 for one item)
+  S1 += blockIdx.y * sS;
   const int tid = threadIdx.x, j0 = blockIdx.x * S1W_ROWS;
   const int nj = min(S1W_ROWS, b - j0);
   auto stage = [&](int c, int buf) {  // columns [c, c + S1W_COLS) of the workgroup's rows
@@ -931,8 +933,10 @@ __global__ __launch_bounds__(256) void s1_rows_kernel(const float* A, long lda, 
 // Blocks up to 512 columns: one workgroup per row j gathers A[blk_j][blk_l] (all loads in
 // flight at once), then one lane sums them in l order (the aga_s1_kernel order).
 __global__ __launch_bounds__(128) void s1_row_wg_kernel(const float* A, long lda, const int* blk,
-                                                        int b, float* S1) {
+                                                        int b, float* S1, long sA, long sS) {
   __shared__ float v[512];
+  A += blockIdx.y * sA;
+  S1 += blockIdx.y * sS;
   const int j = blockIdx.x;
   const float* row = A + (long)(blk ? blk[j] : j) * lda;
   for (int l = threadIdx.x; l < b; l += 128) v[l] = row[blk ? blk[l] : l];
@@ -953,8 +957,10 @@ __global__ __launch_bounds__(128) void s1_row_wg_kernel(const float* A, long lda
 
 // d = sequential sum of S1 (j ascending); S1 is staged through LDS in chunks so the serial
 // chain never waits on a global load.
-__global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, float* d) {
+__global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, float* d, long sS, long sD) {
   __shared__ float v[4096];
+  S1 += blockIdx.x * sS;  // batched: item blockIdx.x (strides 0 for one item)
+  d += blockIdx.x * sD;
   float dd = 0.0f;
   for (int j0 = 0; j0 < b; j0 += 4096) {
     const int len = min(4096, b - j0);
@@ -1079,11 +1085,11 @@ int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b,
   }
   if (src == 1) {
     if (b > 512)
-      hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, S1W_ROWS)), dim3(256), 0, st, A, lda, blk, b, S1);
+      hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(b, S1W_ROWS)), dim3(256), 0, st, A, lda, blk, b, S1, 0l, 0l);
     else
-      hipLaunchKernelGGL(s1_row_wg_kernel, dim3(b), dim3(128), 0, st, A, lda, blk, b, S1);
+      hipLaunchKernelGGL(s1_row_wg_kernel, dim3(b), dim3(128), 0, st, A, lda, blk, b, S1, 0l, 0l);
     PT2Q_LAUNCH_CHECK();
-    hipLaunchKernelGGL(s1_total_kernel, dim3(1), dim3(256), 0, st, S1, b, d);
+    hipLaunchKernelGGL(s1_total_kernel, dim3(1), dim3(256), 0, st, S1, b, d, 0l, 0l);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }
@@ -1093,6 +1099,31 @@ int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b,
   else lds += (size_t)b * sizeof(int);
   if (lds > 160 * 1024) return PT2Q_E_UNSUPPORTED;
   hipLaunchKernelGGL(aga_s1_kernel, dim3(1), dim3(256), lds, st, src, A, lda, blk, b, S1, d);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
+
+// S1 = S·1, d = 1ᵀS1 of `batch` whole m x m raw Grams (item z at G + z * sG) in one launch pair:
+// S1d[z * (m + 1) + j] = S1[j] of item z, S1d[z * (m + 1) + m] = its d.  Same kernels and order as
+// pt2q_launch_aga_s1 (src 1, no block indices), so every value is bit-identical to the per-item
+// call; the batch fills the chip where one item's serial d chain ran on one workgroup.
+int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st) {
+  if (m <= 128) {
+    for (int z = 0; z < batch; ++z) {
+      const int rc = pt2q_launch_aga_s1(1, G + z * sG, ldg, nullptr, m, S1d + (long)z * (m + 1),
+                                        S1d + (long)z * (m + 1) + m, st);
+      if (rc != PT2Q_OK) return rc;
+    }
+    return PT2Q_OK;
+  }
+  const long sS = m + 1;
+  if (m > 512)
+    hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(m, S1W_ROWS), batch), dim3(256), 0, st, G, ldg, nullptr, m,
+                       S1d, sG, sS);
+  else
+    hipLaunchKernelGGL(s1_row_wg_kernel, dim3(m, batch), dim3(128), 0, st, G, ldg, nullptr, m, S1d, sG, sS);
+  PT2Q_LAUNCH_CHECK();
+  hipLaunchKernelGGL(s1_total_kernel, dim3(batch), dim3(256), 0, st, S1d, m, S1d + m, sS, sS);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
 }

@@ -150,11 +150,13 @@ def blocks_workspace_bytes(n: int, m: int, block_size: int, flags: int) -> int:
 def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[torch.Tensor],
                     block_size: int = 128, use_ssr: bool = True, aga: int = _lib.AGA_ACT,
                     max_iter: int = 100, t_dtype=torch.int8, workspace: Optional[torch.Tensor] = None,
-                    check: bool = True) -> LayerOutput:
+                    check: bool = True, s1d: Optional[torch.Tensor] = None) -> LayerOutput:
     """The block loop given the AGA matrix A (raw Gram for variant M, damped H for variant G).
     Hinv may be None for a single block (block_size >= m: it is never read).  workspace: reused
     when large enough (pt2q_blocks_workspace_bytes); check=False leaves the status word to the
-    caller (`_lib.check_status(workspace)`; no host read here)."""
+    caller (`_lib.check_status(workspace)`; no host read here).  s1d: per-channel only (one block,
+    m > 512, variant M) -- S1 then d of A from s1_from_gram_batched, formed once per Gram; A is
+    then not read (PT2Q_FLAG_S1_GIVEN)."""
     W = _float_input(W)
     n, m = W.shape
     dev = W.device
@@ -166,6 +168,10 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[t
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     flags = (_lib.FLAG_SSR if use_ssr else 0) | aga
     nbytes = blocks_workspace_bytes(n, m, block_size, flags)
+    if s1d is not None:
+        if aga != _lib.AGA_ACT or block_size < m or m <= 512 or s1d.numel() != m + 1:
+            raise ValueError("quantize_blocks: s1d is for one-block (per-channel) variant-M loops, m + 1 floats")
+        A, flags = s1d, flags | _lib.FLAG_S1_GIVEN
     ws = workspace if workspace is not None and workspace.numel() >= nbytes else _lib.workspace(nbytes, dev)
     if Hinv is None:
         if needs_inverse(m, block_size):
@@ -181,6 +187,19 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[t
     if check:
         _lib.check_status(ws, "pt2q_quantize_blocks")
     return LayerOutput(alpha, mu, T, perm, iters)
+
+
+def s1_from_gram_batched(G: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """S1 = S·1 and d = 1ᵀS1 (quantizer.py:215-218) of every m x m raw Gram in G (batch, m, m) in
+    one launch pair: row z of the (batch, m + 1) result is S1 then d of item z, bit-identical to
+    pt2q_s1_from_gram per item (quantize_blocks(..., s1d=row) consumes it)."""
+    b, m = G.shape[0], G.shape[-1]
+    if out is None:
+        out = torch.empty((b, m + 1), dtype=torch.float32, device=G.device)
+    _lib.check(_lib.lib().pt2q_s1_from_gram_batched(_lib.ptr(G), G.stride(1), m, b, G.stride(0) if b > 1 else m * m,
+                                                    _lib.ptr(out), _lib.stream_of(G.device)),
+               "pt2q_s1_from_gram_batched")
+    return out
 
 
 GROUP_MAX = 16  # linears per pt2q_quantize_blocks_group call (PT2Q_GROUP_MAX)

@@ -425,10 +425,16 @@ class GramsFirst:
             have = self.groups.get(g)
             m = g[0]
             inv = self.batched and self.needs_inverse(m)
-            if have is None or have["G"].shape[0] != c or (have["Hinv"] is not None) != inv:
+            # per-channel groups (no inverse): S1 / d of every Gram, formed once in inverses()
+            # and shared by the unit's linears (pt2q_s1_from_gram_batched, PT2Q_FLAG_S1_GIVEN)
+            s1 = self.batched and not self.needs_inverse(m) and m > 512
+            if have is None or have["G"].shape[0] != c or (have["Hinv"] is not None) != inv or \
+                    (have.get("S1d") is not None) != s1:
                 self.groups[g] = {"G": torch.empty((c, m, m), dtype=torch.float32, device=self.dev),
                                   "Hinv": torch.empty((c, m, m), dtype=torch.float32, device=self.dev)
                                   if inv else None,
+                                  "S1d": torch.empty((c, m + 1), dtype=torch.float32, device=self.dev)
+                                  if s1 else None,
                                   "info": torch.zeros(c, dtype=torch.int32, device=self.dev)}
         for g in [g for g in self.groups if g not in count]:
             del self.groups[g]
@@ -479,6 +485,10 @@ class GramsFirst:
         if not self.batched:
             return
         caller = torch.cuda.current_stream(self.dev)
+        for g in sorted(self.groups):  # per-channel groups: S1 / d once per Gram (caller's stream)
+            grp = self.groups[g]
+            if grp.get("S1d") is not None:
+                self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
         self.inv_done = {}
         live = [g for g in sorted(self.groups) if self.groups[g]["Hinv"] is not None]
         if self.inv_stream is None and self.inv_streams > 1 and self.dev.type == "cuda":
@@ -558,12 +568,13 @@ class GramsFirst:
             runs.append(run)
             state.runs.append(run)
             Hz = grp["Hinv"][z] if grp["Hinv"] is not None else None  # None: per-channel, never read
+            S1z = grp["S1d"][z] if grp.get("S1d") is not None else None  # per-channel: S1 / d formed
             for k, W in enumerate(Ws):
                 n, m = W.shape
                 if eng.group_supported(n, m, bs, flags):
                     classes.setdefault((n, m, W.dtype), []).append((run, k, W, grp["G"][z], Hz))
                 else:  # a lone linear of an unsupported shape: its own loop on the next lane
-                    classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], Hz))
+                    classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], Hz, S1z))
         caller = torch.cuda.current_stream(self.dev)
         lanes = self.pipe.lanes
         # groups: at most `group` linears, and small enough that every lane gets work; issued
@@ -586,14 +597,15 @@ class GramsFirst:
                 self._wait_inverse(ln.stream, key)
             with torch.cuda.stream(ln.stream):
                 if ckey[0] == "one":  # stream-ordered like a group: lane workspace, status read in finish()
-                    run, k, W, G, H = chunk[0]
+                    run, k, W, G, H, S1z = chunk[0]
                     n, m = W.shape
                     nbytes = eng.blocks_workspace_bytes(n, m, bs, flags)
                     okey = (id(ln), W.device)
                     if okey not in self.ows or self.ows[okey].numel() < nbytes:
                         self.ows[okey] = lib.workspace(nbytes, self.dev)
                     ws = self.ows[okey]
-                    run.outs[k] = eng.quantize_blocks(W, G, H, bs, ssr, lib.AGA_ACT, mi, workspace=ws, check=False)
+                    run.outs[k] = eng.quantize_blocks(W, G, H, bs, ssr, lib.AGA_ACT, mi, workspace=ws, check=False,
+                                                      s1d=S1z)
                     state.statuses.append(lib.status_view(ws).clone())
                     continue
                 n, m, _ = ckey

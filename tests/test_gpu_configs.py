@@ -229,3 +229,26 @@ def test_per_channel_zero_block(pt2q, m, dt):
     torch.cuda.synchronize()
     assert int(host(out.iters)[0]) == 0
     assert not host(out.T).any() and not host(out.alpha).any() and not host(out.mu).any()
+
+
+@pytest.mark.parametrize("m,batch", [(5120, 3), (1000, 2), (300, 2), (100, 3)])
+def test_s1_batched_equals_per_item_and_given(pt2q, m, batch):
+    """pt2q_s1_from_gram_batched (S1 = S·1, d = 1ᵀS1 of several Grams in one launch pair) ==
+    pt2q_s1_from_gram per item, bit for bit; a per-channel block loop fed the formed S1 / d
+    (PT2Q_FLAG_S1_GIVEN) == the same loop forming them itself (quantizer.py:215-218)."""
+    Gs = torch.stack([pt2q.gram(pt2q.fill_synthetic((384, m), 31 + z, std=1.0, outliers=True).half())
+                      for z in range(batch)]).contiguous()
+    S1d = pt2q.engine.s1_from_gram_batched(Gs)
+    for z in range(batch):
+        S1 = torch.empty(m, device=DEV)
+        d = torch.empty(1, device=DEV)
+        rc = pt2q._lib.lib().pt2q_s1_from_gram(pt2q._lib.ptr(Gs[z]), m, m, pt2q._lib.ptr(S1), pt2q._lib.ptr(d),
+                                               pt2q._lib.stream_of(Gs.device))
+        assert rc == 0
+        assert bits_equal(host(S1d[z, :m]), host(S1)) and bits_equal(host(S1d[z, m:]), host(d))
+    if m > 512:
+        Wd = pt2q.fill_synthetic((96, m), 77, std=0.02).to(torch.bfloat16)
+        a = pt2q.engine.quantize_blocks(Wd, Gs[1], None, block_size=m)
+        b = pt2q.engine.quantize_blocks(Wd, Gs[1], None, block_size=m, s1d=S1d[1])
+        for x, y in ((a.T, b.T), (a.alpha, b.alpha), (a.mu, b.mu), (a.iters, b.iters)):
+            assert bits_equal(host(x.float()), host(y.float()))
