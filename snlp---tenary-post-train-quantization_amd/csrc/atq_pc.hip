@@ -97,20 +97,22 @@ struct PcRows {
   const char* rowp[4];  // the wave's 4 rows (clamped)
   lds_char* ring;       // wave-private: 2 stages, then the masks [chunk][lane] (Z, S)
   lds_char* masks;
-  u32x4 stg[G::PIECES];  // next chunk's pieces (registers, one chunk ahead)
+  int par = 0;           // parity of the stream position q (which runs on across passes)
+  int c3 = 0;            // chunk of q + 3 (= (q + 3) % nc, advanced incrementally)
+  u32x4 stg[2][G::PIECES];  // the next two chunks' pieces (registers, in flight)
 
-  PT2Q_DEV void load_chunk(int c) {  // global -> registers: piece p = row (p % 4), 1 KiB part p / 4
-#pragma unroll
+  PT2Q_DEV void load_chunk(int c, u32x4 (&dst)[G::PIECES]) const {  // global -> registers: piece p =
+#pragma unroll                                                       // row p % 4, 1 KiB part p / 4
     for (int p = 0; p < G::PIECES; ++p) {
       const long off = (long)c * G::CHUNK_B + (p / 4) * 1024 + 16 * lane;
       const long lim = (long)A.m * G::E;  // m % (16 / E) == 0: pieces never straddle the row end
-      stg[p] = *(const u32x4*)(rowp[p % 4] + (off < lim ? off : 0));
+      dst[p] = *(const u32x4*)(rowp[p % 4] + (off < lim ? off : 0));
     }
   }
-  PT2Q_DEV void store_stage(int st) {  // registers -> LDS stage st
+  PT2Q_DEV void store_stage(int st, const u32x4 (&src)[G::PIECES]) {  // registers -> LDS stage st
 #pragma unroll
     for (int p = 0; p < G::PIECES; ++p)
-      *(lds_t<u32x4>*)(ring + st * G::STAGE + (p % 4) * G::ROWB + (p / 4) * 1024 + 16 * lane) = stg[p];
+      *(lds_t<u32x4>*)(ring + st * G::STAGE + (p % 4) * G::ROWB + (p / 4) * 1024 + 16 * lane) = src[p];
   }
   // this lane's 32 elements of the chunk in stage st (element j = column c*512 + l + 16 j)
   PT2Q_DEV void read_stage(int st, float (&x)[PC_J]) const {
@@ -123,22 +125,33 @@ struct PcRows {
       x[j] = PcIn<TI>::cvt(raw);
     }
   }
-  // One streamed pass: f.template chunk<TAIL>(c, x, jn) for every chunk in order (jn: this lane's
-  // elements in the chunk, < 32 only in the last chunk).  Prologue: chunk 0 in the stage, chunk 1
-  // in registers.  Every pass restarts the stream (the ring is wave-private: no barriers).
+  // The stream: at the start of step q, stage q & 1 holds chunk q, register set (q + 1) & 1 chunk
+  // q + 1 and set q & 1 chunk q + 2 (both in flight).  Every pass reads the same chunks in the
+  // same order, so the stream wraps from one pass into the next without a cold restart, and each
+  // chunk's loads are issued two chunks ahead.
+  PT2Q_DEV void prime() {
+    load_chunk(0, stg[0]);
+    store_stage(0, stg[0]);
+    load_chunk(1 % nc, stg[1]);
+    load_chunk(2 % nc, stg[0]);
+    c3 = 3 % nc;
+  }
+  template <int P>
+  PT2Q_DEV void step(float (&x)[PC_J]) {  // P = q & 1 (static: the register sets never move)
+    read_stage(P, x);
+    store_stage(P ^ 1, stg[P ^ 1]);  // chunk q + 1 (stage of chunk q - 1: read)
+    load_chunk(c3, stg[P ^ 1]);      // chunk q + 3
+    c3 = c3 + 1 == nc ? 0 : c3 + 1;
+  }
+  // One streamed pass: f.template chunk<TAIL>(rows, c, x, jn, masks) for every chunk in order (jn:
+  // this lane's elements in the chunk, < 32 only in the last chunk).  No barriers: the ring is
+  // wave-private.
   template <typename F>
   PT2Q_DEV void pass(F&& f) {
-    load_chunk(0);
-    store_stage(0);
-    if (nc > 1) load_chunk(1);
-    for (int c = 0; c < nc; ++c) {
-      const int st = c & 1;
+    for (int c = 0; c < nc; ++c, par ^= 1) {
       float x[PC_J];
-      read_stage(st, x);
-      if (c + 1 < nc) {
-        store_stage(st ^ 1);  // chunk c+1 (its stage was last read for chunk c-1: done)
-        if (c + 2 < nc) load_chunk(c + 2);
-      }
+      if (par) step<1>(x);
+      else step<0>(x);
       u32x2 mk = {0u, 0u};
       if constexpr (std::decay_t<F>::MASKS_IN) mk = *mask_at(c);
       if ((c + 1) * PC_COLS <= A.m) {  // wave-uniform
@@ -163,16 +176,39 @@ struct PcRegs {
   bool valid;
   uint32_t wr[16 * NW];
   u32x2 M[NW];
-  PT2Q_DEV void load(const char* row) {
-    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-    const uint16_t* w = (const uint16_t*)row + l;
+  // W into the registers: 16-byte loads of the wave's 4 rows, staged through a wave-private
+  // two-stage LDS ring (PcRows' geometry, loads two chunks ahead), each lane reading back its
+  // strided elements.  (One 2-byte load per element, 320 per lane in batches of 16 with a wait
+  // after each, left the waves parked 34 % of their cycles.)
+  PT2Q_DEV void load(const char* const (&rowp)[4], lds_char* ring) {
+    typedef PcGeom<TI> G;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 stg[2][4];
+    auto ld = [&](int c, u32x4 (&dst)[4]) {
 #pragma unroll
-    for (int p = 0; p < 16 * NW; ++p) {
-      const int s = 2 * p;  // columns l + 16 s and l + 16 (s + 1): 16-bit loads into the two halves
-      u16x2 v;
-      v.x = w[16 * s];
-      v.y = w[16 * s + 16];
-      wr[p] = __builtin_bit_cast(uint32_t, v);
+      for (int p = 0; p < 4; ++p) dst[p] = *(const u32x4*)(rowp[p] + (long)c * G::CHUNK_B + 16 * lane);
+    };
+    auto st = [&](int sg, const u32x4 (&src)[4]) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) *(lds_t<u32x4>*)(ring + sg * G::STAGE + p * G::ROWB + 16 * lane) = src[p];
+    };
+    ld(0, stg[0]);
+    st(0, stg[0]);
+    if (NW > 1) ld(1, stg[1]);
+    if (NW > 2) ld(2, stg[0]);
+#pragma unroll
+    for (int c = 0; c < NW; ++c) {
+      const lds_char* b = ring + (c & 1) * G::STAGE + r * G::ROWB + 2 * l;
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {  // elements 2p, 2p + 1 of the chunk: columns +32p, +32p + 16
+        const uint32_t lo = *(const lds_t<uint16_t>*)(b + 64 * p);
+        const uint32_t hi = *(const lds_t<uint16_t>*)(b + 64 * p + 32);
+        wr[16 * c + p] = lo | (hi << 16);
+      }
+      if (c + 1 < NW) {
+        st((c + 1) & 1, stg[(c + 1) & 1]);
+        if (c + 3 < NW) ld(c + 3, stg[(c + 1) & 1]);
+      }
     }
   }
   // Makes a chunk's 16 packed registers opaque to the optimiser: without it, LLVM unpacks every
@@ -369,63 +405,48 @@ PT2Q_DEV void pc_rows(R& rows) {
   }
 }
 
-// Row groups (4 consecutive rows, one wave) are claimed dynamically: the grid is what the chip
-// holds at once, and each wave takes the next group from a counter (counters[1], zeroed with
-// counters[0] by the caller) until none is left -- the ITF iteration counts of the groups vary
-// (5-11), so a static grid's last round of waves ran far emptier than its first.
-PT2Q_DEV int pc_claim(const PcArgs& A, int lane) {
-  int g = 0;
-  if (lane == 0) g = atomicAdd(&A.counters[1], 1);
-  return __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-}
-
+// One row group (4 consecutive rows) per wave, a static grid.  (Claiming groups dynamically from a
+// counter, so a wave takes the next group when its ITF ends, measured slower: the loop around the
+// unrolled register-resident body raised its spills 47 -> 246 VGPRs, 230 -> 264 us per 5120-column
+// linear; the streamed kernel 498 -> 517 us per 5120 x 13824.)
 template <class TI, class TO>
 __global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
   extern __shared__ __attribute__((aligned(16))) char pc_lds[];
   typedef PcGeom<TI> G;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nc = (A.m + PC_COLS - 1) / PC_COLS;
-  const int groups = (A.n + 3) / 4;
-  for (int g = pc_claim(A, lane); g < groups; g = pc_claim(A, lane)) {
-    PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr, {}};
-    const int row0 = g * 4;
-    R.i = row0 + R.r;
-    R.valid = R.i < A.n;
-    if (!R.valid) R.i = 0;
+  PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr};
+  const int row0 = ((int)blockIdx.x * PC_WAVES + wave) * 4;
+  R.i = row0 + R.r;
+  R.valid = R.i < A.n;
+  if (!R.valid) R.i = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int iq = row0 + q < A.n ? row0 + q : 0;
-      R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
-    }
-    R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
-    R.masks = R.ring + 2 * G::STAGE;
-    pc_rows<TO>(R);
+  for (int q = 0; q < 4; ++q) {
+    const int iq = row0 + q < A.n ? row0 + q : 0;
+    R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
   }
+  R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
+  R.masks = R.ring + 2 * G::STAGE;
+  R.prime();
+  pc_rows<TO>(R);
 }
 
 constexpr int PCR_WAVES = 4;
 template <class TI, class TO, int NW>
 __global__ __launch_bounds__(64 * PCR_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void atq_pcr_kernel(PcArgs A) {
-  const int lane = threadIdx.x & 63;
-  const int groups = (A.n + 3) / 4;
-  for (int g = pc_claim(A, lane); g < groups; g = pc_claim(A, lane)) {
-    PcRegs<TI, NW> R{A, lane, lane & 15, lane >> 4, 0, false, {}, {}};
-    R.i = g * 4 + R.r;
-    R.valid = R.i < A.n;
-    if (!R.valid) R.i = 0;
-    R.load((const char*)A.W + (long)R.i * A.ldw * 2);
-    pc_rows<TO>(R);
-  }
-}
-
-// workgroups the chip holds at once (occupancy x CUs), at most `need`
-template <typename K>
-int pc_grid(K kern, int threads, size_t lds, int need) {
-  int dev = 0, cus = 256, per_cu = 1;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  return std::max(1, std::min(need, per_cu * cus));
+  typedef PcGeom<TI> G;
+  __shared__ __attribute__((aligned(16))) char ring_lds[PCR_WAVES * 2 * G::STAGE];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  PcRegs<TI, NW> R{A, lane, lane & 15, lane >> 4, 0, false, {}, {}};
+  const int row0 = ((int)blockIdx.x * PCR_WAVES + wave) * 4;
+  R.i = row0 + R.r;
+  R.valid = R.i < A.n;
+  if (!R.valid) R.i = 0;
+  const char* rowp[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rowp[q] = (const char*)A.W + (long)(row0 + q < A.n ? row0 + q : 0) * A.ldw * 2;
+  R.load(rowp, (lds_char*)ring_lds + wave * 2 * G::STAGE);
+  pc_rows<TO>(R);
 }
 
 }  // namespace
@@ -447,9 +468,8 @@ int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const 
   PcArgs A{W, ldw, n, m, S1, d, max_iter, alpha, mu, T, ldt, iters, counters};
   if (m == PC_COLS * PCR_NW && wdtype == PT2Q_BF16 && pt2q_tuning().atq_pc_regs) {
     auto gor = [&](auto ti, auto to) {
-      auto kern = atq_pcr_kernel<decltype(ti), decltype(to), PCR_NW>;
-      const int grid = pc_grid(kern, 64 * PCR_WAVES, 0, ceil_div(n, 4 * PCR_WAVES));
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PCR_WAVES), 0, st, A);
+      hipLaunchKernelGGL((atq_pcr_kernel<decltype(ti), decltype(to), PCR_NW>), dim3(ceil_div(n, 4 * PCR_WAVES)),
+                         dim3(64 * PCR_WAVES), 0, st, A);
       PT2Q_LAUNCH_CHECK();
       return PT2Q_OK;
     };
@@ -461,8 +481,7 @@ int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const 
     typedef decltype(ti) TI;
     typedef decltype(to) TO;
     const size_t lds = PC_WAVES * pc_wave_bytes(PcGeom<TI>::STAGE, ceil_div(m, PC_COLS));
-    auto kern = atq_pc_kernel<TI, TO>;
-    hipLaunchKernelGGL(kern, dim3(pc_grid(kern, 64 * PC_WAVES, lds, grid)), dim3(64 * PC_WAVES), lds, st, A);
+    hipLaunchKernelGGL((atq_pc_kernel<TI, TO>), dim3(grid), dim3(64 * PC_WAVES), lds, st, A);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };
