@@ -190,6 +190,25 @@ __global__ void pack_kernel(const int8_t* T, long count, uint8_t* out) {
   out[q] = v;
 }
 
+// 16 codes per thread (16-byte load, 4-byte store), the same bytes as pack_kernel: per byte
+// c = T + 1 in {0, 1, 2} without carries between bytes ((b & 0x7f) + 1: -1 -> 0x80, 0 -> 1, 1 -> 2,
+// then & 3), then the four 2-bit fields of a word folded into its low byte.
+__global__ void pack16_kernel(const uint4* T, long n16, uint32_t* out) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n16) return;
+  const uint4 w = T[q];
+  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t x = ((v[k] & 0x7f7f7f7fu) + 0x01010101u) & 0x03030303u;
+    x |= x >> 6;
+    x |= x >> 12;
+    r |= (x & 0xffu) << (8 * k);
+  }
+  out[q] = r;
+}
+
 __global__ void unpack_kernel(const uint8_t* in, long count, int8_t* T) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
@@ -348,6 +367,13 @@ extern "C" int pt2q_pack_ternary(const int8_t* T, int64_t count, uint8_t* packed
   if (count < 0 || !T || !packed) return PT2Q_E_ARG;
   long nb = (count + 3) / 4;
   if (nb == 0) return PT2Q_OK;
+  if (count % 16 == 0 && ((uintptr_t)T & 15) == 0 && ((uintptr_t)packed & 3) == 0) {
+    const long n16 = count / 16;
+    hipLaunchKernelGGL(pack16_kernel, dim3(ceil_div(n16, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)T, n16, (uint32_t*)packed);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   hipLaunchKernelGGL(pack_kernel, dim3(ceil_div(nb, 256)), dim3(256), 0, (hipStream_t)stream, T,
                      (long)count, packed);
   PT2Q_LAUNCH_CHECK();

@@ -392,8 +392,10 @@ def test_fill_synthetic_matches_numpy(pt2q):
     np.testing.assert_array_equal(host(b), synth.activations(99, 64, 1000))
 
 
-def test_pack_unpack_matches_reference_layout(pt2q):
-    T = (synth.centered24(5, 1001).astype(np.int64) % 3 - 1).astype(np.int8)
+@pytest.mark.parametrize("count", [1001, 4096 * 3])
+def test_pack_unpack_matches_reference_layout(pt2q, count):
+    """1001 codes: the per-byte kernel; 12288 (a multiple of 16): the 16-codes-per-thread kernel."""
+    T = (synth.centered24(5, count).astype(np.int64) % 3 - 1).astype(np.int8)
     packed, shape = pt2q.pack_ternary(cuda(T))
     # utils.py:202-217 layout: {-1,0,1} -> {0,1,2}, element 4q+s at bits 2s of byte q
     flat = np.concatenate([T + 1, np.zeros((-len(T)) % 4, np.int8)]).astype(np.uint8).reshape(-1, 4)
