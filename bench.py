@@ -162,15 +162,20 @@ def config_runs(a, dev):
                            "--lanes", str(a.lanes), "--inv-streams", str(a.inv_streams)]))
         io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[b.io_dtype]
         try:
+            tw = time.perf_counter()
             w = ModelStep(b, 0, 1, dev, io)
             for _ in range(b.warmup):
                 w.step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            step_ms = []
             for _ in range(b.steps):
+                ts = time.perf_counter()
                 w.step()
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
+                step_ms.append(1e3 * (time.perf_counter() - ts))
             s = (time.perf_counter() - t0) / b.steps
+            log(0, f"config {name}: setup + warmup {t0 - tw:.1f}s, steps {[round(x, 1) for x in step_ms]} ms")
             cols = sharding.units_cols(w.units)
             # live roofline of this config: phase walls + one-lane stage busy times (outside the timing)
             ph = w.phase_step()
@@ -543,7 +548,7 @@ def model_work(units, bs, io_bytes=2, ssr=True):
     """Algorithmic work of one model step per stage: flops and HBM bytes.
     Per-channel units (bs >= m: one block) have no inverse, no error feedback and no SSR pass."""
     w = {k: 0.0 for k in ("gram_fl_2nm2", "gram_fl_done", "gram_bytes", "chol_fl", "ef_fl", "ef_bytes",
-                          "ssr_bytes", "atq_bytes", "setup_bytes", "out_bytes")}
+                          "ssr_bytes", "atq_bytes", "atq_valu", "setup_bytes", "out_bytes")}
     for _, lins, N in units:
         m = lins[0][2]
         w["gram_fl_2nm2"] += 2.0 * N * m * m          # §8(d) basis: the full product
@@ -561,12 +566,29 @@ def model_work(units, bs, io_bytes=2, ssr=True):
                 # columns) plus block 0's stand-alone w-bar pass (m columns); later blocks' w-bar
                 # partials come out of the error feedback (no pass over W, DESIGN.md §3 CHUNK128)
                 w["ssr_bytes"] += 4.0 * n * (2 * m + rsum)
-            # every block's W columns read (fp32) and codes written; the error term E written
-            # for every block that leaves columns behind
-            w["atq_bytes"] += 5.0 * n * m + (4.0 * n * (m - (m - (nblk - 1) * bs)) if nblk > 1 else 0.0)
-            w["setup_bytes"] += (io_bytes + 4.0) * n * m  # W in, feature-major fp32 copy out
-            w["out_bytes"] += 2.0 * n * m              # codes transposed back (int8 in + out)
+            if nblk > 1:
+                # every block's W columns read (fp32) and codes written; the error term E written
+                # for every block that leaves columns behind
+                w["atq_bytes"] += 5.0 * n * m + 4.0 * n * (m - (m - (nblk - 1) * bs))
+                w["setup_bytes"] += (io_bytes + 4.0) * n * m  # W in, feature-major fp32 copy out
+                w["out_bytes"] += 2.0 * n * m              # codes transposed back (int8 in + out)
+            else:
+                # per-channel: the caller's W read in place (io_bytes) and int8 codes written, no
+                # layout copies (api.hip run_blocks); the ITF passes are VALU work (atq_pc.hip)
+                w["atq_bytes"] += (io_bytes + 1.0) * n * m
+                w["atq_valu"] += PC_VALU_PER_ELEM * n * m
+        if nblk == 1:
+            w["atq_bytes"] += 4.0 * m * m                  # S1 = S·1 over the unit's Gram, once per unit
     return w
+
+
+# VALU lane-operations per element of a per-channel ATQ row (atq_pc.hip, counted from the
+# register kernel's ISA: sum w 2, sum |w - mu| 3, init 10, one ITF pass 10-11 x ~7 passes (the
+# wave's slowest row, tools/itf_dist), AGA + codes 14), and the chip's VALU rate: 256 CUs x 4
+# SIMDs x 32 lanes per cycle at 2.4 GHz (MI355X_MICROARCH.md: a wave64 VALU op issues over 2
+# cycles on a SIMD-32).
+PC_VALU_PER_ELEM = 106.0
+MI355X_VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
 STAGE_KERNELS = {"gram": "gram16b_kernel / gram_streamk_kernel", "inverse": "chol_* + rank_update2 + gemmx_kernel",
@@ -610,6 +632,10 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
     if b["atq"] > 0:
         st["atq"] = {"bound": "hbm/latency", "kernel_busy_s": b["atq"], "bytes": work["atq_bytes"],
                      "frac_hbm": work["atq_bytes"] / b["atq"] / HBM, "source": src}
+        if work["atq_valu"] > 0:  # per-channel rows: VALU-bound ITF passes
+            st["atq"].update(bound="valu", valu_lane_ops=work["atq_valu"],
+                             frac_valu=work["atq_valu"] / b["atq"] / (MI355X_VALU_PEAK_TOPS * 1e12),
+                             valu_peak_tops=MI355X_VALU_PEAK_TOPS)
     io = b["setup"] + b["out"]
     if io > 0:
         st["layout"] = {"bound": "hbm", "kernel_busy_s": io, "bytes": work["setup_bytes"] + work["out_bytes"],
@@ -623,12 +649,14 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
                     cc[stage] += ms / 1e3
         st["cross_check"] = {"kernel_busy_s": cc, "source": "committed:profiles/stage_kernels.json "
                                                             "(rocprof kernel trace of a one-lane step)"}
-    floor = (work["gram_fl_done"] / GP + work["chol_fl"] / F32 + work["ef_fl"] / F32 +
-             (work["ef_bytes"] + work["ssr_bytes"] + work["atq_bytes"] + work["setup_bytes"] + work["out_bytes"]) / HBM
+    atq_floor = max(work["atq_bytes"] / HBM, work["atq_valu"] / (MI355X_VALU_PEAK_TOPS * 1e12))
+    floor = (work["gram_fl_done"] / GP + work["chol_fl"] / F32 + work["ef_fl"] / F32 + atq_floor +
+             (work["ef_bytes"] + work["ssr_bytes"] + work["setup_bytes"] + work["out_bytes"]) / HBM
              ) / max(world, 1)
     st["step"] = {"floor_s": floor, "frac": floor / (ms_per_step * 1e-3),
                   "floor": "Gram work done at the MFMA peak of its input type + Cholesky inverse and EF flops at "
-                           "the f32 MFMA peak + EF/SSR/ATQ/layout bytes at HBM peak, stages back to back, / ranks"}
+                           "the f32 MFMA peak + EF/SSR/layout bytes at HBM peak + ATQ at the larger of its bytes at "
+                           "HBM peak and (per-channel) its VALU work at the VALU peak, stages back to back, / ranks"}
     # the dominant stage: the largest live busy time, against the roofline that bounds it
     dom = max(("gram", "inverse", "ssr", "atq", "ef"), key=lambda k: b[k])
     d = {"stage": dom, "kernels": STAGE_KERNELS[dom], "busy_s": b[dom]}
@@ -638,6 +666,9 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
     elif dom == "inverse" or dom == "ef":
         fl = work["chol_fl"] if dom == "inverse" else work["ef_fl"]
         d.update(bound="mfma", unit="TFLOP/s", achieved=fl / b[dom] / 1e12, peak=MI355X_F32_MFMA_PEAK_TFLOPS)
+    elif dom == "atq" and work["atq_valu"] > 0:
+        d.update(bound="valu", unit="Tlane-op/s", achieved=work["atq_valu"] / b[dom] / 1e12, peak=MI355X_VALU_PEAK_TOPS,
+                 hbm_frac=work["atq_bytes"] / b[dom] / HBM)
     else:
         by = work["ssr_bytes"] if dom == "ssr" else work["atq_bytes"]
         d.update(bound="hbm", unit="GB/s", achieved=by / b[dom] / 1e9, peak=MI355X_HBM_PEAK_GBS)
