@@ -194,7 +194,7 @@ bool carve_blocks(Carve& c, int n, int m, int b, BlockWs& w, int flags = 0) {
   // [2k, 2k+1] ATQ; [2B+2k, 2B+2k+1] top-k/S1 sync; [4B ..) the wbar hand-off counters
   w.counters = c.take<int>((size_t)4 * B + pt2q_ssr_counter_ints(n));
   w.iters = c.take<int>((size_t)B);
-  w.iters_part = c.take<int>((size_t)ceil_div(n, 16));
+  w.iters_part = c.take<int>((size_t)ceil_div(n, 16) * 4);  // one per ATQ wave (4 waves of 4 rows per workgroup)
   w.hb = w.hS = nullptr;
   if (hess_wide(flags, bb)) {
     w.hb = c.take<float>((size_t)bb * bb);

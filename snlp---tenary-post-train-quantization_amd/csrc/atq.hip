@@ -331,7 +331,7 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   return it;
 }
 
-// Iteration count of a block: one store per workgroup (iters_part), reduced by the post / fixup
+// Iteration count of a block: one store per wave (iters_part), reduced by the post / fixup
 // launch -- not one atomic per wave on a single word (1024 atomics serialise at the memory side
 // and hold the kernel's end for ~10 us).
 // S1[j] = l-ascending sum of G[blk_j][blk_l], d = j-ascending sum of S1 (the s1_block order):
@@ -396,23 +396,39 @@ struct CoeffArgs {
   long ldc;
   int per_k;  // coefficient workgroups per k row (COEF_SPAN columns e each)
 };
-constexpr int COEF_SPAN = 1024;  // columns e per coefficient workgroup (4 per lane)
+// columns e per coefficient workgroup: 16 per lane (4 x 16-byte index loads, 16 gathers in flight
+// before the divisions); 1024 per workgroup (4 per lane) gave 4x the workgroups, each parked on
+// two dependent load round trips for a few divisions
+constexpr int COEF_SPAN = 4096;
 
 PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
   const int k = cb / K.per_k;
   if (k >= K.bs) return;
-  const int e0 = (cb - k * K.per_k) * COEF_SPAN + 4 * (int)threadIdx.x;
+  const int base = (cb - k * K.per_k) * COEF_SPAN + 4 * (int)threadIdx.x;  // + 1024 j + v
   const long rowb = (long)A.blk[k] * K.ldh;
+  int re[16];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = base + 1024 * j;
+    if (e + 3 < K.nr && (((uintptr_t)(K.rem + e)) & 15) == 0) {
+      const int4 v = *(const int4*)(K.rem + e);
+      re[4 * j] = v.x, re[4 * j + 1] = v.y, re[4 * j + 2] = v.z, re[4 * j + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) re[4 * j + v] = e + v < K.nr ? K.rem[e + v] : 0;
+    }
+  }
   const float dg = clampmin(K.Hinv[rowb + A.blk[k]]);
-  int re[4];
+  float h[16];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) re[u] = e0 + u < K.nr ? K.rem[e0 + u] : 0;
-  float h[4];
+  for (int u = 0; u < 16; ++u) h[u] = K.Hinv[rowb + re[u]];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) h[u] = K.Hinv[rowb + re[u]];
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (e0 + u < K.nr) K.C[(long)k * K.ldc + e0 + u] = h[u] / dg;
+    for (int v = 0; v < 4; ++v) {
+      const int e = base + 1024 * j + v;
+      if (e < K.nr) K.C[(long)k * K.ldc + e] = h[4 * j + v] / dg;
+    }
 }
 
 template <int NS, bool F>
@@ -442,19 +458,16 @@ PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int
     coeff_part(A, K, (int)blockIdx.x - A.nS1 - rowgrid);
     return;
   }
-  __shared__ int wmax[WAVES];
   const int wave = threadIdx.x >> 6;
   const int rb = (int)blockIdx.x - A.nS1;
   const int row0 = rb * ROWS_PER_WG + wave * ROWS_PER_WAVE;
   const int it = block_rows<NS, F>(A, row0, false, true);
-  if (!A.iters) return;
-  if ((threadIdx.x & 63) == 0) wmax[wave] = it;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-    if (A.iters_part) A.iters_part[rb] = mx;
-    else atomicMax(A.iters, mx);
-  }
+  if (!A.iters || (threadIdx.x & 63) != 0) return;
+  // one store per wave, no barrier: a wave whose rows converged early leaves at once instead of
+  // holding its slot until the workgroup's slowest wave (the block-ATQ waves were parked 59 % of
+  // their cycles, profiles/r05j_atq7b_pmc.txt)
+  if (A.iters_part) A.iters_part[rb * WAVES + wave] = it;
+  else atomicMax(A.iters, it);
 }
 
 // *iters = max of the block kernel's per-workgroup maxima, or 0 for an all-zero block (ITF did
@@ -478,7 +491,7 @@ PT2Q_DEV void finish_iters(const BlockArgs& A, int nparts) {
 template <int NS>
 __global__ __launch_bounds__(256) void atq_finish_kernel(BlockArgs A0, int rowgrid, Grp g) {
   const BlockArgs A = at_linear(A0, g);
-  finish_iters(A, rowgrid);
+  finish_iters(A, rowgrid * WAVES);
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
   if (A.iters && !A.iters_part && threadIdx.x == 0) *A.iters = 0;

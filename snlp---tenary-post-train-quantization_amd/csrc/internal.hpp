@@ -40,7 +40,7 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,
                           hipStream_t st, const float* Hinv = nullptr, long ldh = 0,
                           const int* rem = nullptr, int nr = 0, float* C = nullptr, long ldc = 0,
-                          int* iters_part = nullptr,  // ceil(n/16) ints of scratch, nullable
+                          int* iters_part = nullptr,  // 4 ceil(n/16) ints of scratch (one per wave), nullable
                           // variant M, b <= 128: S1/d (into S1, d) formed inside the launch from
                           // the raw Gram G; s1sync: 2 zeroed ints
                           const float* G = nullptr, long ldg = 0, int* s1sync = nullptr,
