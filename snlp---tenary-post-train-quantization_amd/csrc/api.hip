@@ -50,6 +50,7 @@ Pt2qTuning load_tuning() {
   // ef2 knock-outs (tools/ef2_knock.sh; results garbage): only a development build
   // (make DEV_PROBES=1) reads this, so a stray variable cannot corrupt a release library's results
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
+  geti("PT2Q_ATQ_PROBE", t.atq_probe);
 #endif
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);

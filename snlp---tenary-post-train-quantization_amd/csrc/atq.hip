@@ -21,6 +21,7 @@ namespace {
 constexpr int ROWS_PER_WAVE = 4;
 constexpr int WAVES = 4;
 constexpr int ROWS_PER_WG = ROWS_PER_WAVE * WAVES;
+PT2Q_DEV int ceil_div_dev(int a, int b) { return (a + b - 1) / b; }
 
 // FULL: b == 16 * NS (every lane holds NS elements; no per-element range checks)
 template <int NS, bool FULL = false>
@@ -196,6 +197,7 @@ struct BlockArgs {
   float* dw;
   int* status;       // stall reports (nullable)
   long cap;          // polls before a wait gives up
+  int probe;         // development knock-outs (pt2q_tuning().atq_probe; 0 in release builds)
 };
 
 // Grouped launch (grid.z = linear): this linear's pointers -- its workspace slice, its raw Gram.
@@ -297,8 +299,8 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
   bool zero = row_init(R, wsum, &a, &m);
   if (count_zero && valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
   int it = 0;
-  if (!skip_itf) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
-  if (A.S1 && A.nS1 > 0) {  // S1 / d from this launch's leading workgroups (write-through)
+  if (!skip_itf && !(A.probe & 4)) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
+  if (A.S1 && A.nS1 > 0 && !(A.probe & 1)) {  // S1 / d from this launch's leading workgroups (write-through)
     int ready = 1;
     if ((threadIdx.x & 63) == 0) ready = wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, nullptr, 0);
     ready = __builtin_amdgcn_readfirstlane(ready);
@@ -330,6 +332,98 @@ PT2Q_DEV int block_rows(const BlockArgs& A, int row0, bool skip_itf, bool count_
     }
   return it;
 }
+
+// RG row groups per wave (rows base + 16 g + r, g < RG): every group's gathers are issued before
+// the first group's arithmetic, the block indices and S1 / d are loaded once for all of them.  The
+// block ATQ is bound by these load round trips, not by its ITF arithmetic (knock-outs,
+// tools/atq_knock.sh: skipping ITF altogether moved a grouped 7B launch 100 -> 99 us), so one
+// wave carrying several groups' loads at once is what shortens it.  Per row, the values and their
+// order are block_rows' (same Row arithmetic), so the bits are the same.
+template <int NS, bool F, int RG>
+PT2Q_DEV int block_rows_rg(const BlockArgs& A, int base) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane >> 4, l = lane & 15;
+  int colrow[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = l + 16 * s;
+    colrow[s] = A.blk[k < A.b ? k : 0];
+  }
+  float v[RG][NS];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int i = base + 16 * g + r;
+    const int ic = i < A.n ? i : 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      v[g][s] = (A.probe & 32) ? (float)(ic + s) : A.Wt[(long)colrow[s] * A.ldw + ic];
+  }
+  const bool s1_now = A.S1 && A.nS1 == 0;
+  float S1[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = l + 16 * s;
+    S1[s] = s1_now ? A.S1[k < A.b ? k : 0] : 0.0f;
+    S1[s] = k < A.b ? S1[s] : 0.0f;
+  }
+  float dv = s1_now ? *A.d : 0.0f;
+  int itmax = 0;
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int i = base + 16 * g + r;
+    const bool valid = i < A.n;
+    Row<NS, F> R;
+    R.l = l;
+    R.b = A.b;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) R.w[s] = (valid && l + 16 * s < A.b) ? v[g][s] : 0.0f;
+    const float wsum = row_sum_w(R);
+    float a, m;
+    const bool zero = row_init(R, wsum, &a, &m);
+    if (valid && l == 0 && zero) atomicAdd(&A.counters[0], 1);
+    int it = 0;
+    if (!(A.probe & 4)) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
+    itmax = max(itmax, it);
+    if (g == 0 && A.S1 && A.nS1 > 0 && !(A.probe & 1)) {  // S1 / d from the leading workgroups, once
+      int ready = 1;
+      if (lane == 0) ready = wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, nullptr, 0);
+      ready = __builtin_amdgcn_readfirstlane(ready);
+      __builtin_amdgcn_wave_barrier();
+      if (ready) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const int k = l + 16 * s;
+          const float x = __hip_atomic_load(&A.S1w[k < A.b ? k : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          S1[s] = k < A.b ? x : 0.0f;
+        }
+        dv = __hip_atomic_load(A.dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        s1_local<NS>(A, l, S1, &dv);
+      }
+    }
+    if (A.S1) row_aga(R, S1, dv, &a, &m);
+    if (valid && !(A.probe & 8)) {
+      if (l == 0) {
+        A.alpha[i] = a;
+        A.mu[i] = m;
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if (R.has(s)) {
+          const int k = l + 16 * s;
+          A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
+          if (A.Et) A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
+        }
+    }
+  }
+  return itmax;
+}
+
+// row groups per wave of the fused block ATQ (registers: RG x NS gathered values in flight): 4 at
+// 128-column blocks (122 VGPRs, four waves per SIMD), 2 in the six-wave variant (PT2Q_ATQ_OCC),
+// one group for wider blocks
+template <int NS, int OCC>
+constexpr int atq_rg() { return NS == 8 ? (OCC > 0 ? 2 : 4) : 1; }
 
 // Iteration count of a block: one store per wave (iters_part), reduced by the post / fixup
 // launch -- not one atomic per wave on a single word (1024 atomics serialise at the memory side
@@ -431,7 +525,7 @@ PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
     }
 }
 
-template <int NS, bool F>
+template <int NS, bool F, int RG>
 PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid);
 
 // OCC: 0 = the compiler's register budget (85 VGPRs at NS = 8, 5 waves per SIMD); 6 = at least
@@ -439,13 +533,14 @@ PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int
 template <int NS, bool F, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8))) void atq_block_kernel(
     BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
-  atq_block_body<NS, F>(A0, g, K, rowgrid);
+  atq_block_body<NS, F, atq_rg<NS, OCC>()>(A0, g, K, rowgrid);
 }
 
-template <int NS, bool F>
+template <int NS, bool F, int RG>
 PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid) {
   const BlockArgs A = at_linear(A0, g);
   if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
+    if (A.probe & 16) return;
     atq_s1_part(A);
     return;
   }
@@ -458,10 +553,10 @@ PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int
     coeff_part(A, K, (int)blockIdx.x - A.nS1 - rowgrid);
     return;
   }
+  if (A.probe & 64) return;
   const int wave = threadIdx.x >> 6;
   const int rb = (int)blockIdx.x - A.nS1;
-  const int row0 = rb * ROWS_PER_WG + wave * ROWS_PER_WAVE;
-  const int it = block_rows<NS, F>(A, row0, false, true);
+  const int it = block_rows_rg<NS, F, RG>(A, rb * ROWS_PER_WG * RG + wave * ROWS_PER_WAVE);
   if (!A.iters || (threadIdx.x & 63) != 0) return;
   // one store per wave, no barrier: a wave whose rows converged early leaves at once instead of
   // holding its slot until the workgroup's slowest wave (the block-ATQ waves were parked 59 % of
@@ -495,7 +590,8 @@ __global__ __launch_bounds__(256) void atq_finish_kernel(BlockArgs A0, int rowgr
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
   if (A.iters && !A.iters_part && threadIdx.x == 0) *A.iters = 0;
-  for (int rb = 0; rb < rowgrid; ++rb) block_rows<NS>(A, rb * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
+  for (int rb = 0; rb < ceil_div_dev(A.n, ROWS_PER_WG); ++rb)
+    block_rows<NS>(A, rb * ROWS_PER_WG + wave * ROWS_PER_WAVE, true, false);
 }
 
 // ----------------------------------------------------------------- per-stage kernel (row-major)
@@ -935,19 +1031,22 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
   }
   const int nS1 = (G && S1 && s1sync && b <= 128) ? ceil_div(b, 8) : 0;
   BlockArgs A{Wt, ldw, n, b, blk, S1, d, max_iter, alpha, mu, Tt, ldt, Et, lde, iters, counters, iters_part,
-              G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_fallback};
-  int grid = ceil_div(n, ROWS_PER_WG);
+              G, ldg, nS1, s1sync, (float*)S1, (float*)d, status, pt2q_tuning().spin_cap_fallback,
+              pt2q_tuning().atq_probe};
   // the EF coefficient workgroups (Hinv given, columns left): COEF_SPAN columns e of one k row each
   const int per_k = (Hinv && nr > 0) ? ceil_div(nr, COEF_SPAN) : 0;
   const CoeffArgs K{Hinv, ldh, rem, nr, b, C, ldc, per_k > 0 ? per_k : 1};
-  const int cgrid = per_k * b;
+  const int cgrid = (pt2q_tuning().atq_probe & 2) ? 0 : per_k * b;
   return dispatch_ns(b, [&](auto ns) {
     constexpr int NS = decltype(ns)::value;
-    const dim3 gd(nS1 + grid + cgrid, 1, nz);
     // the six-wave variant only where it costs no spills: full 128-column blocks
     constexpr int OCC = NS == 8 ? 6 : 0;
+    const bool occ = OCC && b == 16 * NS && pt2q_tuning().atq_occ == 6;
+    // row workgroups: RG groups of 4 rows per wave (atq_rg)
+    const int grid = ceil_div(n, ROWS_PER_WG * (occ ? atq_rg<NS, OCC>() : atq_rg<NS, 0>()));
+    const dim3 gd(nS1 + grid + cgrid, 1, nz);
     if (b == 16 * NS) {
-      if (OCC && pt2q_tuning().atq_occ == 6)
+      if (occ)
         hipLaunchKernelGGL((atq_block_kernel<NS, true, OCC>), gd, dim3(256), 0, st, A, g, K, grid);
       else
         hipLaunchKernelGGL((atq_block_kernel<NS, true, 0>), gd, dim3(256), 0, st, A, g, K, grid);

@@ -144,6 +144,9 @@ struct Pt2qTuning {
   int ef2_per_cu = 2;          // PT2Q_EF2_PER_CU: ef2 workgroups per CU (1 or 2)
   int ef2_stagger = 0;         // PT2Q_EF2_STAGGER: ef2 start de-phasing (0: off)
   int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)
+  int atq_probe = 0;           // PT2Q_ATQ_PROBE (DEV_PROBES builds only; results garbage): block-ATQ
+                               // knock-outs, 1 = rows skip the S1 wait, 2 = no coefficient workgroups,
+                               // 4 = rows skip ITF
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
   int atq_occ = 6;             // PT2Q_ATQ_OCC: block-ATQ waves per SIMD floor (6, or 0: compiler's)
   bool atq_pc = true;          // PT2Q_ATQ_PC=0: per-channel rows on the old streaming wide kernel

@@ -649,6 +649,30 @@ def test_blocks_group_equals_per_linear(pt2q, n, m, count, ssr, dt):
             assert bits_equal(host(a), host(b)), z
 
 
+@pytest.mark.parametrize("n,m", [(11008, 4096), (4096, 11008)])
+def test_blocks_group_vs_oracle_at_mlp_shapes(pt2q, n, m):
+    """The grouped block loop the 7B bench times (pt2q_quantize_blocks_group at the MLP shapes,
+    fp16 weights, N = 2048) pinned to the oracle directly, not only through the per-linear path:
+    two linears sharing one Gram and H^-1 (gate/up read the same input), each vs
+    orc.quantize_blocks fed the device G and H^-1 -- codes, permutation, scales and ITF counts
+    bit for bit (main.py:158-215, reorder.py:107-143)."""
+    X = pt2q.fill_synthetic((2048, m), 4100 + m, outliers=True, device="cuda").half()
+    G = pt2q.gram(X)
+    Hinv, spd = pt2q.hessian_inverse(G, X.shape[0])
+    assert spd
+    Ws = [pt2q.fill_synthetic((n, m), 910 + z, std=0.02, device="cuda").half() for z in range(2)]
+    got = pt2q.engine.quantize_blocks_group(Ws, [G, G], [Hinv, Hinv], 128, True)
+    torch.cuda.synchronize()
+    orc.set_threads(16)
+    Gh, Hh = host(G), host(Hinv)
+    for z in range(2):
+        ref = orc.quantize_blocks(host(Ws[z].float()), Gh, Hh, 128, True, 1)
+        np.testing.assert_array_equal(host(got[z].perm), ref["perm"])
+        np.testing.assert_array_equal(host(got[z].T), ref["T"])
+        assert bits_equal(host(got[z].alpha), ref["alpha"]) and bits_equal(host(got[z].mu), ref["mu"])
+        np.testing.assert_array_equal(host(got[z].iters), ref["iters"])
+
+
 @pytest.mark.parametrize("m,N,batch,dt", [(256, 1000, 3, torch.float16), (512, 2048, 5, torch.bfloat16),
                                           (4096, 8192, 3, torch.float16), (768, 64, 130, torch.float16),
                                           (1280, 192, 2, torch.float16), (1024, 4160, 2, torch.bfloat16),
