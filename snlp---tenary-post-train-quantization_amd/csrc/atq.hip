@@ -402,8 +402,8 @@ PT2Q_DEV int block_rows_rg(const BlockArgs& A, int base) {
       }
     }
     if (A.S1) row_aga(R, S1, dv, &a, &m);
-    if (valid && !(A.probe & 8)) {
-      if (l == 0) {
+    if (valid) {
+      if (l == 0 && !(A.probe & 256)) {
         A.alpha[i] = a;
         A.mu[i] = m;
       }
@@ -411,9 +411,138 @@ PT2Q_DEV int block_rows_rg(const BlockArgs& A, int base) {
       for (int s = 0; s < NS; ++s)
         if (R.has(s)) {
           const int k = l + 16 * s;
-          A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
-          if (A.Et) A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
+          if (!(A.probe & 8)) A.Tt[(long)colrow[s] * A.ldt + i] = (int8_t)R.t[s];
+          if (A.Et && !(A.probe & 128)) A.Et[(long)k * A.lde + i] = R.w[s] - (a * R.t[s] + m);
         }
+    }
+  }
+  return itmax;
+}
+
+// 128-column blocks through a per-wave LDS stage (VEC): a wave owns 16 consecutive rows (four
+// groups of 4) and moves them as 16-byte pieces -- a block column's 16 rows of W are read, and its
+// 16 codes and 16 error terms written, 16 bytes per lane.  The per-element form (block_rows_rg:
+// 4- and 1-byte pieces, 16 cache lines per instruction) spent ~18 us of a grouped 7B launch on the
+// code stores and ~18 us on the error-term stores (knock-outs, tools/atq_knock.sh masks 8 / 128).
+// Per row, the arithmetic is block_rows_rg's, so the bits are the same.
+constexpr int VEC_KC = 32;                  // block columns per staging chunk
+constexpr int VEC_KS = 20;                  // floats per staged column: 16 rows + pad (16-B aligned,
+                                            // the 64 lanes' writes on 64 distinct banks)
+constexpr int VEC_STAGE = VEC_KC * VEC_KS;  // floats per wave (2560 B)
+
+PT2Q_DEV uint32_t byte_of(uint32_t x, int j) { return (x >> (8 * j)) & 0xffu; }
+
+template <int NS>
+PT2Q_DEV int block_rows_vec(const BlockArgs& A, int base) {
+  constexpr int RG = 4, NC = 16 * NS / VEC_KC;
+  static_assert(16 * NS == 128, "VEC: 128-column blocks");
+  __shared__ float stage_all[WAVES][VEC_STAGE];
+  float* stg = stage_all[threadIdx.x >> 6];
+  uint32_t* stg32 = (uint32_t*)stg;
+  const int lane = threadIdx.x & 63;
+  const int r = lane >> 4, l = lane & 15;
+  const int q4 = lane >> 2, part = lane & 3;  // staging lanes: chunk columns q4 + 16 h, rows 4 part ..
+  if (base >= A.n) return 0;                  // n % 16 == 0: a wave's rows are all valid or none
+  // W: every chunk's 16-byte pieces in flight, then through the stage into the row layout
+  float4 gv[NC][2];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long col = A.blk[VEC_KC * c + q4 + 16 * h];
+      gv[c][h] = (A.probe & 32) ? make_float4(0.f, 1.f, 2.f, 3.f)
+                                : *(const float4*)(A.Wt + col * A.ldw + base + 4 * part);
+    }
+  const bool s1_now = A.S1 && A.nS1 == 0;
+  float S1[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) S1[s] = s1_now ? A.S1[l + 16 * s] : 0.0f;
+  float dv = s1_now ? *A.d : 0.0f;
+  float v[RG][NS];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) *(float4*)(stg + (q4 + 16 * h) * VEC_KS + 4 * part) = gv[c][h];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < RG; ++g) v[g][2 * c + j] = stg[(l + 16 * j) * VEC_KS + 4 * g + r];
+  }
+  uint32_t tc[NS];  // codes of the four groups, byte g = row base + 4 g + r
+#pragma unroll
+  for (int s = 0; s < NS; ++s) tc[s] = 0;
+  int itmax = 0;
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int i = base + 4 * g + r;
+    Row<NS, true> R;
+    R.l = l;
+    R.b = A.b;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) R.w[s] = v[g][s];
+    const float wsum = row_sum_w(R);
+    float a, m;
+    const bool zero = row_init(R, wsum, &a, &m);
+    if (l == 0 && zero) atomicAdd(&A.counters[0], 1);
+    int it = 0;
+    if (!(A.probe & 4)) it = row_itf<true>(R, wsum, A.max_iter, &a, &m);
+    itmax = max(itmax, it);
+    if (g == 0 && A.S1 && A.nS1 > 0 && !(A.probe & 1)) {  // S1 / d from the leading workgroups, once
+      int ready = 1;
+      if (lane == 0) ready = wait_flag_ge<2>(&A.s1sync[0], 1, A.cap, nullptr, 0);
+      ready = __builtin_amdgcn_readfirstlane(ready);
+      __builtin_amdgcn_wave_barrier();
+      if (ready) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          S1[s] = __hip_atomic_load(&A.S1w[l + 16 * s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dv = __hip_atomic_load(A.dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        s1_local<NS>(A, l, S1, &dv);
+      }
+    }
+    if (A.S1) row_aga(R, S1, dv, &a, &m);
+    if (l == 0 && !(A.probe & 256)) {
+      A.alpha[i] = a;
+      A.mu[i] = m;
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      tc[s] |= ((uint32_t)(uint8_t)(int8_t)R.t[s]) << (8 * g);
+      v[g][s] = R.w[s] - (a * R.t[s] + m);  // the error term, in place of w
+    }
+  }
+  // codes: lane (r, l) puts row r's four group bytes of column k at dword 4 k + r; lane q reads
+  // column q + 64 h (16 bytes, row-group-major) and transposes it to row order
+#pragma unroll
+  for (int s = 0; s < NS; ++s) stg32[4 * (l + 16 * s) + r] = tc[s];
+  if (!(A.probe & 8)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = lane + 64 * h;
+      const uint4 x = *(const uint4*)(stg32 + 4 * k);
+      uint4 y;
+      uint32_t* yy = (uint32_t*)&y;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        yy[g] = byte_of(x.x, g) | byte_of(x.y, g) << 8 | byte_of(x.z, g) << 16 | byte_of(x.w, g) << 24;
+      *(uint4*)(A.Tt + (long)A.blk[k] * A.ldt + base) = y;
+    }
+  }
+  // error terms, a chunk of 32 columns at a time
+  if (A.Et && !(A.probe & 128)) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < RG; ++g) stg[(l + 16 * j) * VEC_KS + 4 * g + r] = v[g][2 * c + j];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kk = q4 + 16 * h;
+        *(float4*)(A.Et + (long)(VEC_KC * c + kk) * A.lde + base + 4 * part) =
+            *(const float4*)(stg + kk * VEC_KS + 4 * part);
+      }
     }
   }
   return itmax;
@@ -525,18 +654,18 @@ PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
     }
 }
 
-template <int NS, bool F, int RG>
+template <int NS, bool F, int RG, bool VEC>
 PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid);
 
-// OCC: 0 = the compiler's register budget (85 VGPRs at NS = 8, 5 waves per SIMD); 6 = at least
-// six waves per SIMD (76 VGPRs, no spills) to hide more of the row gathers (PT2Q_ATQ_OCC).
-template <int NS, bool F, int OCC>
+// OCC: 0 = the compiler's register budget (four waves per SIMD at NS = 8); 6 = at least six waves
+// per SIMD (80 VGPRs, two row groups per wave, no spills: PT2Q_ATQ_OCC).  VEC: block_rows_vec.
+template <int NS, bool F, int OCC, bool VEC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8))) void atq_block_kernel(
     BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
-  atq_block_body<NS, F, atq_rg<NS, OCC>()>(A0, g, K, rowgrid);
+  atq_block_body<NS, F, VEC ? 4 : atq_rg<NS, OCC>(), VEC>(A0, g, K, rowgrid);
 }
 
-template <int NS, bool F, int RG>
+template <int NS, bool F, int RG, bool VEC>
 PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid) {
   const BlockArgs A = at_linear(A0, g);
   if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
@@ -556,7 +685,11 @@ PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int
   if (A.probe & 64) return;
   const int wave = threadIdx.x >> 6;
   const int rb = (int)blockIdx.x - A.nS1;
-  const int it = block_rows_rg<NS, F, RG>(A, rb * ROWS_PER_WG * RG + wave * ROWS_PER_WAVE);
+  int it;
+  if constexpr (VEC && NS == 8)
+    it = block_rows_vec<NS>(A, rb * ROWS_PER_WG * RG + wave * ROWS_PER_WAVE * RG);
+  else
+    it = block_rows_rg<NS, F, RG>(A, rb * ROWS_PER_WG * RG + wave * ROWS_PER_WAVE);
   if (!A.iters || (threadIdx.x & 63) != 0) return;
   // one store per wave, no barrier: a wave whose rows converged early leaves at once instead of
   // holding its slot until the workgroup's slowest wave (the block-ATQ waves were parked 59 % of
@@ -1041,12 +1174,19 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
     constexpr int NS = decltype(ns)::value;
     // the six-wave variant only where it costs no spills: full 128-column blocks
     constexpr int OCC = NS == 8 ? 6 : 0;
-    const bool occ = OCC && b == 16 * NS && pt2q_tuning().atq_occ == 6;
-    // row workgroups: RG groups of 4 rows per wave (atq_rg)
-    const int grid = ceil_div(n, ROWS_PER_WG * (occ ? atq_rg<NS, OCC>() : atq_rg<NS, 0>()));
+    // 16-byte staged rows (block_rows_vec): full 128-column blocks, 16-byte aligned pieces
+    const auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    const bool vec = NS == 8 && b == 128 && pt2q_tuning().atq_vec && n % 16 == 0 && al16(Wt) && ldw % 4 == 0 &&
+                     al16(Tt) && ldt % 16 == 0 && (!Et || (al16(Et) && lde % 4 == 0)) && g.ws % 16 == 0;
+    const bool occ = !vec && OCC && b == 16 * NS && pt2q_tuning().atq_occ == 6;
+    // row workgroups: RG groups of 4 rows per wave (atq_rg; 4 in the staged form)
+    const int rg = vec ? 4 : occ ? atq_rg<NS, OCC>() : atq_rg<NS, 0>();
+    const int grid = ceil_div(n, ROWS_PER_WG * rg);
     const dim3 gd(nS1 + grid + cgrid, 1, nz);
     if (b == 16 * NS) {
-      if (occ)
+      if (vec)
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0, NS == 8>), gd, dim3(256), 0, st, A, g, K, grid);
+      else if (occ)
         hipLaunchKernelGGL((atq_block_kernel<NS, true, OCC>), gd, dim3(256), 0, st, A, g, K, grid);
       else
         hipLaunchKernelGGL((atq_block_kernel<NS, true, 0>), gd, dim3(256), 0, st, A, g, K, grid);

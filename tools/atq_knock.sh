@@ -3,7 +3,8 @@
 # fp16 4096 x 4096 linears) per PT2Q_ATQ_PROBE mask, on a DEV_PROBES library copied over the box's
 # package library (tools/_probe/libpt2q_dev.so, built with make DEV_PROBES=1).
 #   bash tools/atq_knock.sh TAG [mask ...]     masks: 1 no S1 wait, 2 no coefficient WGs, 4 no ITF,
-#   8 no row stores, 16 no S1 workgroups, 32 no row gathers (synthetic w), 64 row workgroups idle
+#   8 no code stores, 16 no S1 workgroups, 32 no row gathers (synthetic w), 64 row workgroups idle,
+#   128 no error-term stores, 256 no scale stores
 set -o pipefail
 TAG=${1:-atqk}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
