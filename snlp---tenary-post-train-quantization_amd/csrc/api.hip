@@ -44,6 +44,7 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_WIDE_WAVES", t.wide_waves);
   geti("PT2Q_ATQ_OCC", t.atq_occ);
   getb("PT2Q_ATQ_VEC", t.atq_vec);
+  getb("PT2Q_GRAM_ORDER", t.gram_order);
   getb("PT2Q_ATQ_PC", t.atq_pc);
   getb("PT2Q_ATQ_PC_REGS", t.atq_pc_regs);
   geti("PT2Q_EF_V2", t.ef_v2);

@@ -148,6 +148,7 @@ struct Pt2qTuning {
                                // knock-outs, 1 = rows skip the S1 wait, 2 = no coefficient workgroups,
                                // 4 = rows skip ITF, 8 / 128 / 256 = no code / error-term / scale
                                // stores, 16 = no S1 workgroups, 32 = no row gathers, 64 = idle rows
+  bool gram_order = true;      // PT2Q_GRAM_ORDER=0: batched Gram in the super-block tile order
   bool atq_vec = true;         // PT2Q_ATQ_VEC=0: 128-column block ATQ with per-element row stores
   int wide_waves = 4;          // PT2Q_WIDE_WAVES: waves (4 rows each) per wide-ATQ workgroup (4 or 8)
   int atq_occ = 6;             // PT2Q_ATQ_OCC: block-ATQ waves per SIMD floor (6, or 0: compiler's)
