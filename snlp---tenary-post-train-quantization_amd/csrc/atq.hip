@@ -200,25 +200,29 @@ struct BlockArgs {
   int probe;         // development knock-outs (pt2q_tuning().atq_probe; 0 in release builds)
 };
 
-// Grouped launch (grid.z = linear): this linear's pointers -- its workspace slice, its raw Gram.
-PT2Q_DEV BlockArgs at_linear(BlockArgs A, const Grp& g) {
+// Grouped launch: linear z's pointers -- its workspace slice, its raw Gram.
+template <typename T>
+PT2Q_DEV T* zslice(T* p, long ws, int z) {  // nullptr stays nullptr
+  return p ? (T*)((char*)p + (long)z * ws) : p;
+}
+PT2Q_DEV BlockArgs at_linear(BlockArgs A, const Grp& g, int z) {
   if (g.count == 0) return A;
   const long zs = g.ws;
-  A.Wt = zws(A.Wt, zs);
-  A.blk = zws(A.blk, zs);
-  A.S1 = zws(A.S1, zs);
-  A.d = zws(A.d, zs);
-  A.alpha = zws(A.alpha, zs);
-  A.mu = zws(A.mu, zs);
-  A.Tt = zws(A.Tt, zs);
-  A.Et = zws(A.Et, zs);
-  A.iters = zws(A.iters, zs);
-  A.counters = zws(A.counters, zs);
-  A.iters_part = zws(A.iters_part, zs);
-  A.s1sync = zws(A.s1sync, zs);
-  A.S1w = zws(A.S1w, zs);
-  A.dw = zws(A.dw, zs);
-  if (A.G) A.G = g.G[blockIdx.z];
+  A.Wt = zslice(A.Wt, zs, z);
+  A.blk = zslice(A.blk, zs, z);
+  A.S1 = zslice(A.S1, zs, z);
+  A.d = zslice(A.d, zs, z);
+  A.alpha = zslice(A.alpha, zs, z);
+  A.mu = zslice(A.mu, zs, z);
+  A.Tt = zslice(A.Tt, zs, z);
+  A.Et = zslice(A.Et, zs, z);
+  A.iters = zslice(A.iters, zs, z);
+  A.counters = zslice(A.counters, zs, z);
+  A.iters_part = zslice(A.iters_part, zs, z);
+  A.s1sync = zslice(A.s1sync, zs, z);
+  A.S1w = zslice(A.S1w, zs, z);
+  A.dw = zslice(A.dw, zs, z);
+  if (A.G) A.G = g.G[z];
   return A;  // status: one word for the whole call
 }
 
@@ -576,11 +580,11 @@ PT2Q_DEV float s1_serial_sum(const float* v, int b) {  // ((v0 + v1) + v2) ..., 
   return s;
 }
 
-PT2Q_DEV void atq_s1_part(const BlockArgs& A) {
+PT2Q_DEV void atq_s1_part(const BlockArgs& A, int x) {
   __shared__ float gb[8][129];
   __shared__ int last;
   const int tid = threadIdx.x, jj = tid >> 5, ln = tid & 31;
-  const int j = blockIdx.x * 8 + jj;
+  const int j = x * 8 + jj;
   if (j < A.b) {
     const long bj = (long)A.blk[j] * A.ldg;
 #pragma unroll
@@ -655,36 +659,49 @@ PT2Q_DEV void coeff_part(const BlockArgs& A, const CoeffArgs& K, int cb) {
 }
 
 template <int NS, bool F, int RG, bool VEC>
-PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid);
+PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid, int cgrid);
 
 // OCC: 0 = the compiler's register budget (four waves per SIMD at NS = 8); 6 = at least six waves
 // per SIMD (80 VGPRs, two row groups per wave, no spills: PT2Q_ATQ_OCC).  VEC: block_rows_vec.
 template <int NS, bool F, int OCC, bool VEC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1, 8))) void atq_block_kernel(
-    BlockArgs A0, Grp g, CoeffArgs K, int rowgrid) {
-  atq_block_body<NS, F, VEC ? 4 : atq_rg<NS, OCC>(), VEC>(A0, g, K, rowgrid);
+    BlockArgs A0, Grp g, CoeffArgs K, int rowgrid, int cgrid) {
+  atq_block_body<NS, F, VEC ? 4 : atq_rg<NS, OCC>(), VEC>(A0, g, K, rowgrid, cgrid);
 }
 
+// One 1-D grid for every linear z of the launch, in three role ranges: the S1 / d workgroups of
+// every linear (dispatched first, they wait on nobody), then the row workgroups of every linear,
+// then the EF-coefficient workgroups of every linear (dispatched last, they fill the CUs the rows'
+// ITF tail leaves idle).  Linear-major inside each range: every linear's S1 is under way before
+// any row workgroup, where a grid.z launch dispatched linear z's S1 workgroups only after every
+// workgroup of linears 0 .. z-1.
 template <int NS, bool F, int RG, bool VEC>
-PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid) {
-  const BlockArgs A = at_linear(A0, g);
-  if ((int)blockIdx.x < A.nS1) {  // dispatched first, waits on nobody
-    if (A.probe & 16) return;
-    atq_s1_part(A);
+PT2Q_DEV void atq_block_body(const BlockArgs& A0, const Grp& g, CoeffArgs K, int rowgrid, int cgrid) {
+  const int nz = g.count > 0 ? g.count : 1;
+  int b = (int)blockIdx.x;
+  if (b < nz * A0.nS1) {
+    const int z = b / A0.nS1;
+    if (A0.probe & 16) return;
+    atq_s1_part(at_linear(A0, g, z), b - z * A0.nS1);
     return;
   }
-  if ((int)blockIdx.x >= A.nS1 + rowgrid) {  // dispatched last: the EF coefficients
+  b -= nz * A0.nS1;
+  if (b >= nz * rowgrid) {
+    b -= nz * rowgrid;
+    const int z = b / cgrid;
     if (g.count > 0) {
-      K.Hinv = g.Hinv[blockIdx.z];
-      K.rem = zws(K.rem, g.ws);
-      K.C = zws(K.C, g.ws);
+      K.Hinv = g.Hinv[z];
+      K.rem = zslice(K.rem, g.ws, z);
+      K.C = zslice(K.C, g.ws, z);
     }
-    coeff_part(A, K, (int)blockIdx.x - A.nS1 - rowgrid);
+    coeff_part(at_linear(A0, g, z), K, b - z * cgrid);
     return;
   }
-  if (A.probe & 64) return;
+  if (A0.probe & 64) return;
+  const int z = b / rowgrid;
+  const BlockArgs A = at_linear(A0, g, z);
   const int wave = threadIdx.x >> 6;
-  const int rb = (int)blockIdx.x - A.nS1;
+  const int rb = b - z * rowgrid;
   int it;
   if constexpr (VEC && NS == 8)
     it = block_rows_vec<NS>(A, rb * ROWS_PER_WG * RG + wave * ROWS_PER_WAVE * RG);
@@ -718,7 +735,7 @@ PT2Q_DEV void finish_iters(const BlockArgs& A, int nparts) {
 // fence -- an L2 write-back -- per workgroup).
 template <int NS>
 __global__ __launch_bounds__(256) void atq_finish_kernel(BlockArgs A0, int rowgrid, Grp g) {
-  const BlockArgs A = at_linear(A0, g);
+  const BlockArgs A = at_linear(A0, g, blockIdx.z);
   finish_iters(A, rowgrid * WAVES);
   if (A.counters[0] != A.n) return;
   const int wave = threadIdx.x >> 6;
@@ -1182,16 +1199,16 @@ int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int 
     // row workgroups: RG groups of 4 rows per wave (atq_rg; 4 in the staged form)
     const int rg = vec ? 4 : occ ? atq_rg<NS, OCC>() : atq_rg<NS, 0>();
     const int grid = ceil_div(n, ROWS_PER_WG * rg);
-    const dim3 gd(nS1 + grid + cgrid, 1, nz);
+    const dim3 gd(nz * (nS1 + grid + cgrid));
     if (b == 16 * NS) {
       if (vec)
-        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0, NS == 8>), gd, dim3(256), 0, st, A, g, K, grid);
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0, NS == 8>), gd, dim3(256), 0, st, A, g, K, grid, cgrid);
       else if (occ)
-        hipLaunchKernelGGL((atq_block_kernel<NS, true, OCC>), gd, dim3(256), 0, st, A, g, K, grid);
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, OCC>), gd, dim3(256), 0, st, A, g, K, grid, cgrid);
       else
-        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0>), gd, dim3(256), 0, st, A, g, K, grid);
+        hipLaunchKernelGGL((atq_block_kernel<NS, true, 0>), gd, dim3(256), 0, st, A, g, K, grid, cgrid);
     } else {
-      hipLaunchKernelGGL((atq_block_kernel<NS, false, 0>), gd, dim3(256), 0, st, A, g, K, grid);
+      hipLaunchKernelGGL((atq_block_kernel<NS, false, 0>), gd, dim3(256), 0, st, A, g, K, grid, cgrid);
     }
     PT2Q_LAUNCH_CHECK();
     hipLaunchKernelGGL(atq_finish_kernel<NS>, dim3(1, 1, nz), dim3(256), 0, st, A, grid, g);
