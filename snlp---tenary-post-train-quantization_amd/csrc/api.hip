@@ -238,6 +238,16 @@ int hess_block_s1(const float* A, long lda, const int* blk, int bs, BlockWs& w, 
   return pt2q_launch_aga_s1(1, w.hS, bs, nullptr, bs, w.S1, w.d, st);
 }
 
+// per-channel setup in one launch: perm = [0, m) (the block is every column in ascending order),
+// the wide ATQ's counters (2 ints) and the iteration count zeroed -- instead of two memsets and a
+// select_seq launch per linear
+__global__ void pc_setup_kernel(int64_t* perm, int m, int* counters, int* iters) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) perm[i] = i;
+  if (i < 2) counters[i] = 0;
+  if (i == 0) *iters = 0;
+}
+
 __global__ void i64_to_i32_kernel(const int64_t* a, int n, int* b) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = (int)a[i];
@@ -263,9 +273,8 @@ int run_blocks(const void* W, int wdtype, long ldw_in, int n, int m, int b, int 
     // code transpose) and writes T, alpha, mu (n x 1) straight into the outputs.
     {
       StageScope ts(PT2Q_TIMER_SETUP, st);
-      if (hipMemsetAsync(w.counters, 0, sizeof(int) * 2, st) != hipSuccess) return PT2Q_E_HIP;
-      if (hipMemsetAsync(iters, 0, sizeof(int), st) != hipSuccess) return PT2Q_E_HIP;
-      if ((rc = pt2q_launch_select_seq(0, 0, m, m, nullptr, w.blk, w.rem[1], perm, st)) != PT2Q_OK) return rc;
+      hipLaunchKernelGGL(pc_setup_kernel, dim3(ceil_div(m, 256)), dim3(256), 0, st, perm, m, w.counters, iters);
+      PT2Q_LAUNCH_CHECK();
     }
     StageScope ts_atq(PT2Q_TIMER_ATQ, st);
     const bool act = aga == PT2Q_AGA_ACT;

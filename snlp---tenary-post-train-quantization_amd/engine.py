@@ -165,7 +165,7 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[t
     mu = torch.empty((n, B), dtype=torch.float32, device=dev)
     T = torch.empty((n, m), dtype=t_dtype, device=dev)
     perm = torch.empty(m, dtype=torch.int64, device=dev)
-    iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)  # zeroed by the call (run_blocks)
     flags = (_lib.FLAG_SSR if use_ssr else 0) | aga
     nbytes = blocks_workspace_bytes(n, m, block_size, flags)
     if s1d is not None:

@@ -123,21 +123,28 @@ def unit_cost(unit, block_size: int = 128) -> float:
 _ALIGN = 16  # every entry starts 16-byte aligned, so the receiver views the bytes in place
 
 
-def _flatten(results: Dict[str, Dict[str, torch.Tensor]]):
-    """(manifest, flat uint8 tensor) of {name: {key: tensor}}: every tensor's bytes back to back
-    (each padded to 16 bytes) in sorted (name, key) order; the manifest records
-    (name, key, dtype, shape, padded nbytes)."""
-    manifest, parts = [], []
+def _manifest(results: Dict[str, Dict[str, torch.Tensor]]):
+    """[(name, key, dtype, shape, padded nbytes)] of {name: {key: tensor}} in sorted (name, key)
+    order: the layout _flatten gives the bytes (each entry padded to 16 bytes)."""
+    out = []
     for name in sorted(results):
         for key in sorted(results[name]):
-            t = results[name][key].contiguous()
-            b = t.reshape(-1).view(torch.uint8) if t.numel() else torch.empty(0, dtype=torch.uint8,
-                                                                               device=t.device)
-            pad = (-b.numel()) % _ALIGN
-            if pad:
-                b = torch.cat([b, torch.zeros(pad, dtype=torch.uint8, device=b.device)])
-            manifest.append((name, key, str(t.dtype).replace("torch.", ""), tuple(t.shape), b.numel()))
-            parts.append(b)
+            t = results[name][key]
+            nb = t.numel() * t.element_size()
+            out.append((name, key, str(t.dtype).replace("torch.", ""), tuple(t.shape), nb + (-nb) % _ALIGN))
+    return out
+
+
+def _flatten(results: Dict[str, Dict[str, torch.Tensor]]):
+    """(manifest, flat uint8 tensor) of {name: {key: tensor}}: every tensor's bytes back to back
+    (each padded to 16 bytes) in _manifest's order -- the send buffer of a non-destination rank."""
+    manifest, parts = _manifest(results), []
+    for name, key, _, _, nb in manifest:
+        t = results[name][key].contiguous()
+        b = t.reshape(-1).view(torch.uint8) if t.numel() else torch.empty(0, dtype=torch.uint8, device=t.device)
+        if nb > b.numel():
+            b = torch.cat([b, torch.zeros(nb - b.numel(), dtype=torch.uint8, device=b.device)])
+        parts.append(b)
     if parts:
         flat = torch.cat(parts)
     else:
@@ -166,14 +173,18 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
     `dst`: one small object gather of the shape manifests, then ONE size-exact byte buffer per
     rank point-to-point (send/recv; RCCL over xGMI on GPUs, gloo on CPU).  Returns the merged dict
     on dst, None elsewhere.  The receive buffers go on `device`, else on the device of dst's own
-    results, else (dst holds none) the current HIP device under RCCL / the CPU under gloo."""
-    manifest, flat = _flatten(results)
-    if not dist.is_initialized():
-        return _unflatten(manifest, flat)
+    results, else (dst holds none) the current HIP device under RCCL / the CPU under gloo.
+    Only the senders pack their bytes: dst keeps its own tensors as they are (one rank: no copy
+    at all -- packing a 13B step's 1,400 result tensors cost as many device copies)."""
+    own = {name: dict(entry) for name, entry in results.items()}
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return own
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if world == 1:
-        return _unflatten(manifest, flat)
+    if rank != dst:
+        manifest, flat = _flatten(results)
+    else:
+        manifest = _manifest(results)
     manifests = [None] * world if rank == dst else None
     dist.gather_object(manifest, manifests, dst=dst, group=group)
     host = dist.get_backend(group) == "gloo"  # gloo moves host memory only: device bytes go via the CPU
@@ -181,11 +192,11 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
         if flat.numel():
             dist.send(flat.cpu() if host else flat, dst=dst, group=group)
         return None
-    merged = _unflatten(manifest, flat)
+    merged = own
     dev = device
     if dev is None:
         if manifest:
-            dev = flat.device
+            dev = next(iter(next(iter(results.values())).values())).device
         elif dist.get_backend(group) == "nccl":
             dev = torch.device("cuda", torch.cuda.current_device())
         else:
@@ -269,10 +280,16 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
     if grams_first is not None and hasattr(grams_first, "check"):
         grams_first.check()  # every Gram's stall bits of the step, one host read
     results = {}
+    # every linear's "shape" entry: one host-to-device copy for the step, not one blocking copy each
+    outs_all = [out for _, _, outs in finished for out in outs]
+    shapes = {}
+    for dev in {o.T.device for o in outs_all}:
+        mine_d = [o for o in outs_all if o.T.device == dev]
+        tab = torch.tensor([list(o.T.shape) for o in mine_d], dtype=torch.int64).to(dev, non_blocking=False)
+        shapes.update({id(o): tab[j] for j, o in enumerate(mine_d)})
     for name, projs, outs in finished:
         for p, out in zip(projs, outs):
-            r = {"alpha": out.alpha, "mu": out.mu, "perm": out.perm,
-                 "shape": torch.tensor(list(out.T.shape), dtype=torch.int64, device=out.T.device)}
+            r = {"alpha": out.alpha, "mu": out.mu, "perm": out.perm, "shape": shapes[id(out)]}
             if pack:
                 from . import engine
                 r["T2"] = engine.pack_ternary(out.T)[0]
