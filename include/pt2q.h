@@ -123,8 +123,10 @@ int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G
  * batch x m x m fp32 packed.  256 x 256 tiles, every tile one chain over all N rows (no
  * stream-K pieces, no hand-offs, no workspace), so each G[z] is bit-identical to pt2q_gram on
  * X[z] alone.  Needs m % 256 == 0, ldx % 8 == 0, 16-byte aligned X[z] and batch <= 128, else
- * PT2Q_E_UNSUPPORTED (use pt2q_gram per item).  Replaces main.py:128 for every unit of a model
- * step whose activations are at hand (the q/k/v, o, gate/up inputs of all decoder layers). */
+ * PT2Q_E_UNSUPPORTED (use pt2q_gram per item).  fp32 X (any m, batch <= 128): the f32 chain
+ * GEMM over every item's upper tiles in one launch, again bit-identical per item.  Replaces
+ * main.py:128 for every unit of a model step whose activations are at hand (the q/k/v, o,
+ * gate/up inputs of all decoder layers). */
 int pt2q_gram_batched(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
                       float* G, void* stream);
 

@@ -604,6 +604,8 @@ extern "C" int pt2q_gram_batched(int batch, const void* const* X, int xdtype, in
                                  float* G, void* stream) {
   if (batch <= 0 || !X || !G || N < 0 || N > INT_MAX || m <= 0 || ldx < m) return PT2Q_E_ARG;
   StageScope ts(PT2Q_TIMER_GRAM, (hipStream_t)stream);
+  if (xdtype == PT2Q_F32)
+    return pt2q_launch_gram_f32_batched((const float* const*)X, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream);
   return pt2q_launch_gram16_batched(X, xdtype, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream);
 }
 

@@ -397,6 +397,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmDesc g, int tiles_m, int 
   gemm_tile<BM, BN, TIn, VEC>(g, tiles_m, tiles_n, blockIdx.x, gridDim.x, As, Bs);
 }
 
+// A batch of symmetric f32 Grams G[z] = X[z]ᵀX[z] with their own X pointers (pt2q_gram_batched on
+// f32 activations): item blockIdx.y reads X[z], writes G + z * bstride.  Every element is the same
+// k-ascending chain as pt2q_gram on the item alone (the tile size never changes a chain), so the
+// bits are equal; the batch fills the chip where one small Gram's tiles cannot (GPT-2: 21 or 300
+// tiles per Gram).
+constexpr int GF_MAX = 128;
+struct GramF32Ptrs {
+  const float* X[GF_MAX];
+};
+template <int BM, int BN, bool VEC>
+__global__ __launch_bounds__(256) void gram_f32_batched_kernel(GemmDesc g, GramF32Ptrs P, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PAD];
+  g.A = g.B = P.X[blockIdx.y];
+  g.C += (long)blockIdx.y * g.bstride;
+  gemm_tile<BM, BN, float, VEC>(g, tiles_m, tiles_n, blockIdx.x, gridDim.x, As, Bs);
+}
+
 // Two independent GEMMs in one launch (workgroups [0, n0) -> g0, the rest -> g1): saves a
 // kernel boundary on a serial chain (Cholesky trailing update + triangular-inverse update).
 template <int BM, int BN, typename TIn, bool VEC>
@@ -859,6 +877,39 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
       return launch_dt<uint16_t>(g, st);
   }
   return PT2Q_E_ARG;
+}
+
+int pt2q_launch_gram_f32_batched(const float* const* X, long N, int m, long ldx, float* G, long gstride, int batch,
+                                 hipStream_t st) {
+  if (batch <= 0 || batch > GF_MAX || m <= 0 || N < 0 || N > INT_MAX || ldx < m || !G) return PT2Q_E_ARG;
+  GemmDesc g{};
+  g.M = m; g.N = m; g.K = (int)N;
+  g.lda = ldx; g.a_layout = LAY_KMAJOR;
+  g.ldb = ldx; g.b_layout = LAY_KMAJOR;
+  g.in_dtype = PT2Q_F32;
+  g.C = G; g.ldc = m;
+  g.mode = GEMM_STORE; g.upper = 1; g.mirror = 1;
+  g.batch = batch; g.bstride = gstride;
+  GramF32Ptrs P{};
+  bool vec = true;
+  for (int z = 0; z < batch; ++z) {
+    if (!X[z] && N > 0) return PT2Q_E_ARG;
+    P.X[z] = X[z];
+    g.A = g.B = X[z];
+    vec = vec && vec_ok<128, 128, float>(g);  // every item vector-aligned, or none uses it
+  }
+  // the launch_dt balance rule on the whole batch
+  const long t1 = ceil_div(m, 128), t6 = ceil_div(m, 64);
+  const long c128 = t1 * (t1 + 1) / 2 * batch, c64 = t6 * (t6 + 1) / 2 * batch;
+  const double r128 = std::ceil(c128 / 256.0) * 4.0, r64 = std::ceil(c64 / 256.0) * 1.15;
+  const bool big = c128 >= 64 && r128 <= r64;
+  const int tm = (int)(big ? t1 : t6);
+  const dim3 grid((unsigned)(tm * (tm + 1) / 2), (unsigned)batch);
+  auto kern = big ? (vec ? gram_f32_batched_kernel<128, 128, true> : gram_f32_batched_kernel<128, 128, false>)
+                  : (vec ? gram_f32_batched_kernel<64, 64, true> : gram_f32_batched_kernel<64, 64, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, g, P, tm, tm);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
 }
 
 size_t pt2q_gram_flags_ints(int m) {

@@ -91,6 +91,9 @@ struct GemmDesc {
   long bstride;     //      (gemmx and the rank-<=128 update run them in one launch, grid.y = z)
 };
 int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st);
+// batch (<= 128) f32 Grams G + z * gstride = X[z]ᵀX[z] (N x m, ld ldx; G ld m), bit-equal to pt2q_gram per item
+int pt2q_launch_gram_f32_batched(const float* const* X, long N, int m, long ldx, float* G, long gstride, int batch,
+                                 hipStream_t st);
 // block error feedback Wt[crow[e]][i] -= sum_k Ck[k][e] Et[k][i] (ef.hip); E_UNSUPPORTED if bs > 128
 // part (nullable): also the w-bar chunk partials of the updated rows, part[c][i] for i < n (the
 // next block's SSR mean over crow, ssr.hip wbar_chunk order)

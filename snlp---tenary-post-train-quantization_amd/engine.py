@@ -73,6 +73,8 @@ GRAM_BATCH_MAX = 128  # items per pt2q_gram_batched launch
 def gram_batched_supported(X: torch.Tensor) -> bool:
     """Whether pt2q_gram_batched takes activations like X (2-D view N x m)."""
     m = X.shape[-1]
+    if X.dtype == torch.float32:  # any m: the batched f32 GEMM (gemm.hip gram_f32_batched_kernel)
+        return X.is_contiguous()
     return (X.dtype in (torch.float16, torch.bfloat16) and m % 256 == 0 and X.is_contiguous()
             and X.data_ptr() % 16 == 0 and m % 8 == 0)
 
@@ -80,13 +82,15 @@ def gram_batched_supported(X: torch.Tensor) -> bool:
 def gram_batched(Xs, G: torch.Tensor) -> torch.Tensor:
     """G[z] = Xs[z]ᵀ Xs[z] for every item (main.py:128 per unit) in data-parallel launches of up to
     GRAM_BATCH_MAX items (pt2q_gram_batched): G is a contiguous fp32 (batch, m, m) tensor, the Xs
-    fp16 / bf16 (N, m) of one shape.  Each G[z] is bit-identical to gram(Xs[z])."""
+    fp16 / bf16 (m % 256 == 0) or fp32 (N, m) of one shape.  Each G[z] is bit-identical to
+    gram(Xs[z])."""
     Xs = [X.reshape(-1, X.shape[-1]) for X in Xs]
     N, m = Xs[0].shape
     if G.shape != (len(Xs), m, m) or G.dtype != torch.float32 or not G.is_contiguous():
         raise ValueError("gram_batched: G must be a contiguous fp32 (batch, m, m) tensor")
     if any(X.shape != (N, m) or X.dtype != Xs[0].dtype or not gram_batched_supported(X) for X in Xs):
-        raise _lib.Pt2qError("gram_batched: every X must be a contiguous 16-bit (N, m) tensor, m % 256 == 0")
+        raise _lib.Pt2qError("gram_batched: every X must be a contiguous (N, m) tensor of one dtype "
+                             "(16-bit: m % 256 == 0)")
     for z0 in range(0, len(Xs), GRAM_BATCH_MAX):
         chunk = Xs[z0:z0 + GRAM_BATCH_MAX]
         arr, keep = _lib.ptr_array(chunk)
