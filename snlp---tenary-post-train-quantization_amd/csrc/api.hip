@@ -651,10 +651,15 @@ extern "C" int pt2q_hessian_inverse_batched(const float* G, int m, int batch, in
   const bool upper = m <= SUMN_LDS_MAX;
   int rc;
   StageScope ts(PT2Q_TIMER_INVERSE, st);
-  for (int z = 0; z < batch; ++z)
-    if ((rc = pt2q_launch_prepare_hessian(G + z * mm, m, m, nsamples, percdamp, H + z * mm, m, damp + z, st,
-                                          upper)) != PT2Q_OK)
+  if (upper) {  // every item in one launch pair
+    if ((rc = pt2q_launch_prepare_hessian(G, m, m, nsamples, percdamp, H, m, damp, st, true, batch, mm)) != PT2Q_OK)
       return rc;
+  } else {
+    for (int z = 0; z < batch; ++z)
+      if ((rc = pt2q_launch_prepare_hessian(G + z * mm, m, m, nsamples, percdamp, H + z * mm, m, damp + z, st,
+                                            false)) != PT2Q_OK)
+        return rc;
+  }
   return pt2q_launch_cholesky_inverse(H, m, m, Hinv, m, H, Ui, info_dev, st, upper, batch);
 }
 

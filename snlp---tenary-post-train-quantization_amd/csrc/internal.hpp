@@ -126,8 +126,10 @@ int pt2q_launch_transpose_i8(const int8_t* src, long lds, int rows, int cols, vo
                              long ldd, hipStream_t st);
 int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, float* dst, long ldd,
                               hipStream_t st);
+// batch > 1 (m <= SUMN_LDS_MAX, damp given): items at G / H + z * bs, damp[z], in one launch pair
 int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
-                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only = false);
+                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only = false,
+                                int batch = 1, long bs = 0);
 
 // ---- Cholesky (chol.hip)
 // batch > 1: that many independent inverses, all packed (ld = m, item z at + z * m * m, info + z)

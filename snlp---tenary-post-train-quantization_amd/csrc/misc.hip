@@ -117,9 +117,12 @@ __global__ __launch_bounds__(1024) void hess_damp_kernel(float* H, long ldh, int
 
 // damp from the diagonal alone: h_ii = G_ii / fn (hess_scale's rounding), then the same SUMN
 // and scaling as hess_damp_kernel.  *damp_dev feeds hess_fill_kernel (and the caller).
+// batched: item blockIdx.x at G + z * bs, damp_dev[z]
 __global__ __launch_bounds__(1024) void hess_diag_damp_kernel(const float* G, long ldg, int m, float fn,
-                                                              float percdamp, float* damp_dev) {
+                                                              float percdamp, float* damp_dev, long bs) {
   __shared__ float tot;
+  G += (long)blockIdx.x * bs;
+  damp_dev += blockIdx.x;
   __shared__ float stage[SUMN_LDS_MAX];
   for (int i = threadIdx.x; i < m; i += blockDim.x) stage[i] = G[(long)i * ldg + i] / fn;
   __syncthreads();
@@ -134,8 +137,12 @@ __global__ __launch_bounds__(1024) void hess_diag_damp_kernel(const float* G, lo
 
 // H = G / fn with damp on the diagonal (hess_scale + hess_damp in one pass); upper_only: the
 // strictly lower part is written as zero (H then is the Cholesky work matrix as is).
+// batched: item blockIdx.y at G / H + z * bs, damp_dev[z]
 __global__ void hess_fill_kernel(const float* G, long ldg, int m, float fn, const float* damp_dev,
-                                 float* H, long ldh, int upper_only) {
+                                 float* H, long ldh, int upper_only, long bs) {
+  G += (long)blockIdx.y * bs;
+  H += (long)blockIdx.y * bs;
+  damp_dev += blockIdx.y;
   long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (long)m * m) return;
   int r = (int)(q / m), c = (int)(q % m);
@@ -146,8 +153,11 @@ __global__ void hess_fill_kernel(const float* G, long ldg, int m, float fn, cons
 
 // hess_fill_kernel four columns per thread (m, ldg, ldh multiples of 4, 16-byte aligned)
 __global__ void hess_fill4_kernel(const float* G, long ldg, int m, float fn, const float* damp_dev,
-                                  float* H, long ldh, int upper_only) {
+                                  float* H, long ldh, int upper_only, long bs) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  G += (long)blockIdx.y * bs;
+  H += (long)blockIdx.y * bs;
+  damp_dev += blockIdx.y;
   const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int m4 = m / 4;
   if (q >= (long)m * m4) return;
@@ -320,21 +330,24 @@ int pt2q_launch_transpose_f32(const float* src, long lds, int rows, int cols, fl
 }
 
 int pt2q_launch_prepare_hessian(const float* G, long ldg, int m, long nsamples, float percdamp,
-                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only) {
-  if (damp && m <= SUMN_LDS_MAX) {  // damp from the diagonal, then one pass over G
-    hipLaunchKernelGGL(hess_diag_damp_kernel, dim3(1), dim3(1024), 0, st, G, ldg, m, (float)nsamples,
-                       percdamp, damp);
+                                float* H, long ldh, float* damp, hipStream_t st, bool upper_only, int batch,
+                                long bs) {
+  if (damp && m <= SUMN_LDS_MAX) {  // damp from the diagonal, then one pass over G (every item at once)
+    hipLaunchKernelGGL(hess_diag_damp_kernel, dim3(batch), dim3(1024), 0, st, G, ldg, m, (float)nsamples,
+                       percdamp, damp, bs);
     PT2Q_LAUNCH_CHECK();
-    if (m % 4 == 0 && ldg % 4 == 0 && ldh % 4 == 0 && (uintptr_t)G % 16 == 0 && (uintptr_t)H % 16 == 0)
-      hipLaunchKernelGGL(hess_fill4_kernel, dim3(ceil_div((long)m * (m / 4), 256)), dim3(256), 0, st, G,
-                         ldg, m, (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
+    if (m % 4 == 0 && ldg % 4 == 0 && ldh % 4 == 0 && bs % 4 == 0 && (uintptr_t)G % 16 == 0 &&
+        (uintptr_t)H % 16 == 0)
+      hipLaunchKernelGGL(hess_fill4_kernel, dim3(ceil_div((long)m * (m / 4), 256), batch), dim3(256), 0, st, G,
+                         ldg, m, (float)nsamples, damp, H, ldh, upper_only ? 1 : 0, bs);
     else
-      hipLaunchKernelGGL(hess_fill_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg, m,
-                         (float)nsamples, damp, H, ldh, upper_only ? 1 : 0);
+      hipLaunchKernelGGL(hess_fill_kernel, dim3(ceil_div((long)m * m, 256), batch), dim3(256), 0, st, G, ldg, m,
+                         (float)nsamples, damp, H, ldh, upper_only ? 1 : 0, bs);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }
   if (upper_only) return PT2Q_E_UNSUPPORTED;
+  if (batch != 1) return PT2Q_E_ARG;  // (the caller loops over items)
   hipLaunchKernelGGL(hess_scale_kernel, dim3(ceil_div((long)m * m, 256)), dim3(256), 0, st, G, ldg,
                      m, (float)nsamples, H, ldh);
   PT2Q_LAUNCH_CHECK();
