@@ -515,6 +515,8 @@ def test_layer_not_spd_pinv_fallback(pt2q):
     (768, 3072, 512, True, 128),     # GPT-2 mlp.c_proj shape, 24 blocks
     (2304, 768, 1024, False, 128),   # GPT-2 c_attn shape, sequential blocks
     (640, 1000, 700, True, 256),     # ragged m, wider blocks
+    (1000, 640, 700, True, 128),     # n % 16 != 0: the block ATQ's per-element form (no 16-byte stage)
+    (1008, 520, 600, True, 128),     # n % 16 == 0 with a ragged last block (16-byte stage, then b = 8)
 ])
 def test_layer_m_bitexact_larger(pt2q, n, m, N, ssr, bs):
     W = synth.weights(1000 + n, n, m)
@@ -623,7 +625,7 @@ def test_reference_call_shapes_with_cpu_tensors(pt2q):
 
 @pytest.mark.parametrize("n,m,count,ssr,dt", [(256, 512, 3, True, torch.float32), (384, 700, 5, True, torch.float16),
                                              (512, 384, 2, False, torch.float32), (1024, 1024, 16, True, torch.float16),
-                                             (4096, 4096, 3, True, torch.float16),
+                                             (4096, 4096, 3, True, torch.float16), (1000, 512, 3, True, torch.float16),
                                              (11008, 4096, 3, True, torch.float16),
                                              (4096, 11008, 2, True, torch.float16)])
 def test_blocks_group_equals_per_linear(pt2q, n, m, count, ssr, dt):
