@@ -151,14 +151,16 @@ def describe_units(units, layers):
 
 
 def config_runs(a, dev):
-    """extra.configs: one short grams-first run (1 warmup + 2 timed steps, same flags) of every
+    """extra.configs: one short grams-first run (2 warmup + 3 timed steps, same flags) of every
     other BASELINE config's model workload on this GPU (C2 gpt2, C3 opt-1.3b, C5 llama-2-13b, or
-    C4 when another model is the headline)."""
+    C4 when another model is the headline).  Two warmup steps: the second step of a fresh
+    workload can still grow the caching allocator's pools (a C5 step once took 991 ms instead of
+    ~120 ms right after a single warmup step)."""
     out = {}
     for name in sharding.MODELS:
         if name == a.model:
             continue
-        b = resolve(parse(["--model", name, "--steps", "2", "--warmup", "1", "--group", str(a.group),
+        b = resolve(parse(["--model", name, "--steps", "3", "--warmup", "2", "--group", str(a.group),
                            "--lanes", str(a.lanes), "--inv-streams", str(a.inv_streams)]))
         io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[b.io_dtype]
         try:
