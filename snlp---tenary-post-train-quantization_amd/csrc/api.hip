@@ -56,6 +56,7 @@ Pt2qTuning load_tuning() {
 #endif
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
+  getb("PT2Q_EF2_G1LDS", t.ef2_g1lds);
   if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;
   if (t.wide_waves != 8) t.wide_waves = 4;
   if (t.atq_occ != 0) t.atq_occ = 6;

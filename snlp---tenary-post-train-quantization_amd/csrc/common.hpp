@@ -141,6 +141,7 @@ struct Pt2qTuning {
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
   bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM
   int ef_v2 = 1;               // PT2Q_EF_V2: 1 = ef2_gemm_kernel (two workgroups per CU, default), 0 = ef_gemm_kernel
+  bool ef2_g1lds = true;       // PT2Q_EF2_G1LDS=0: column group 1's old values loaded in the epilogue
   int ef2_per_cu = 2;          // PT2Q_EF2_PER_CU: ef2 workgroups per CU (1 or 2)
   int ef2_stagger = 0;         // PT2Q_EF2_STAGGER: ef2 start de-phasing (0: off)
   int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)

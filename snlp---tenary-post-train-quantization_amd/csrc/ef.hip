@@ -711,13 +711,46 @@ PT2Q_DEV void e2_store(const u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const
       __builtin_amdgcn_raw_buffer_store_b128(c[(rm * 2 + RN) * 4 + q], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
 }
 
+// Column group 1's old values by LDS-DMA (G1L): 8 buffer-to-LDS loads per wave, 16 bytes per lane,
+// into the wave's own chunks of a ring slot -- exactly the bytes its own stage DMAs (e2_stage: wave
+// w owns A chunks (4 w + q) and B chunks E2_PANEL + (4 w + q) KiB) write next, so no other wave
+// reads or writes them in between.  Chunk j = 4 rm + q holds c[(2 rm + 1) * 4 + q] of every lane.
+PT2Q_DEV uint32_t e2_g1_chunk(int wv, int j) {
+  return (uint32_t)(j < 4 ? (wv * 4 + j) * 1024 : E2_PANEL + (wv * 4 + j - 4) * 1024);
+}
+PT2Q_DEV void e2_g1_dma(__amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2], uint8_t* slot) {
+  typedef __attribute__((address_space(3))) void* lptr;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lptr)(slot + e2_g1_chunk(wv, 4 * rm + q)), 16,
+                                              rb[rm] + 4 * (32 + 8 * q), 0, 0, 0);
+}
+PT2Q_DEV void e2_g1_read(u32x4 (&c)[EF_CV], const uint8_t* slot) {
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int rm = 0; rm < 2; ++rm)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      c[(rm * 2 + 1) * 4 + q] = *(const u32x4*)(slot + e2_g1_chunk(wv, 4 * rm + q) + 16 * lane);
+}
+
 // NST = K stages per tile (2: bs <= 64, 4: bs <= 128; stages past bs are zero chunks: no-op pairs).
 // Issue order per tile, for the hand-counted vmcnt waits: [next rows: 2] [stage s + 2 after each
 // compute s (the last two: the next tile's stages 0 and 1)] with [old values, column group 0: 8]
 // just before the last stage's compute; the epilogue then [waits for group 0] [loads group 1: 8]
 // [stores group 0: 8] [waits for group 1] [stores it: 8] [w-bar partials: P].  So at the next
 // tile's top only that tile's stores (SP) may still be in flight beside its stages.
-template <int NST>
+// G1L (NST = 4): column group 1's old values come by LDS-DMA (e2_g1_dma) issued after stage 2's
+// compute into the slot it freed, so their latency hides under stage 3's MFMAs instead of the
+// epilogue's; the next tile's stage 0 then goes into stage 3's slot and its stage 1 into the
+// group-1 slot once the waves have read it (mid-epilogue), so the slots' roles alternate from
+// tile to tile (par).  Issue order: [rows: 2] [stage 2, 3 after compute 0, 1] [group 1: 8 after
+// compute 2] [group 0 loads: 8] [next stage 0 after compute 3] [epilogue: stores 0: 8, next stage
+// 1, stores 1: 8, w-bar: P].  Same products, same order: the same bits.
+template <int NST, bool G1L = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void ef2_gemm_kernel(
     EfArgs a0, long wt_bytes, long part_bytes) {
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * E2_STAGE];
@@ -751,6 +784,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   e2_stage(a, e0, i0, 0, smem, lds0, vo, true);
   int Dn1 = e2_stage(a, e0, i0, 1, smem + E2_STAGE, lds0 + E2_STAGE, vo, true);
   int SP = 0;
+  int par = 0;  // G1L: the slot of this tile's stage 0 (stage s in slot (s + par) & 1)
+  static_assert(!G1L || NST == 4, "G1L: four K stages per tile");
   for (;;) {
     const int tn = t + (int)gridDim.x;
     const bool more = tn < total;
@@ -774,18 +809,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int X[NST];  // DMAs issued after compute s (into the slot it freed)
 #pragma unroll
     for (int s = 0; s < NST; ++s) {
-      // this stage landed: everything younger than it may still be in flight
-      const int young = s == 0 ? Dn1 + SP + 2 : s == 1 ? SP + 2 + X[0] : X[s - 1];
+      // this stage landed: everything younger than it may still be in flight (G1L: the stage-1
+      // DMA of this tile was issued after the previous tile's group-0 stores, not before them)
+      const int young = s == 0   ? Dn1 + SP + 2
+                        : s == 1 ? (G1L && SP > 0 ? SP - EF_CV / 2 : SP) + 2 + X[0]
+                                 : X[s - 1];
       e2_vmcnt(young);
       asm volatile("s_barrier" ::: "memory");
       if (s == NST - 1) e2_load<0>(c, rc, rb);  // their latency hides under the last stage
+      const int sl = G1L ? (s + par) & 1 : s & 1;
       EfNoIO nio;
-      if (!(a0.probe & 4)) F.half(lds0 + (s & 1) * E2_STAGE, nio);
+      if (!(a0.probe & 4)) F.half(lds0 + sl * E2_STAGE, nio);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slot
-      uint8_t* slot = smem + (s & 1) * E2_STAGE;
-      const uint32_t slot_lds = lds0 + (s & 1) * E2_STAGE;
+      uint8_t* slot = smem + sl * E2_STAGE;
+      const uint32_t slot_lds = lds0 + sl * E2_STAGE;
       if (s + 2 < NST) {
         X[s] = e2_stage(a, e0, i0, s + 2, slot, slot_lds, vo, true);
+      } else if (G1L && s == NST - 2) {
+        e2_g1_dma(rc, rb, slot);  // column group 1's old values into the slot stage 2 freed
+        X[s] = EF_CV / 2;
+      } else if (G1L) {
+        X[s] = more ? e2_stage(an, en, in, 0, slot, slot_lds, vo, newB) : 0;
       } else if (more) {
         X[s] = e2_stage(an, en, in, s + 2 - NST, slot, slot_lds, vo, newB);
         if (s == NST - 1) Dn1 = X[s];
@@ -793,15 +837,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         X[s] = 0;
       }
     }
-    e2_vmcnt(X[NST - 1]);  // column group 0's old values landed
+    e2_vmcnt(X[NST - 1]);  // column group 0's old values landed (G1L: and group 1's, older)
     e2_sub<0>(c, F);
-    e2_load<1>(c, rc, rb);  // before group 0's stores: waiting for it then leaves those in flight
+    if constexpr (!G1L) e2_load<1>(c, rc, rb);  // before group 0's stores: waiting for it then leaves those in flight
     e2_store<0>(c, rc, rb);
     if (P) {  // this tile's w-bar partials (the next block's SSR mean, DESIGN.md §3 CHUNK128)
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red free (last readers done)
       ef_wbar_span<0, 16>(wrow, c, red);
     }
-    e2_vmcnt(EF_CV / 2);  // group 1 landed (younger: group 0's stores)
+    if constexpr (G1L) {
+      uint8_t* g1 = smem + par * E2_STAGE;  // stage 2's slot
+      e2_g1_read(c, g1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's chunks read: its DMAs may overwrite them
+      Dn1 = more ? e2_stage(an, en, in, 1, g1, lds0 + par * E2_STAGE, vo, newB) : 0;
+      par ^= 1;
+    } else {
+      e2_vmcnt(EF_CV / 2);  // group 1 landed (younger: group 0's stores)
+    }
     e2_sub<1>(c, F);
     e2_store<1>(c, rc, rb);
     if (P) {
@@ -845,6 +897,8 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
     const int grid2 = std::min(a.ntile * a.nz, pt2q_tuning().ef2_per_cu * cus);
     if (bs <= 2 * E2_KS)
       hipLaunchKernelGGL(ef2_gemm_kernel<2>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
+    else if (pt2q_tuning().ef2_g1lds)
+      hipLaunchKernelGGL((ef2_gemm_kernel<4, true>), dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
     else
       hipLaunchKernelGGL(ef2_gemm_kernel<4>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
     PT2Q_LAUNCH_CHECK();
