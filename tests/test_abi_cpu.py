@@ -161,3 +161,25 @@ def test_quantize_blocks_hinv_optional_only_per_channel(pt2q):
     E_ARG, I8 = 1, 3
     assert lib.pt2q_quantize_blocks(p, 0, 64, 16, 64, 32, 0x11, p, 64, None, 64, 100, p, p, p, I8, p,
                                     None, p, 1 << 30, None) == E_ARG
+
+
+def test_gram_order_tables_cover_every_tile_once():
+    """csrc/gram_order.inc (tools/gram_order_search.c): each searched batched-Gram tile order is a
+    permutation of the T (T + 1) / 2 upper tiles of its width, and its runs of 32 (one XCD's
+    concurrent tiles) read fewer distinct X panels per k-row than the super-block order they
+    replace -- the order decides only which workgroup computes which tile, so this (and the
+    bit-exact batched-Gram GPU tests) is its whole contract."""
+    src = open(os.path.join(ROOT, "snlp---tenary-post-train-quantization_amd", "csrc", "gram_order.inc")).read()
+    tab = [int(x, 16) for x in re.findall(r"0x([0-9a-f]{4})", src)]
+    Ts = [int(v) for v in re.search(r"go_T\[GO_COUNT\] = \{([^}]*)\}", src).group(1).split(",")]
+    offs = [int(v) for v in re.search(r"go_off\[GO_COUNT\] = \{([^}]*)\}", src).group(1).split(",")]
+    claimed = {int(T): (int(c), int(c0)) for T, c, c0 in
+               re.findall(r"T = (\d+): \d+ tiles, \d+ runs; distinct panels per k-row (\d+) \(super-block order (\d+)\)", src)}
+    assert len(Ts) == len(offs) == len(claimed) and offs[0] == 0
+    for T, o in zip(Ts, offs):
+        nt = T * (T + 1) // 2
+        tiles = [(e & 0xFF, e >> 8) for e in tab[o:o + nt]]
+        assert sorted(tiles) == [(a, b) for b in range(T) for a in range(b + 1)], T
+        panels = sum(len({p for t in tiles[r:r + 32] for p in t}) for r in range(0, nt, 32))
+        assert panels == claimed[T][0] < claimed[T][1], T
+    assert len(tab) == offs[-1] + Ts[-1] * (Ts[-1] + 1) // 2
