@@ -714,27 +714,35 @@ PT2Q_DEV void e2_store(const u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const
 // Column group 1's old values by LDS-DMA (G1L): 8 buffer-to-LDS loads per wave, 16 bytes per lane,
 // into the wave's own chunks of a ring slot -- exactly the bytes its own stage DMAs (e2_stage: wave
 // w owns A chunks (4 w + q) and B chunks E2_PANEL + (4 w + q) KiB) write next, so no other wave
-// reads or writes them in between.  Chunk j = 4 rm + q holds c[(2 rm + 1) * 4 + q] of every lane.
+// reads or writes them in between.  The loads are row-contiguous: load j brings rows 8 j .. 8 j + 7
+// of the wave's 64 output rows, 8 lanes per row covering its 128-byte group-1 segment (a whole
+// cache line per row, 8 lines per instruction -- the register-path loads touched 32 rows x 32
+// bytes each); lane L of load j holds row 8 j + L / 8, 16-byte piece L % 8, and the epilogue
+// reads each lane's own pieces back from there.
 PT2Q_DEV uint32_t e2_g1_chunk(int wv, int j) {
   return (uint32_t)(j < 4 ? (wv * 4 + j) * 1024 : E2_PANEL + (wv * 4 + j - 4) * 1024);
 }
 PT2Q_DEV void e2_g1_dma(__amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2], uint8_t* slot) {
   typedef __attribute__((address_space(3))) void* lptr;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-  for (int rm = 0; rm < 2; ++rm)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lptr)(slot + e2_g1_chunk(wv, 4 * rm + q)), 16,
-                                              rb[rm] + 4 * (32 + 8 * q), 0, 0, 0);
+  for (int j = 0; j < 8; ++j) {
+    // row 8 j + lane / 8 of the wave: row block rm = j / 4, its base from that row's h = 0 lane
+    const uint32_t src = (uint32_t)__shfl((int)rb[j >> 2], 8 * (j & 3) + (lane >> 3));
+    const uint32_t off = src == EF_DROP ? EF_DROP : src + 4 * (32 + 4 * (lane & 7));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (lptr)(slot + e2_g1_chunk(wv, j)), 16, off, 0, 0, 0);
+  }
 }
 PT2Q_DEV void e2_g1_read(u32x4 (&c)[EF_CV], const uint8_t* slot) {
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      c[(rm * 2 + 1) * 4 + q] = *(const u32x4*)(slot + e2_g1_chunk(wv, 4 * rm + q) + 16 * lane);
+    for (int q = 0; q < 4; ++q) {
+      const int j = rm * 4 + (li >> 3), piece = ((li & 7) << 3) | (2 * q + h);
+      c[(rm * 2 + 1) * 4 + q] = *(const u32x4*)(slot + e2_g1_chunk(wv, j) + 16 * piece);
+    }
 }
 
 // NST = K stages per tile (2: bs <= 64, 4: bs <= 128; stages past bs are zero chunks: no-op pairs).
