@@ -848,8 +848,8 @@ struct GbArgs {
 };
 
 // Batched-Gram tile orders searched offline (tools/gram_order_search.c): an XCD's 32 concurrent
-// tiles (a run) read 10.7 distinct X panels per k-row at m = 11008 instead of 15.2 (super-block
-// order), 8.4 instead of 10.6 at m = 4096.
+// tiles (a run) read 10.3 distinct X panels per k-row at m = 11008 instead of 15.2 (super-block
+// order); tables for m = 8192 / 11008 / 13824 (at m = 4096 a searched order measured no faster).
 #include "gram_order.inc"
 
 template <bool BF16>
