@@ -64,7 +64,7 @@ def parse(argv=None):
                         "sharded step's gather on a one-GPU box; not a scaling measurement)")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--workload", choices=["model", "layer", "split"], default="model",
+    p.add_argument("--workload", choices=["model", "layer", "split", "decoder"], default="model",
                    help="model: LPT-sharded 7B step; layer: one layer per rank (weak); split: one n x m "
                         "layer, its Gram data-parallel over the ranks (strong)")
     p.add_argument("--model", choices=["llama-2-7b", "gpt2", "opt-1.3b", "llama-2-13b"], default="llama-2-7b",
@@ -105,6 +105,15 @@ def parse(argv=None):
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
+    p.add_argument("--shard", default=None,
+                   help="model workload, ONE GPU: time rank r's LPT shard of a --gpus N step alone (r or 'all': "
+                        "every rank's shard in turn, after the whole step on this GPU), without the gather "
+                        "(its bytes are reported) -- a one-GPU projection of the N-GPU step, not a scaling "
+                        "measurement")
+    p.add_argument("--no-shards", action="store_true",
+                   help="skip extra.shards8 (every rank's shard of an 8-GPU step timed alone on this GPU)")
+    p.add_argument("--no-decoder", action="store_true",
+                   help="skip extra.decoder (the layer-by-layer PT2LLMQuantizer.quantize flow, Llama-2-7B shapes)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the single-layer / Gram / per-config extras (profiling: keeps only the "
@@ -185,19 +194,141 @@ def config_runs(a, dev):
             peak = MI355X_F32_MFMA_PEAK_TFLOPS if b.io_dtype == "fp32" else MI355X_F16_MFMA_PEAK_TFLOPS
             st = stage_roofline(model_work(w.units, b.block_size, IO_BYTES[b.io_dtype], not b.no_ssr), ph, busy,
                                 s * 1e3, 1, peak)
-            out[name] = {"config": sharding.MODELS[name]["config"], "workload": describe_units(w.units, b.layers),
+            del w
+            gc.collect()
+            torch.cuda.empty_cache()
+            sh8 = None
+            if name == "llama-2-13b" and not a.no_shards:  # C5 is an 8-GPU config too
+                try:
+                    sh8 = shard_runs(b, dev, io, 8, t1_ms=s * 1e3, t1_phase=ph)
+                except Exception as e:
+                    sh8 = {"error": f"{type(e).__name__}: {e}"}
+            out[name] = {"config": sharding.MODELS[name]["config"], "workload": describe_units(sharding.model_units(name), b.layers),
                          "tokens": b.tokens, "block_size": b.block_size if b.block_size < (1 << 14) else "m (per-channel)",
                          "io_dtype": b.io_dtype, "weight_columns_per_step": cols, "ms_per_step": s * 1e3,
                          "cols_per_s": cols / s, "s_per_decoder_layer": s / b.layers,
                          "steps": b.steps, "warmup": b.warmup,
                          "roofline": {"dominant": st["dominant"], "floor_s": st["step"]["floor_s"],
                                       "frac_step": st["step"]["frac"], "phase_s": ph, "stages": st}}
-            del w
-            gc.collect()
+            if sh8 is not None:
+                out[name]["shards8"] = sh8
         except Exception as e:  # a config that fails is reported, not allowed to drop the line
             out[name] = {"config": sharding.MODELS[name]["config"], "error": f"{type(e).__name__}: {e}"}
         gc.collect()
         torch.cuda.empty_cache()
+    return out
+
+
+def shard_runs(a, dev, io, world, ranks=None, t1_ms=None, t1_phase=None, steps=3, warmup=2):
+    """Every rank's LPT shard of a `world`-rank model step, timed ALONE on this one GPU (no process
+    group, no gather: each shard reports the bytes its gather would send).  A shard's time is what
+    its rank computes in the N-GPU step; the step itself would also wait for the gather and for
+    the slowest rank.  projected_efficiency = T1 / (world x max_r T_r) with T1 the whole step on
+    this GPU -- a one-GPU PROJECTION of the strong-scaling efficiency, not a measurement of it
+    (the RCCL transport and the shared power / fabric of a full node are not in it).  Per phase,
+    `share_ratio` = the slowest shard's phase wall / (T1's phase wall / world): the phases whose
+    fixed latencies do not shrink with the shard (the batched inverse's serial panel chain, the
+    per-block launch chain of the grouped loops) show up there."""
+    ranks = list(range(world)) if ranks is None else list(ranks)
+    out = []
+    for r in ranks:
+        w = ModelStep(a, r, world, dev, io, shard_only=True)
+        for _ in range(warmup):
+            w.step()
+        torch.cuda.synchronize()
+        step_ms = []
+        for _ in range(steps):
+            ts = time.perf_counter()
+            w.step()
+            torch.cuda.synchronize()
+            step_ms.append(1e3 * (time.perf_counter() - ts))
+        ph = w.phase_step() if w.gf is not None and a.schedule == "grams-first" else None
+        units = [w.units[i] for i in w.mine]
+        rec = {"rank": r, "units": len(units), "linears": sum(len(u[1]) for u in units),
+               "cols": sharding.units_cols(units), "ms_per_step": float(np.median(step_ms)),
+               "step_ms": {"min": min(step_ms), "median": float(np.median(step_ms)), "max": max(step_ms)},
+               "phase_s": ph, "gather_send_bytes": w.gather_bytes,
+               "predicted_cost_s": sum(sharding.unit_cost(u, a.block_size) for u in units),
+               "predicted_shard_s": sharding.shard_cost(units, a.block_size)}
+        log(0, f"shard {r}/{world}: {len(units)} units, {rec['ms_per_step']:.1f} ms/step, phases "
+               f"{ {k: round(v * 1e3, 1) for k, v in (ph or {}).items()} }")
+        out.append(rec)
+        del w
+        gc.collect()
+        torch.cuda.empty_cache()
+    res = {"world": world, "shards": out, "steps": steps, "warmup": warmup,
+           "what": "each rank's LPT shard of a world-rank step timed alone on ONE MI355X (no gather); a projection"}
+    if len(out) == world:
+        mx = max(x["ms_per_step"] for x in out)
+        res["max_shard_ms"] = mx
+        res["max_over_mean"] = mx / (sum(x["ms_per_step"] for x in out) / world)
+        res["gather_bytes_to_rank0"] = sum(x["gather_send_bytes"] for x in out)
+        pred = [x["predicted_shard_s"] * 1e3 for x in out]
+        res["predicted_vs_measured"] = {"max_abs_rel_err": max(abs(p - x["ms_per_step"]) / x["ms_per_step"]
+                                                               for p, x in zip(pred, out)),
+                                        "predicted_max_over_mean": max(pred) / (sum(pred) / world),
+                                        "model": "sharding.shard_cost (phase model fitted to one-GPU shard timings)"}
+        if t1_ms:
+            res["t1_ms"] = t1_ms
+            res["projected_efficiency"] = t1_ms / (world * mx)
+            res["projected_value_cols_per_s"] = sharding.units_cols(model_units(a)) / (mx * 1e-3)
+        if t1_phase and all(x["phase_s"] for x in out):
+            res["t1_phase_s"] = t1_phase
+            res["share_ratio"] = {k: max(x["phase_s"][k] for x in out) / (t1_phase[k] / world)
+                                  for k in t1_phase if t1_phase[k] > 0}
+    return res
+
+
+def decoder_run(a, dev, layers=None, samples=128, seq=2048):
+    """extra.decoder / --workload decoder: the REAL calibration flow of a PT2LLMQuantizer.quantize
+    user (main.py:232-308) on a Llama-2-7B-shaped model, one decoder layer after another: a
+    random-init fp16 transformers LlamaForCausalLM (hidden 4096, MLP 11008, 32 heads; no
+    checkpoint exists offline), `samples` calibration sequences of `seq` random token ids
+    (N = samples x seq = 262144 rows per linear), per layer: the layer's forward over every sample
+    with the capture hooks streaming each linear's input into its Gram (4 Grams: q/k/v, o,
+    gate/up, down), the layer's batched inverses and grouped block loops (GramsFirst), the
+    reference's write-back, the layer's forward again on the written-back weights (the next
+    layer's inputs: propagate="layerwise"), the results copied to the host as the reference
+    returns them.  Only the 7 linears of one layer are independent here (layer L+1's activations
+    depend on layer L's write-back), unlike the headline step's 128 batched units."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    L = a.layers if layers is None else layers
+    cfg = LlamaConfig(hidden_size=4096, intermediate_size=11008, num_hidden_layers=L, num_attention_heads=32,
+                      num_key_value_heads=32, vocab_size=32000, max_position_embeddings=4096)
+    cfg._attn_implementation = "sdpa"
+    t0 = time.perf_counter()
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = LlamaForCausalLM(cfg).to(torch.float16)
+    model.eval()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    toks = [torch.randint(0, cfg.vocab_size, (1, seq), generator=g).to(dev) for _ in range(samples)]
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t0
+    q = pt2q.PT2LLMQuantizer(model, None, "llama", block_size=a.block_size, use_ssr=not a.no_ssr,
+                             device=str(dev))
+    timings = []
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    res = q.quantize(toks, writeback="reference", propagate="layerwise", timings=timings)
+    torch.cuda.synchronize()
+    tot = time.perf_counter() - t1
+    cols = sum(v["T"].shape[1] for v in res.values())
+    steady = timings[1:] if len(timings) > 1 else timings
+    per = {k: float(np.mean([t[k] for t in steady])) for k in steady[0] if k != "layer"}
+    out = {"what": "PT2LLMQuantizer.quantize(propagate='layerwise', writeback='reference'): the real per-decoder-layer "
+                   "flow (capture forwards + streamed Grams -> batched inverses + grouped loops -> write-back -> "
+                   "forward on the written-back layer -> results to host)",
+           "model": f"random-init fp16 LlamaForCausalLM, {L} layers x (q,k,v,o 4096x4096; gate,up 11008x4096; down 4096x11008)",
+           "calibration": f"{samples} x {seq} random token ids (N = {samples * seq} rows per linear)",
+           "layers": L, "linears": len(res), "weight_columns": cols, "total_s": tot,
+           "cols_per_s": cols / tot, "s_per_decoder_layer": tot / L,
+           "s_per_decoder_layer_steady": per["total_s"], "phase_s_per_layer_steady": per,
+           "first_layer_s": timings[0]["total_s"], "setup_s": t_setup,
+           "projected_32_layers_s": per["total_s"] * 31 + timings[0]["total_s"] if L < 32 else tot}
+    del q, model, res, toks
+    gc.collect()
+    torch.cuda.empty_cache()
     return out
 
 
@@ -224,6 +355,11 @@ def launch_or_check(a, argv):
       on 127.0.0.1 as a CHILD process (this process has not touched the GPU and never execs).
     * WORLD_SIZE set (torchrun / the driver's launcher): --gpus, when given, must equal it."""
     env_world = os.environ.get("WORLD_SIZE")
+    if a.shard is not None:  # one process on one GPU times the shards of a --gpus N step
+        if env_world is not None and int(env_world) > 1:
+            print("[bench] refusing: --shard runs in ONE process (no launcher)", file=sys.stderr)
+            return 2
+        return None
     if env_world is not None:
         if a.gpus is not None and a.gpus != int(env_world):
             print(f"[bench] refusing: --gpus {a.gpus} but WORLD_SIZE={env_world}", file=sys.stderr)
@@ -444,10 +580,14 @@ class ModelStep:
     stream different rows -- a real model's layers have their own activations, and a single
     shared tensor would let concurrent items hit each other's X lines in L2 / MALL."""
 
-    def __init__(self, a, rank, world, dev, io):
+    def __init__(self, a, rank, world, dev, io, shard_only=False):
         self.units = model_units(a)
         self.shards = sharding.assign_lpt([sharding.unit_cost(u, a.block_size) for u in self.units], world)
         self.mine = self.shards[rank]
+        # shard_only: rank `rank`'s shard of a `world`-rank step on this one GPU (no process
+        # group): the step skips the gather and keeps the bytes it would have sent (bench --shard)
+        self.shard_only, self.rank = shard_only, rank
+        self.gather_bytes = 0
         self.bs, self.ssr = a.block_size, not a.no_ssr
         self.pipe = None if a.no_overlap else pt2q.UnitPipeline(dev, self.bs, self.ssr, lanes=a.lanes)
         self.schedule = a.schedule
@@ -488,7 +628,13 @@ class ModelStep:
     def step(self):
         gf = self.gf if self.schedule == "grams-first" and self.pipe is not None else None
         res, _ = sharding.quantize_units_sharded(self.units, self.provider, run_unit=self.run_unit,
-                                                 pack=True, dst=0, grams_first=gf)
+                                                 pack=True, dst=0, grams_first=gf, mine=self.mine,
+                                                 gather=not self.shard_only, block_size=self.bs)
+        if self.shard_only:
+            # the bytes this rank's packed results would put on its xGMI link (rank 0 keeps its own)
+            self.gather_bytes = 0 if self.rank == 0 else sum(e[4] for e in sharding._manifest(res))
+            self.gathered = None
+            return res
         self.gathered = None if res is None else len(res)  # linears whose results reached rank 0
         return res
 
@@ -844,10 +990,14 @@ class DryStep:
     shards, sharding.quantize_units_sharded and gather as ModelStep, with a stub run_unit that
     returns small deterministic outputs instead of launching kernels."""
 
-    def __init__(self, a, rank, world, dev, io):
+    def __init__(self, a, rank, world, dev, io, shard_only=False):
         self.units = model_units(a)
         self.shards = sharding.assign_lpt([sharding.unit_cost(u, a.block_size) for u in self.units], world)
         self.mine = self.shards[rank]
+        # shard_only: rank `rank`'s shard of a `world`-rank step on this one GPU (no process
+        # group): the step skips the gather and keeps the bytes it would have sent (bench --shard)
+        self.shard_only, self.rank = shard_only, rank
+        self.gather_bytes = 0
         self.bs = a.block_size
         self.ran = []
 
@@ -874,6 +1024,41 @@ class DryStep:
                                                  pack=False, dst=0)
         self.last = res
         return res
+
+
+def shard_main(a, dev, io):
+    """bench.py --gpus N --shard r|all (one process, one GPU): rank r's LPT shard of an N-rank
+    model step timed alone ('all': the whole step on this GPU first -- T1 and its phases -- then
+    every rank's shard); one JSON line with the per-shard times and the projection."""
+    world = a.gpus or 1
+    if a.workload != "model" or world < 2 or a.dry_run:
+        raise SystemExit("--shard needs the model workload and --gpus N >= 2")
+    ranks = list(range(world)) if a.shard == "all" else [int(a.shard)]
+    t1 = t1p = None
+    if a.shard == "all":
+        w = ModelStep(a, 0, 1, dev, io)
+        for _ in range(a.warmup):
+            w.step()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.steps):
+            t0 = time.perf_counter()
+            w.step()
+            torch.cuda.synchronize()
+            ts.append(1e3 * (time.perf_counter() - t0))
+        t1 = float(np.median(ts))
+        t1p = w.phase_step()
+        log(0, f"whole step on one GPU: {t1:.1f} ms, phases { {k: round(v * 1e3, 1) for k, v in t1p.items()} }")
+        del w
+        gc.collect()
+        torch.cuda.empty_cache()
+    res = shard_runs(a, dev, io, world, ranks, t1, t1p, steps=a.steps, warmup=max(a.warmup, 2))
+    res.update({"metric": "one-GPU shard timing (projection; no RCCL, no scaling measurement)",
+                "model": a.model, "config": sharding.MODELS[a.model]["config"],
+                "workload": describe_units(model_units(a), a.layers), "tokens": a.tokens,
+                "block_size": a.block_size, "io_dtype": a.io_dtype})
+    print(json.dumps(res), flush=True)
+    return 0
 
 
 def main(argv=None):
@@ -911,6 +1096,17 @@ def main(argv=None):
     if world > 1:
         world, rank = dist.get_world_size(), dist.get_rank()
     io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[a.io_dtype]
+    if a.shard is not None:
+        return shard_main(a, dev, io)
+    if a.workload == "decoder":  # one line: the layer-by-layer flow (see decoder_run)
+        if world > 1:
+            raise SystemExit("--workload decoder runs on one GPU")
+        r = decoder_run(a, dev)
+        print(json.dumps({"metric": "weight-columns quantized/sec (and s/layer) at d=4096 [real calibration flow, "
+                                    "decoder layer by decoder layer]", "value": r["cols_per_s"], "unit": "cols/s",
+                          "n_gpus": 1, "higher_is_better": True, "dtype": "fp16->f32",
+                          "data": "synthetic (random-init model, random token ids)", "decoder": r}), flush=True)
+        return 0
     N, bs, d = a.tokens, a.block_size, a.hidden
     use_ssr = not a.no_ssr
 
@@ -1140,14 +1336,33 @@ def main(argv=None):
                 extra["h2d"] = {"error": f"{type(e).__name__}: {e}"}
             gc.collect()
             torch.cuda.empty_cache()
-        if (a.workload == "model" and world == 1 and not a.no_extra and not a.no_configs
-                and not a.hidden_given and a.layers == sharding.MODELS[a.model]["layers"]):
-            log(rank, "per-config runs ...")
+        full_model = (a.workload == "model" and world == 1 and not a.no_extra and not a.hidden_given
+                      and a.layers == sharding.MODELS[a.model]["layers"])
+        if full_model and (not a.no_configs or not a.no_shards or not a.no_decoder):
             units_main = work.units
             del work  # the headline model's resident inputs and buffers (~150 GB) make room
             gc.collect()
             torch.cuda.empty_cache()
-            extra["configs"] = config_runs(a, dev)
+            if not a.no_shards and a.schedule == "grams-first":
+                log(rank, "8-rank shards, one at a time on this GPU (projection) ...")
+                try:
+                    extra["shards8"] = shard_runs(a, dev, io, 8, t1_ms=ms_per_step,
+                                                  t1_phase=roof.get("phase_s") if roof else None)
+                except Exception as e:  # reported, never allowed to drop the line
+                    extra["shards8"] = {"error": f"{type(e).__name__}: {e}"}
+                gc.collect()
+                torch.cuda.empty_cache()
+            if not a.no_decoder and a.model == "llama-2-7b":
+                log(rank, "decoder flow (PT2LLMQuantizer.quantize, layer by layer) ...")
+                try:
+                    extra["decoder"] = decoder_run(a, dev)
+                except Exception as e:  # reported, never allowed to drop the line
+                    extra["decoder"] = {"error": f"{type(e).__name__}: {e}"}
+                gc.collect()
+                torch.cuda.empty_cache()
+            if not a.no_configs:
+                log(rank, "per-config runs ...")
+                extra["configs"] = config_runs(a, dev)
             work = argparse.Namespace(units=units_main)
         res["extra"] = extra
         if world == 1 and not a.no_cpu_baseline and a.workload != "split":

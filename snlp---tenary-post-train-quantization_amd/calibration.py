@@ -208,11 +208,59 @@ def dequantize_weight_reference(params, block_size: int) -> torch.Tensor:
     return W[:, torch.argsort(perm)]
 
 
+class _StopForward(Exception):
+    pass
+
+
+@torch.no_grad()
+def capture_layer_inputs(model: nn.Module, layer: nn.Module, samples, model_dev=None):
+    """The inputs of decoder layer `layer` (normally layer 0) for every calibration sample:
+    [(args, kwargs)] as the model's forward passes them, recorded by a forward pre-hook that
+    stops the forward there (only the embeddings and the layers before it run).  The forward
+    is called with use_cache=False (a KV cache never changes a single forward's outputs)."""
+    rec = []
+
+    def hook(mod, args, kwargs):
+        rec.append((tuple(args), dict(kwargs)))
+        raise _StopForward
+
+    h = layer.register_forward_pre_hook(hook, with_kwargs=True)
+    try:
+        for sample in samples:
+            try:
+                model(sample.to(model_dev) if model_dev is not None else sample, use_cache=False)
+            except _StopForward:
+                pass
+    finally:
+        h.remove()
+    return rec
+
+
+def _with_hidden(args, kwargs, x):
+    if args:
+        return (x,) + tuple(args[1:]), kwargs
+    kw = dict(kwargs)
+    kw["hidden_states"] = x
+    return args, kw
+
+
+@torch.no_grad()
+def propagate_layer(layer: nn.Module, inputs):
+    """Run the (quantised, written-back) layer on every sample's recorded inputs -> the next
+    layer's inputs (the same hidden states the reference's full-model forward would hand it)."""
+    out = []
+    for args, kwargs in inputs:
+        y = layer(*args, **kwargs)
+        y = y[0] if isinstance(y, (tuple, list)) else y
+        out.append(_with_hidden(args, kwargs, y))
+    return out
+
+
 @torch.no_grad()
 def quantize_decoder_layer(layer: nn.Module, run_forward, block_size: int = 128,
                            use_ssr: bool = True, percdamp: float = 0.01, layer_idx: int = 0,
                            writeback: str = "reference", device=None,
-                           pipeline: Optional["engine.UnitPipeline"] = None):
+                           pipeline: Optional["engine.UnitPipeline"] = None, grams_first=None):
     """One iteration of main.py:258-303 for decoder layer `layer`.
 
     run_forward(capture) must run the calibration forwards (calling capture.next_pass() between
@@ -221,14 +269,28 @@ def quantize_decoder_layer(layer: nn.Module, run_forward, block_size: int = 128,
     "correct": gptq.py:201-230 reconstruction, "none": leave weights untouched).  With a
     UnitPipeline the input groups' tails (their Grams are already captured) run concurrently on
     its lanes -- they are independent: every input was captured before any write-back -- with
-    results identical to the one-after-another order."""
+    results identical to the one-after-another order.
+    With a sharding.GramsFirst (`grams_first`, built on such a pipeline) the captured Grams go into
+    its packed slots instead: the layer's Hessian inverses run batched per width and the block
+    loops grouped by shape on the lanes (q/k/v/o, gate/up) -- bit-identical again."""
     linears = find_linear_layers(layer)
     cap = GramCapture(linears, device)
     with cap:
         run_forward(cap)
     results = {}
     issued = []
-    for acc, names in cap.groups():
+    groups = cap.groups()
+    if grams_first is not None:
+        gf = grams_first
+        gf.begin([(g, acc.m, acc.nsamples) for g, (acc, _) in enumerate(groups)])
+        for g, (acc, _) in enumerate(groups):
+            gf.set_gram(g, acc.G)
+        gf.inverses()
+        jobs = [(g, [linears[nm].weight.data.to(acc.device) for nm in names], acc.nsamples)
+                for g, (acc, names) in enumerate(groups)]
+        runs = gf.tails(jobs)
+        issued = [(names, run) for (_, names), run in zip(groups, runs)]
+    for acc, names in ([] if grams_first is not None else groups):
         Ws = [linears[nm].weight.data.to(acc.device) for nm in names]
         if pipeline is not None:
             issued.append((names, pipeline.run(Ws, G=acc.G, nsamples=acc.nsamples)))
@@ -236,7 +298,7 @@ def quantize_decoder_layer(layer: nn.Module, run_forward, block_size: int = 128,
             issued.append((names, engine.quantize_shared(Ws, acc.G, acc.nsamples, block_size, use_ssr,
                                                          percdamp)))
     for names, outs in issued:
-        if pipeline is not None:
+        if pipeline is not None or grams_first is not None:
             outs = outs.finish()
         for nm, out in zip(names, outs):
             lin = linears[nm]

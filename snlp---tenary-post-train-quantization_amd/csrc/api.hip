@@ -13,15 +13,21 @@
 
 namespace {
 
-// Development overrides (tools/ probes only), read once at library load -- see Pt2qTuning.
+// Tuning, read once at library load -- see Pt2qTuning.  Release builds read only the debug
+// spin cap; every kernel-selecting variable is a development-build (PT2Q_DEV_PROBES) override.
 Pt2qTuning load_tuning() {
   Pt2qTuning t;
+#ifdef PT2Q_DEV_PROBES
   auto geti = [](const char* k, int& v) {
     if (const char* e = std::getenv(k)) v = std::atoi(e);
   };
   auto getb = [](const char* k, bool& v) {
     if (const char* e = std::getenv(k)) v = e[0] != '0';
   };
+  // Kernel-selecting overrides and knock-outs: read only by a development build (make
+  // DEV_PROBES=1, tools/build_dev_lib.sh).  The release library runs the defaults of Pt2qTuning
+  // whatever the environment holds, so no variable can switch it onto a kernel variant the GPU
+  // tests do not cover (or onto a knock-out whose results are garbage).
   geti("PT2Q_GRAM_SUPER", t.gram_super);
   geti("PT2Q_GRAM_GROUPS", t.gram_groups);
   geti("PT2Q_GRAM_CUS", t.gram_cus);
@@ -48,18 +54,17 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_ATQ_PC", t.atq_pc);
   getb("PT2Q_ATQ_PC_REGS", t.atq_pc_regs);
   geti("PT2Q_EF_V2", t.ef_v2);
-#ifdef PT2Q_DEV_PROBES
-  // ef2 knock-outs (tools/ef2_knock.sh; results garbage): only a development build
-  // (make DEV_PROBES=1) reads this, so a stray variable cannot corrupt a release library's results
+  // knock-outs (tools/ef2_knock.sh, tools/atq_knock.sh; results garbage)
   geti("PT2Q_EF2_PROBE", t.ef2_probe);
   geti("PT2Q_ATQ_PROBE", t.atq_probe);
-#endif
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
   getb("PT2Q_EF2_G1LDS", t.ef2_g1lds);
   if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;
   if (t.wide_waves != 8) t.wide_waves = 4;
   if (t.atq_occ != 0) t.atq_occ = 6;
+#endif
+  // release and development: the stall-reporting test hook (tests/test_gpu_status.py)
   if (const char* e = std::getenv("PT2Q_DEBUG_SPIN_CAP")) {
     const long c = std::atol(e);
     if (c >= 0) t.spin_cap_long = t.spin_cap_short = t.spin_cap_fallback = c;

@@ -516,6 +516,11 @@ PT2Q_DEV int block_rows_vec(const BlockArgs& A, int base) {
       v[g][s] = R.w[s] - (a * R.t[s] + m);  // the error term, in place of w
     }
   }
+  // The stage is accessed as float (W, error terms) and as uint32 / uint4 (codes); the library
+  // is built without -fno-strict-aliasing, so a compiler barrier keeps each typed phase's
+  // accesses on its side (type-based alias analysis could otherwise move a uint32 store above
+  // the float reads of W, or the error-term float stores above the code loads).
+  asm volatile("" ::: "memory");
   // codes: lane (r, l) puts row r's four group bytes of column k at dword 4 k + r; lane q reads
   // column q + 64 h (16 bytes, row-group-major) and transposes it to row order
 #pragma unroll
@@ -533,6 +538,7 @@ PT2Q_DEV int block_rows_vec(const BlockArgs& A, int base) {
       *(uint4*)(A.Tt + (long)A.blk[k] * A.ldt + base) = y;
     }
   }
+  asm volatile("" ::: "memory");  // code loads of the stage before its float reuse (see above)
   // error terms, a chunk of 32 columns at a time
   if (A.Et && !(A.probe & 128)) {
 #pragma unroll

@@ -33,7 +33,7 @@ constexpr int EF_T = 128;                    // output tile (e and i)
 constexpr int EF_KH = 64;                    // k rows per LDS stage
 constexpr int EF_ROWB = EF_T * 4;            // 512 B per k row of a panel
 constexpr int EF_PANEL = EF_KH * EF_ROWB;    // 32 KiB
-constexpr int EF_STAGE = 2 * EF_PANEL;       // A + B
+[[maybe_unused]] constexpr int EF_STAGE = 2 * EF_PANEL;  // A + B (ef_gemm_kernel: development builds)
 constexpr int EF_DMA = 16;                   // DMA instructions per wave per stage
 constexpr int EF_CV = 16;                    // C float4 loads (= stores) per lane per tile
 constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropped access)
@@ -442,6 +442,9 @@ PT2Q_DEV void ef_wbar_store(int n, __amdgpu_buffer_rsrc_t rp, bool valid, int e0
   }
 }
 
+#ifdef PT2Q_DEV_PROBES
+// ef_gemm_kernel (one workgroup per CU): superseded by ef2_gemm_kernel; kept for A/B runs in
+// development builds only (PT2Q_EF_V2=0), never reachable from a release library.
 template <int J>
 PT2Q_DEV void ef_wbar_all(const int (&prow)[2], const u32x4 (&pend)[EF_CV], float* red) {
   if constexpr (J < 32) {
@@ -576,6 +579,8 @@ __global__ __launch_bounds__(256) void ef_gemm_kernel(EfArgs a0, long wt_bytes, 
     ef_wbar_store(a0.n, prp, true, pe0, pi0, red);
   }
 }
+
+#endif  // PT2Q_DEV_PROBES
 
 // ---- ef2_gemm_kernel: the same product with two workgroups per CU ----------------------------
 // ef_gemm_kernel holds ONE workgroup per CU (two 64-row K stages = 128 KiB of LDS, 336 registers):
@@ -905,15 +910,21 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
     const int grid2 = std::min(a.ntile * a.nz, pt2q_tuning().ef2_per_cu * cus);
     if (bs <= 2 * E2_KS)
       hipLaunchKernelGGL(ef2_gemm_kernel<2>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
-    else if (pt2q_tuning().ef2_g1lds)
-      hipLaunchKernelGGL((ef2_gemm_kernel<4, true>), dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
-    else
+#ifdef PT2Q_DEV_PROBES
+    else if (!pt2q_tuning().ef2_g1lds)  // development A/B only (PT2Q_EF2_G1LDS=0)
       hipLaunchKernelGGL(ef2_gemm_kernel<4>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
+#endif
+    else
+      hipLaunchKernelGGL((ef2_gemm_kernel<4, true>), dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   }
+#ifdef PT2Q_DEV_PROBES
   const int grid = std::min(a.ntile * a.nz, cus);
   hipLaunchKernelGGL(ef_gemm_kernel, dim3(grid), dim3(256), 0, st, a, wt_bytes, part_bytes);
   PT2Q_LAUNCH_CHECK();
   return PT2Q_OK;
+#else
+  return PT2Q_E_UNSUPPORTED;  // unreachable: ef_v2 is 1 in a release library
+#endif
 }

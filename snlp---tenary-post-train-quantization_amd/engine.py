@@ -175,6 +175,9 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[t
     if s1d is not None:
         if aga != _lib.AGA_ACT or block_size < m or m <= 512 or s1d.numel() != m + 1:
             raise ValueError("quantize_blocks: s1d is for one-block (per-channel) variant-M loops, m + 1 floats")
+        # the library reads it as m + 1 raw fp32 values on W's device
+        if s1d.dtype != torch.float32 or not s1d.is_contiguous() or s1d.device != dev:
+            raise ValueError("quantize_blocks: s1d must be a contiguous fp32 tensor on W's device")
         A, flags = s1d, flags | _lib.FLAG_S1_GIVEN
     ws = workspace if workspace is not None and workspace.numel() >= nbytes else _lib.workspace(nbytes, dev)
     if Hinv is None:
@@ -197,9 +200,15 @@ def s1_from_gram_batched(G: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     """S1 = S·1 and d = 1ᵀS1 (quantizer.py:215-218) of every m x m raw Gram in G (batch, m, m) in
     one launch pair: row z of the (batch, m + 1) result is S1 then d of item z, bit-identical to
     pt2q_s1_from_gram per item (quantize_blocks(..., s1d=row) consumes it)."""
+    _lib.require_device(G)
+    if G.dim() != 3 or G.shape[1] != G.shape[2] or G.dtype != torch.float32 or not G.is_contiguous():
+        raise ValueError("s1_from_gram_batched: G must be a contiguous fp32 (batch, m, m) device tensor")
     b, m = G.shape[0], G.shape[-1]
     if out is None:
         out = torch.empty((b, m + 1), dtype=torch.float32, device=G.device)
+    elif (out.shape != (b, m + 1) or out.dtype != torch.float32 or not out.is_contiguous()
+          or out.device != G.device):
+        raise ValueError("s1_from_gram_batched: out must be a contiguous fp32 (batch, m + 1) tensor on G's device")
     _lib.check(_lib.lib().pt2q_s1_from_gram_batched(_lib.ptr(G), G.stride(1), m, b, G.stride(0) if b > 1 else m * m,
                                                     _lib.ptr(out), _lib.stream_of(G.device)),
                "pt2q_s1_from_gram_batched")

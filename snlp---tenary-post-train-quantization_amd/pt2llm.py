@@ -64,14 +64,31 @@ class PT2LLMQuantizer:
                            "dataset download (utils.py:47-60) is not available offline")
 
     @torch.no_grad()
-    def quantize(self, calibration_samples=None, writeback: str = "reference"):
+    def quantize(self, calibration_samples=None, writeback: str = "reference",
+                 propagate: str = "model", schedule: str = "grams-first", timings=None):
         """main.py:232-308: decoder layer by decoder layer, capture the linears' inputs over the
         calibration forwards, quantise every linear, write the weights back.  The captured
         inputs go straight into per-input Grams (calibration.GramCapture), so q/k/v and gate/up
         share one Gram and one Cholesky inverse; results equal quantize_layer on the
-        concatenated activations bit-for-bit.  Returns {name: {alpha, mu, T, perm}} on CPU."""
+        concatenated activations bit-for-bit.  Returns {name: {alpha, mu, T, perm}} on CPU.
+
+        propagate="model" runs, per decoder layer, a full-model forward per sample as the
+        reference does (main.py:280-282; O(layers²) layer forwards).  "layerwise" records layer
+        0's inputs once (calibration.capture_layer_inputs) and then runs each layer on its
+        recorded inputs: for capture, and -- after the write-back -- to produce the next layer's
+        inputs (calibration.propagate_layer).  Those are the hidden states the full forward hands
+        that layer, so the results are the same; the forward work drops from L² to 2L layer passes.
+        schedule="grams-first": one layer's captured Grams go into a sharding.GramsFirst (its
+        inverses batched per width, the block loops grouped by shape on the lanes); "lanes": one
+        unit per lane of an engine.UnitPipeline.  Bit-identical.
+        timings: a list that receives one dict per decoder layer (wall seconds of capture,
+        quantise, write-back, propagate and the host copies; device-synchronised between them)."""
+        import time
+        from . import sharding
         if self.model is None:
             raise RuntimeError("PT2LLMQuantizer.quantize needs a model")
+        if propagate not in ("model", "layerwise") or schedule not in ("grams-first", "lanes"):
+            raise ValueError("propagate must be model|layerwise and schedule grams-first|lanes")
         if calibration_samples is None:
             calibration_samples = self.get_calibration_data()
         layers = calibration.get_llm_layers(self.model, self.model_type)
@@ -82,13 +99,43 @@ class PT2LLMQuantizer:
         # the units of one decoder layer are independent: their tails run on concurrent lanes
         pipe = engine.UnitPipeline(self.device, self.block_size, self.use_ssr,
                                    self.percdamp)
+        gf = sharding.GramsFirst(pipe, self.device) if schedule == "grams-first" else None
+        inputs = (calibration.capture_layer_inputs(self.model, layers[0], calibration_samples, model_dev)
+                  if propagate == "layerwise" else None)
+
+        def mark():
+            if timings is not None:
+                torch.cuda.synchronize(self.device)
+            return time.perf_counter()
+
         for idx, layer in enumerate(layers):
-            def run(cap):
-                for sample in calibration_samples:
-                    self.model(sample.to(model_dev))
-                    cap.next_pass()
-            res = calibration.quantize_decoder_layer(layer, run, self.block_size, self.use_ssr,
-                                                     self.percdamp, idx, writeback, self.device, pipe)
+            t0 = mark()
+            if inputs is None:
+                def run(cap):
+                    for sample in calibration_samples:
+                        self.model(sample.to(model_dev))
+                        cap.next_pass()
+            else:
+                def run(cap, layer=layer):
+                    for args, kwargs in inputs:
+                        layer(*args, **kwargs)
+                        cap.next_pass()
+            tq = [0.0]
+
+            def run_timed(cap):
+                run(cap)
+                tq[0] = mark()
+            res = calibration.quantize_decoder_layer(layer, run_timed, self.block_size, self.use_ssr,
+                                                     self.percdamp, idx, writeback, self.device,
+                                                     None if gf is not None else pipe, gf)
+            t2 = mark()
+            if inputs is not None and idx + 1 < len(layers):
+                inputs = calibration.propagate_layer(layer, inputs)
+            t3 = mark()
             for name, p in res.items():
                 self.quantized_params[name] = {k: v.cpu() for k, v in p.items()}
+            t4 = mark()
+            if timings is not None:
+                timings.append({"layer": idx, "capture_s": tq[0] - t0, "quantize_writeback_s": t2 - tq[0],
+                                "propagate_s": t3 - t2, "to_host_s": t4 - t3, "total_s": t4 - t0})
         return self.quantized_params

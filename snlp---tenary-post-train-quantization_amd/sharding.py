@@ -118,6 +118,65 @@ def unit_cost(unit, block_size: int = 128) -> float:
     return t
 
 
+# Phase model of one rank's grams-first step (GramsFirst: every Gram, then the batched inverses,
+# then the grouped block loops on the lanes) -- what a rank's SHARD costs, as opposed to unit_cost's
+# additive per-unit seconds.  The fixed latencies that do not shrink with the shard are explicit:
+# the batched inverse's serial panel chain per chunk (each chunk of <= chunk items of one width
+# walks m / 64 dependent panel steps whatever its size) and the grouped loop's per-block launch
+# chain (every block of a group is a short sequence of dependent launches).  Constants: see
+# fit notes at SHARD_MODEL.
+SHARD_MODEL = dict(
+    gram_rate=1.19e15,      # N·m·(m+1) per second, the batched 16-bit Gram (work done)
+    gram_launch=4e-4,       # s per batched launch (ramp + last partial wave)
+    inv_rate=1.25e14,       # m³ per second, the trailing updates of the batched inverse (gemmx)
+    inv_step=1.7e-4,        # s per 64-column panel step of one chunk (the serial chain)
+    loop_nr=6.5e-12,        # s per n·r (error feedback + SSR passes over the remaining columns)
+    loop_block=4.5e-5,      # s per block of one grouped loop (its launch chain), any group size
+    loop_pc=4.0e-11,        # s per n·m of a per-channel linear (one block: ATQ passes)
+    lanes=3,                # tail lanes the groups spread over
+)
+
+
+def shard_cost(units, block_size: int = 128, chunk: int = 32, group: int = 16, model=None) -> float:
+    """Modelled seconds of ONE rank's grams-first step over `units` (see SHARD_MODEL)."""
+    c = dict(SHARD_MODEL, **(model or {}))
+    by_w = {}
+    lins = []
+    for _, ls, N in units:
+        m = ls[0][2]
+        by_w.setdefault((m, int(N)), []).append(len(ls))
+        lins += [(n, m) for _, n, _ in ls]
+    t_gram = sum(len(v) * float(N) * m * (m + 1) / c["gram_rate"] + c["gram_launch"] for (m, N), v in by_w.items())
+    t_inv = 0.0
+    for (m, N), v in by_w.items():
+        if block_size >= m:
+            continue  # per-channel: no inverse
+        cnt = len(v)
+        t_inv += -(-cnt // chunk) * (m / 64.0) * c["inv_step"] + cnt * float(m) ** 3 / c["inv_rate"]
+    # tails: same-shape linears in groups of <= group (at least one group per lane), groups on
+    # the lanes longest first; a group's time is its per-block launch chain or its work, the
+    # larger, and the phase is the busiest lane or the chip's total work, the larger
+    shapes = {}
+    for n, m in lins:
+        shapes[(n, m)] = shapes.get((n, m), 0) + 1
+    groups, busy = [], 0.0
+    for (n, m), cnt in shapes.items():
+        nblk = -(-m // block_size) if block_size < m else 1
+        rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))
+        per = float(n) * rsum * c["loop_nr"] if nblk > 1 else float(n) * m * c["loop_pc"]
+        size = max(1, min(group, -(-cnt // c["lanes"])))
+        for g0 in range(0, cnt, size):
+            g = min(size, cnt - g0)
+            groups.append(max(nblk * c["loop_block"], g * per))
+            busy += g * per
+    load = [0.0] * c["lanes"]
+    for t in sorted(groups, reverse=True):
+        i = min(range(len(load)), key=lambda k: load[k])
+        load[i] += t
+    t_tail = max(max(load) if load else 0.0, busy)
+    return t_gram + t_inv + t_tail
+
+
 # ----------------------------------------------------------------- heterogeneous result gather
 
 _ALIGN = 16  # every entry starts 16-byte aligned, so the receiver views the bytes in place
@@ -175,7 +234,10 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
     on dst, None elsewhere.  The receive buffers go on `device`, else on the device of dst's own
     results, else (dst holds none) the current HIP device under RCCL / the CPU under gloo.
     Only the senders pack their bytes: dst keeps its own tensors as they are (one rank: no copy
-    at all -- packing a 13B step's 1,400 result tensors cost as many device copies)."""
+    at all -- packing a 13B step's 1,400 result tensors cost as many device copies), so dst's own
+    entries in the returned dict ALIAS the caller's tensors (they may be non-contiguous views;
+    clone before modifying them in place); received entries are views into one receive buffer
+    per sender."""
     own = {name: dict(entry) for name, entry in results.items()}
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return own
@@ -195,8 +257,8 @@ def gather_results(results: Dict[str, Dict[str, torch.Tensor]], dst: int = 0, gr
     merged = own
     dev = device
     if dev is None:
-        if manifest:
-            dev = next(iter(next(iter(results.values())).values())).device
+        if manifest:  # the first manifest entry's tensor (a name may map to an empty dict)
+            dev = results[manifest[0][0]][manifest[0][1]].device
         elif dist.get_backend(group) == "nccl":
             dev = torch.device("cuda", torch.cuda.current_device())
         else:
@@ -227,7 +289,7 @@ def units_cols(units) -> int:
 def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callable] = None,
                            block_size: int = 128, use_ssr: bool = True, percdamp: float = 0.01,
                            pack: bool = True, dst: int = 0, group=None, gather: bool = True,
-                           grams_first: Optional["GramsFirst"] = None):
+                           grams_first: Optional["GramsFirst"] = None, mine: Optional[Sequence[int]] = None):
     """Quantise a list of independent work units across the ranks of `group` (LPT shards), then
     gather every linear's result to `dst`.
 
@@ -237,12 +299,17 @@ def quantize_units_sharded(units, provider: Callable, run_unit: Optional[Callabl
     the next unit's Gram overlapping this unit's tail on a second stream).
     grams_first (a GramsFirst) replaces run_unit: every Gram of this rank's units first, then
     their tails.
+    mine: this rank's unit indices, overriding the LPT assignment (the caller's own shards, e.g.
+    one rank's shard of a larger world timed alone on one GPU, bench.py --shard).
     Results are {f"{unit}.{proj}": {"T2" (2-bit packed, utils.py:189-219) or "T", "alpha", "mu",
-    "perm", "shape"}}.  Returns (results on dst or None, this rank's unit indices)."""
+    "perm", "shape"}}; every "shape" entry (int64 (2,): T's n, m) is a row of ONE device table
+    per step (a single host-to-device copy), i.e. a read-only view -- clone it before writing to
+    it or saving it alone.  Returns (results on dst or None, this rank's unit indices)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    shards = assign_lpt([unit_cost(u) for u in units], world)
-    mine = shards[rank]
+    if mine is None:
+        mine = assign_lpt([unit_cost(u, block_size) for u in units], world)[rank]
+    mine = list(mine)
     if run_unit is None and grams_first is None:
         from . import engine  # noqa: WPS433 (device code only when quantising for real)
 
@@ -476,6 +543,12 @@ class GramsFirst:
             self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
         self.engine.gram(X2, G=self._gbuf(key, m), workspace=self.ws[m], check=False)
         torch.bitwise_or(self.stall, self.lib.status_view(self.ws[m]), out=self.stall)
+
+    def set_gram(self, key, G: torch.Tensor):
+        """A unit's raw Gram formed elsewhere (calibration.GramAccumulator): copied into its slot
+        on the current stream (begin() first)."""
+        g, z = self.slot[key]
+        self.groups[g]["G"][z].copy_(G)
 
     def flush(self):
         """Issue the batched Grams gram() collected: one pt2q_gram_batched sequence per group

@@ -111,3 +111,31 @@ def test_model_layer1_teacher_forced_vs_reference(pt2q):
         assert np.array_equal(out.mu.cpu().numpy(), g[f"mu{i}"]), name
         check_vs_unmodified_reference(g, i, name, out.perm.cpu().numpy(), out.T.cpu().numpy(),
                                       out.alpha.cpu().numpy(), out.mu.cpu().numpy())
+
+
+def test_model_loop_layerwise_and_schedules_identical(pt2q):
+    """PT2LLMQuantizer.quantize(propagate="layerwise") -- layer 0's inputs recorded once, every
+    later layer fed by the previous layer's forward on its written-back weights -- quantises the
+    same activations as the reference's full-model forward per layer (main.py:280-282), and the
+    grams-first schedule (batched inverses, grouped loops) equals one unit per lane: every
+    result of the three runs is bit-identical (model on the CPU, one thread, as above)."""
+    runs = {}
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        for key, kw in {"model/gf": dict(propagate="model"), "layerwise/gf": dict(propagate="layerwise"),
+                        "model/lanes": dict(propagate="model", schedule="lanes")}.items():
+            model, samples = tiny_llama_and_samples()
+            q = pt2q.PT2LLMQuantizer(model, None, "llama", block_size=128, use_ssr=True)
+            timings = []
+            runs[key] = q.quantize(samples, writeback="reference", timings=timings, **kw)
+            assert len(timings) == 2 and all(t["total_s"] > 0 for t in timings)
+    finally:
+        torch.set_num_threads(threads)
+    base = runs["model/gf"]
+    assert len(base) == 14
+    for key, got in runs.items():
+        assert sorted(got) == sorted(base), key
+        for name in base:
+            for k in ("alpha", "mu", "T", "perm"):
+                assert torch.equal(got[name][k], base[name][k]), (key, name, k)

@@ -10,7 +10,12 @@ TAG=${1:-atqk}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-cp $R/tools/_probe/libpt2q_dev.so $R/snlp---tenary-post-train-quantization_amd/libpt2q.so || exit 1
+# the DEV_PROBES library stands in for the package's release library for this script only: the
+# release copy is saved first and put back on exit, so later runs on the box load the release build
+PKG=$R/snlp---tenary-post-train-quantization_amd
+cp $PKG/libpt2q.so $OUT/libpt2q_release.so || exit 1
+trap 'cp $OUT/libpt2q_release.so $PKG/libpt2q.so' EXIT
+cp $R/tools/_probe/libpt2q_dev.so $PKG/libpt2q.so || exit 1
 cd /tmp && export TMPDIR=/tmp
 for M in ${@:-0 1 2 4 7}; do
   export PT2Q_ATQ_PROBE=$M

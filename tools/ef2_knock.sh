@@ -4,13 +4,19 @@
 # (1 = no Wt traffic, 2 = operand DMAs from one hot chunk, 4 = no MFMAs; results garbage), and
 # ef_gemm_kernel for reference.   bash tools/ef2_knock.sh TAG [mask ...]
 # masks: N (ef2 knock-out N), sN (ef2, stagger N), nV (PT2Q_EF_V2=V, no w-bar)
-# The knock-out masks need a development library: make -C <pkg> clean && make -C <pkg> DEV_PROBES=1
-# (the release build ignores PT2Q_EF2_PROBE).
+# The knock-out masks need the development library (bash tools/build_dev_lib.sh builds
+# tools/_probe/libpt2q_dev.so; the release build ignores every PT2Q_EF* variable).
 set -o pipefail
 TAG=${1:-ef2k}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
+# the DEV_PROBES library stands in for the package's release library for this script only: the
+# release copy is saved first and put back on exit, so later runs on the box load the release build
+PKG=$R/snlp---tenary-post-train-quantization_amd
+cp $PKG/libpt2q.so $OUT/libpt2q_release.so || exit 1
+trap 'cp $OUT/libpt2q_release.so $PKG/libpt2q.so' EXIT
+cp $R/tools/_probe/libpt2q_dev.so $PKG/libpt2q.so || exit 1
 cd /tmp && export TMPDIR=/tmp
 for M in v1 ${@:-0 1 2 4 3 7}; do
   # M: a knock-out mask, or sN = no knock-out with PT2Q_EF2_STAGGER=N
