@@ -249,7 +249,8 @@ def shard_runs(a, dev, io, world, ranks=None, t1_ms=None, t1_phase=None, steps=3
                "step_ms": {"min": min(step_ms), "median": float(np.median(step_ms)), "max": max(step_ms)},
                "phase_s": ph, "gather_send_bytes": w.gather_bytes,
                "predicted_cost_s": sum(sharding.unit_cost(u, a.block_size) for u in units),
-               "predicted_shard_s": sharding.shard_cost(units, a.block_size)}
+               "predicted_shard_s": sharding.shard_cost(units, a.block_size, IO_BYTES[a.io_dtype]),
+               "predicted_phase_s": sharding.shard_phases(units, a.block_size, IO_BYTES[a.io_dtype])}
         log(0, f"shard {r}/{world}: {len(units)} units, {rec['ms_per_step']:.1f} ms/step, phases "
                f"{ {k: round(v * 1e3, 1) for k, v in (ph or {}).items()} }")
         out.append(rec)
@@ -596,19 +597,28 @@ class ModelStep:
                                        inv_streams=a.inv_streams, chunk=parse_chunk(a.inv_chunk))
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
-        self.xi = {}  # unit -> which of its width's activation tensors it reads
+        self.xi = {}  # unit -> which of this rank's activation tensors of its width it reads
         self.index = {u[0]: i for i, u in enumerate(self.units)}
+        # unit i reads activation slot (its position among the model's units of its width) %
+        # X_DISTINCT, seeded by the slot alone: the same tensor on whichever rank runs the unit,
+        # so every shard of a sharded step quantises exactly the whole step's inputs
+        pos, slot = {}, {}
+        for j, (_, lins, _) in enumerate(self.units):
+            m = lins[0][2]
+            slot[j] = pos.get(m, 0) % X_DISTINCT
+            pos[m] = pos.get(m, 0) + 1
+        have = {}
         for i in self.mine:
             name, lins, N = self.units[i]
             m = lins[0][2]
             if m not in self.X:
                 self.X[m] = []
                 self.ws[m] = self.pipe.workspace(m) if self.pipe else pt2q.UnitWorkspace(m, dev, self.bs)
-            cnt = sum(1 for j in self.xi if self.units[j][1][0][2] == m)
-            if cnt < X_DISTINCT:
-                self.X[m].append(pt2q.fill_synthetic((N, m), 2000 + 97 * rank + m + 7919 * cnt, std=1.0,
+            if (m, slot[i]) not in have:
+                have[(m, slot[i])] = len(self.X[m])
+                self.X[m].append(pt2q.fill_synthetic((N, m), 2000 + m + 7919 * slot[i], std=1.0,
                                                      outliers=True, device=dev).to(io))
-            self.xi[i] = cnt % X_DISTINCT
+            self.xi[i] = have[(m, slot[i])]
             for k, (p, n, _) in enumerate(lins):
                 self.W[(i, p)] = pt2q.fill_synthetic((n, m), 100_000 + 16 * i + k, std=0.02,
                                                      device=dev).to(io)
@@ -1156,6 +1166,9 @@ def main(argv=None):
         # the LPT cost model's seconds for this shard (sharding.unit_cost), beside the measured ms,
         # so a first multi-GPU run shows a modelled-vs-measured imbalance at once
         me["predicted_cost_s"] = sum(sharding.unit_cost(work.units[i], a.block_size) for i in mine)
+        # the phase model of this rank's step (fixed latencies included, sharding.shard_phases)
+        me["predicted_shard_s"] = sharding.shard_cost([work.units[i] for i in mine], a.block_size,
+                                                      IO_BYTES[a.io_dtype])
         if world > 1:
             ranks = [None] * world
             dist.all_gather_object(ranks, me)
@@ -1167,9 +1180,12 @@ def main(argv=None):
     if ranks:
         pc = [r["predicted_cost_s"] for r in ranks]
         mc = [r["ms_per_step"] for r in ranks]
+        ps = [r["predicted_shard_s"] for r in ranks]
         balance = {"predicted_max_over_mean": max(pc) / (sum(pc) / len(pc)) if sum(pc) > 0 else None,
+                   "shard_model_max_over_mean": max(ps) / (sum(ps) / len(ps)) if sum(ps) > 0 else None,
                    "measured_max_over_mean": max(mc) / (sum(mc) / len(mc)) if sum(mc) > 0 else None,
-                   "model": "sharding.unit_cost (Gram N*m^2, inverse m^3, block loop n*r), LPT over the ranks"}
+                   "model": "sharding.unit_cost (per-unit shares of the fitted phase model), LPT over the ranks; "
+                            "sharding.shard_cost: the phase model of each rank's step"}
     log(rank, f"timed {a.steps} steps: {ms_per_step:.1f} ms/step")
     if a.dry_run:
         if rank == 0:

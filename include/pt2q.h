@@ -194,6 +194,25 @@ int pt2q_quantize_blocks_group(int count, const void* const* W, int wdtype, int6
                                int64_t* const* perm, int* const* iters_dev, void* workspace,
                                size_t workspace_bytes, void* stream);
 
+/* Per-channel block loops (b >= m > 512: one block of every column in ascending order,
+ * main.py:158-230 with block_size >= in_features; BASELINE config 5) of `count` (1..16) linears
+ * of one width m and W dtype in ONE launch sequence -- their row counts n[z] may differ (the
+ * q/k/v/o and gate/up projections of a Llama layer share m).  A 5120-row linear alone fills 1.25
+ * waves per SIMD; the group's rows share one grid.  Linear z: row-major W[z] (n[z] x m, leading
+ * dim ldw), S1d[z] = S1 (m floats) then d -- a row of pt2q_s1_from_gram_batched (variant M, the
+ * raw Gram's S·1 and 1ᵀS1, quantizer.py:215-218; a NULL array or entry = no AGA) -- outputs
+ * alpha[z], mu[z] (n[z] fp32), T[z] (n[z] x m, tdtype, leading dim m), perm[z] (m int64: [0, m))
+ * and iters_dev[z] (1 int; nullable array / entries), each exactly pt2q_quantize_blocks(W[z], ...,
+ * b = m, PT2Q_FLAG_S1_GIVEN | PT2Q_AGA_ACT) -- bit for bit.  Pointer arrays are HOST arrays of
+ * device pointers, read during the call only.  Replaces main.py:289-299's per-linear calls for a
+ * list of per-channel linears.  workspace: pt2q_quantize_perchannel_group_workspace_bytes(count). */
+size_t pt2q_quantize_perchannel_group_workspace_bytes(int count);
+int pt2q_quantize_perchannel_group(int count, const void* const* W, int wdtype, int64_t ldw, const int* n,
+                                   int m, const float* const* S1d, int max_iter, float* const* alpha,
+                                   float* const* mu, void* const* T, int tdtype, int64_t* const* perm,
+                                   int* const* iters_dev, void* workspace, size_t workspace_bytes,
+                                   void* stream);
+
 /* Whole layer, variant M (main.py:102-230): gram -> prepare -> cholesky_inverse -> blocks.
  * If info_dev reports a breakdown the outputs are undefined; the caller recomputes Hinv with
  * pinv and calls pt2q_quantize_blocks (the staged path). */

@@ -66,6 +66,8 @@ _SIGS = {
     "pt2q_quantize_blocks_group_workspace_bytes": (SZ, [I, I, I, I, I]),
     "pt2q_quantize_blocks_group": (I, [I, P, I, I64, I, I, I, I, P, I64, P, I64, I, P, P, P, I, P, P, P,
                                        SZ, P]),
+    "pt2q_quantize_perchannel_group_workspace_bytes": (SZ, [I]),
+    "pt2q_quantize_perchannel_group": (I, [I, P, I, I64, P, I, P, I, P, P, P, I, P, P, P, SZ, P]),
     "pt2q_quantize_layer": (I, [P, I, I64, I, I, P, I, I64, I64, I, I, F, I, P, P, P, I, P, P, P,
                                 P, SZ, P]),
     "pt2q_atq_stage": (I, [I, P, I64, I, I, P, P, P, I64, P, P, I, P, P, SZ, P]),

@@ -55,13 +55,19 @@ def get_llm_layers(model: nn.Module, model_type: str = "llama"):
 class GramAccumulator:
     """An m x m fp32 Gram fed batch by batch; bit-identical to XᵀX of the concatenated rows.
 
-    The 16-bit MFMA Gram advances each fp32 chain in groups of 8 rows, so a batch may only be
-    continued from a row count that is a multiple of 8: the (< 8) remainder rows of a 16-bit
-    batch are held back and lead the next batch's first group (flushed when `G` is read).
-    Stall reports of the streamed Gram launches are OR-ed into a device word and checked once,
-    when `G` is read."""
+    Batches are copied into a staging buffer of `buffer_rows` rows (a multiple of 8, capped at
+    ~512 MiB) and the Gram runs once per full buffer, chain-continuing (pt2q_gram accumulate=2):
+    one calibration sample's 2048 rows make a Gram launch too short to fill the chip (0.55 PF/s on
+    a Llama-2-7B layer's captures, against 1.2 PF/s for the long chains).  The 16-bit MFMA Gram
+    advances each fp32 chain in groups of 8 rows, so a chain may only be continued from a row
+    count that is a multiple of 8: every full buffer is, and only the last (flushed) launch may be
+    ragged.  Stall reports of the Gram launches are OR-ed into a device word and checked once,
+    when `G` is read.  buffer_rows=0: a Gram launch per batch (the remainder rows of a 16-bit batch
+    held back to lead the next one)."""
 
-    def __init__(self, m: int, device):
+    MAX_BUFFER_BYTES = 512 << 20
+
+    def __init__(self, m: int, device, buffer_rows: int = 32768):
         self.m = m
         self.device = torch.device(device)
         self._G = torch.zeros((m, m), dtype=torch.float32, device=self.device)
@@ -70,6 +76,9 @@ class GramAccumulator:
         self._pend: Optional[torch.Tensor] = None
         self._ws = _lib.workspace(_lib.lib().pt2q_gram_workspace_bytes(m), self.device)
         self._stall = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._cap = max(0, int(buffer_rows)) // 8 * 8
+        self._buf: Optional[torch.Tensor] = None
+        self._fill = 0
 
     def _run(self, X: torch.Tensor):
         mode = "continue" if self._rows_in_G else False
@@ -78,9 +87,28 @@ class GramAccumulator:
         self._rows_in_G += X.shape[0]
 
     def _flush(self):
+        if self._buf is not None and self._fill:
+            fill, self._fill = self._fill, 0
+            self._run(self._buf[:fill])
         if self._pend is not None:
             pend, self._pend = self._pend, None
             self._run(pend)
+
+    def _buffered(self, X: torch.Tensor):
+        if self._buf is None or self._buf.dtype != X.dtype:
+            self._flush()
+            cap = min(self._cap, max(8, self.MAX_BUFFER_BYTES // (self.m * X.element_size()) // 8 * 8))
+            self._buf = torch.empty((cap, self.m), dtype=X.dtype, device=self.device)
+        cap = self._buf.shape[0]
+        o = 0
+        while o < X.shape[0]:
+            k = min(cap - self._fill, X.shape[0] - o)
+            self._buf[self._fill:self._fill + k].copy_(X[o:o + k])
+            self._fill += k
+            o += k
+            if self._fill == cap:  # a full buffer: a multiple of 8 rows, so the chain may continue
+                self._fill = 0
+                self._run(self._buf)
 
     def add(self, X: torch.Tensor):
         X = X.reshape(-1, X.shape[-1])
@@ -90,6 +118,9 @@ class GramAccumulator:
         if X.shape[0] == 0:
             return
         self.nsamples += X.shape[0]
+        if self._cap:
+            self._buffered(X)
+            return
         if X.dtype not in (torch.float16, torch.bfloat16):
             self._flush()  # f32 chains advance row by row: any split is exact
             self._run(X)
@@ -125,9 +156,10 @@ class GramCapture:
     Gram.  Linears whose input is the very same tensor in a forward pass share one accumulator
     (grouping is fixed at the first pass and checked afterwards)."""
 
-    def __init__(self, linears: Dict[str, nn.Linear], device=None):
+    def __init__(self, linears: Dict[str, nn.Linear], device=None, buffer_rows: int = 32768):
         self.linears = linears
         self.device = device
+        self.buffer_rows = buffer_rows  # GramAccumulator staging (0: a Gram launch per batch)
         self.group_of: Dict[str, int] = {}
         self.accs: List[GramAccumulator] = []
         self.members: List[List[str]] = []
@@ -155,7 +187,7 @@ class GramCapture:
                         break
                 if gid is None:
                     dev = self.device if self.device is not None else x.device
-                    self.accs.append(GramAccumulator(x.shape[-1], dev))
+                    self.accs.append(GramAccumulator(x.shape[-1], dev, self.buffer_rows))
                     self.members.append([])
                     gid = len(self.accs) - 1
                 self.group_of[name] = gid

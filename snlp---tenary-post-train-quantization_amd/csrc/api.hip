@@ -254,6 +254,20 @@ __global__ void pc_setup_kernel(int64_t* perm, int m, int* counters, int* iters)
   if (i == 0) *iters = 0;
 }
 
+// the grouped per-channel setup (pc_setup_kernel per linear z = blockIdx.y)
+struct PcSetupGroup {
+  int64_t* perm[PT2Q_PC_GROUP_MAX];
+  int* counters[PT2Q_PC_GROUP_MAX];
+  int* iters[PT2Q_PC_GROUP_MAX];
+};
+__global__ void pc_setup_group_kernel(PcSetupGroup g, int m) {
+  const int z = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) g.perm[z][i] = i;
+  if (i < 2) g.counters[z][i] = 0;
+  if (i == 0) *g.iters[z] = 0;
+}
+
 __global__ void i64_to_i32_kernel(const int64_t* a, int n, int* b) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) b[i] = (int)a[i];
@@ -694,6 +708,49 @@ extern "C" int pt2q_quantize_blocks(const void* W, int wdtype, int64_t ldw, int 
   if (!carve_blocks(c, n, m, b, w, flags)) return PT2Q_E_WORKSPACE;
   return run_blocks(W, wdtype, ldw, n, m, b, flags, A, lda, Hinv, ldhi, max_iter, alpha, mu, T,
                     tdtype, perm, iters_dev, w, (hipStream_t)stream);
+}
+
+extern "C" size_t pt2q_quantize_perchannel_group_workspace_bytes(int count) {
+  if (count <= 0) return 0;
+  return PT2Q_STATUS_BYTES + (((size_t)count * 3 * sizeof(int) + 255) & ~(size_t)255);
+}
+
+extern "C" int pt2q_quantize_perchannel_group(int count, const void* const* W, int wdtype, int64_t ldw,
+                                              const int* n, int m, const float* const* S1d, int max_iter,
+                                              float* const* alpha, float* const* mu, void* const* T, int tdtype,
+                                              int64_t* const* perm, int* const* iters_dev, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (count <= 0 || count > PT2Q_PC_GROUP_MAX || !W || !n || !alpha || !mu || !T || !perm || m <= 512 ||
+      !dtype_ok(wdtype) || (tdtype != PT2Q_I8 && tdtype != PT2Q_F32) || max_iter < 0 || ldw < m)
+    return PT2Q_E_ARG;
+  for (int z = 0; z < count; ++z)
+    if (!W[z] || n[z] <= 0 || !alpha[z] || !mu[z] || !T[z] || !perm[z]) return PT2Q_E_ARG;
+  Carve c{(char*)workspace, workspace_bytes};
+  int rc;
+  int* status = take_status(c, st, rc);
+  (void)status;  // no cross-workgroup waits here: the word stays 0
+  if (rc != PT2Q_OK) return rc;
+  int* ints = c.take<int>((size_t)count * 3);
+  if (!c.ok) return PT2Q_E_WORKSPACE;
+  PcLinear lin[PT2Q_PC_GROUP_MAX];
+  PcSetupGroup sg{};
+  for (int z = 0; z < count; ++z) {
+    const float* s1 = S1d ? S1d[z] : nullptr;
+    int* it = (iters_dev && iters_dev[z]) ? iters_dev[z] : ints + 2 * count + z;
+    lin[z] = PcLinear{W[z], (long)ldw, n[z], s1, s1 ? s1 + m : nullptr, alpha[z], mu[z], T[z], (long)m, it,
+                      ints + 2 * z, perm[z]};
+    sg.perm[z] = perm[z];
+    sg.counters[z] = ints + 2 * z;
+    sg.iters[z] = it;
+  }
+  {
+    StageScope ts(PT2Q_TIMER_SETUP, st);
+    hipLaunchKernelGGL(pc_setup_group_kernel, dim3(ceil_div(m, 256), count), dim3(256), 0, st, sg, m);
+    PT2Q_LAUNCH_CHECK();
+  }
+  StageScope ts_atq(PT2Q_TIMER_ATQ, st);
+  return pt2q_launch_atq_rm_group(count, lin, wdtype, m, max_iter, tdtype, st);
 }
 
 extern "C" size_t pt2q_quantize_blocks_group_workspace_bytes(int count, int n, int m, int b, int flags) {

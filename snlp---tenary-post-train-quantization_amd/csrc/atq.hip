@@ -11,6 +11,7 @@
 // grid+round, so continuing them reproduces the block loop exactly; the one block-level case
 // that differs (every row's T_init == 0 -> the block loop returns the init grid untouched) is
 // detected with a per-block counter and repaired by the last workgroup to finish.
+#include <algorithm>
 #include <type_traits>
 
 #include "common.hpp"
@@ -1107,6 +1108,20 @@ __global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_zero_fixup_kerne
   wide_block_rows<L>(A, true, false);
 }
 
+// the repair of a grouped per-channel launch: linear blockIdx.y (its rows past blockIdx.x's skip)
+struct WideGroup {
+  int count;
+  WideArgs a[PT2Q_PC_GROUP_MAX];
+};
+template <class L>
+__global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_zero_fixup_group_kernel(WideGroup G) {
+  const WideArgs& A = G.a[blockIdx.y];
+  if (A.counters[0] != A.n) return;
+  if ((int)blockIdx.x * (int)(blockDim.x >> 6) * 4 >= A.n) return;
+  if (A.iters && blockIdx.x == 0 && threadIdx.x == 0) *A.iters = 0;
+  wide_block_rows<L>(A, true, false);
+}
+
 // Per-method stages on row-major W / float T (quantizer.py surface) for b > 512.
 __global__ __launch_bounds__(64 * WIDE_WAVES_MAX) void atq_wide_stage_kernel(WideArgs A) {
   const WideRow<LayStage> R = wide_row<LayStage>(A);
@@ -1246,6 +1261,52 @@ int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, c
       PT2Q_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(atq_wide_zero_fixup_kernel<L>, dim3(wgrid), dim3(64 * wide_waves()), 0, st, WA);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  };
+  const bool i8 = tdtype == PT2Q_I8;
+  switch (wdtype) {
+    case PT2Q_F32: return i8 ? go(LayRM<float, int8_t>{}) : go(LayRM<float, float>{});
+    case PT2Q_F16: return i8 ? go(LayRM<_Float16, int8_t>{}) : go(LayRM<_Float16, float>{});
+    case PT2Q_BF16: return i8 ? go(LayRM<uint16_t, int8_t>{}) : go(LayRM<uint16_t, float>{});
+  }
+  return PT2Q_E_ARG;
+}
+
+// Grouped per-channel blocks (pt2q_quantize_perchannel_group): the rows of every linear in one
+// atq_pc launch when the streamed / register kernels take them all (else each linear on the wide
+// kernel), then one repair launch for the group (grid.y = linear).  The same per-row programs as
+// pt2q_launch_atq_wide_rm: the same bits.
+int pt2q_launch_atq_rm_group(int count, const PcLinear* lin, int wdtype, int m, int max_iter, int tdtype,
+                             hipStream_t st) {
+  if (count <= 0 || count > PT2Q_PC_GROUP_MAX) return PT2Q_E_ARG;
+  bool pc = true;
+  int nmax = 0;
+  for (int z = 0; z < count; ++z) {
+    pc = pc && pt2q_atq_pc_supported(lin[z].W, wdtype, lin[z].ldw, m);
+    nmax = std::max(nmax, lin[z].n);
+  }
+  WideGroup G{};
+  G.count = count;
+  for (int z = 0; z < count; ++z) {
+    const PcLinear& L = lin[z];
+    G.a[z] = WideArgs{MODE_BLOCK, (const float*)L.W, L.ldw, L.n, m, nullptr, L.S1, L.d, max_iter, L.alpha, L.mu,
+                      L.T, L.ldt, nullptr, 0, L.iters, L.counters, 0};
+  }
+  const int wgrid = ceil_div(nmax, 4 * wide_waves());
+  auto go = [&](auto lay) {
+    typedef decltype(lay) L;
+    if (pc) {
+      const int rc = pt2q_launch_atq_pc_group(count, lin, wdtype, m, max_iter, tdtype, st);
+      if (rc != PT2Q_OK) return rc;
+    } else {
+      for (int z = 0; z < count; ++z) {
+        hipLaunchKernelGGL(atq_wide_block_kernel<L>, dim3(ceil_div(lin[z].n, 4 * wide_waves())),
+                           dim3(64 * wide_waves()), 0, st, G.a[z]);
+        PT2Q_LAUNCH_CHECK();
+      }
+    }
+    hipLaunchKernelGGL(atq_wide_zero_fixup_group_kernel<L>, dim3(wgrid, count), dim3(64 * wide_waves()), 0, st, G);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };

@@ -409,43 +409,74 @@ PT2Q_DEV void pc_rows(R& rows) {
 // counter, so a wave takes the next group when its ITF ends, measured slower: the loop around the
 // unrolled register-resident body raised its spills 47 -> 246 VGPRs, 230 -> 264 us per 5120-column
 // linear; the streamed kernel 498 -> 517 us per 5120 x 13824.)
+//
+// Grouped launches (PcGroup): the rows of up to PC_GROUP_MAX linears of one width in ONE 1-D grid,
+// linear z taking workgroups [wg0[z], wg0[z + 1]) -- a single 5120-row linear fills only 1.25
+// waves per SIMD, so launched alone its last wave leaves most of the chip idle; a group of 16
+// keeps every SIMD at the kernel's occupancy until the grid drains.  Per row, the program and its
+// arithmetic are unchanged (the same bits).
+struct PcGroup {
+  int count;
+  int wg0[PT2Q_PC_GROUP_MAX + 1];
+  PcArgs a[PT2Q_PC_GROUP_MAX];
+};
+
+// This workgroup's linear (its args, selected with constant indices so they stay in scalar
+// registers: a dynamically indexed kernarg array is copied to scratch) and its workgroup index.
+PT2Q_DEV PcArgs pc_linear(const PcGroup& G, int& wg) {
+  const int b = (int)blockIdx.x;
+  PcArgs A = G.a[0];
+  wg = b;
+#pragma unroll
+  for (int k = 1; k < PT2Q_PC_GROUP_MAX; ++k)
+    if (k < G.count && b >= G.wg0[k]) {
+      A = G.a[k];
+      wg = b - G.wg0[k];
+    }
+  return A;
+}
+
 template <class TI, class TO>
-__global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcArgs A) {
+__global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcGroup G) {
   extern __shared__ __attribute__((aligned(16))) char pc_lds[];
-  typedef PcGeom<TI> G;
+  typedef PcGeom<TI> G_;
+  int wg;
+  const PcArgs A = pc_linear(G, wg);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nc = (A.m + PC_COLS - 1) / PC_COLS;
   PcRows<TI> R{A, lane, lane & 15, lane >> 4, 0, false, nc, {}, nullptr, nullptr};
-  const int row0 = ((int)blockIdx.x * PC_WAVES + wave) * 4;
+  const int row0 = (wg * PC_WAVES + wave) * 4;
   R.i = row0 + R.r;
   R.valid = R.i < A.n;
   if (!R.valid) R.i = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int iq = row0 + q < A.n ? row0 + q : 0;
-    R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G::E;
+    R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G_::E;
   }
-  R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G::STAGE, nc);
-  R.masks = R.ring + 2 * G::STAGE;
+  R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G_::STAGE, nc);
+  R.masks = R.ring + 2 * G_::STAGE;
   R.prime();
   pc_rows<TO>(R);
 }
 
 constexpr int PCR_WAVES = 4;
 template <class TI, class TO, int NW>
-__global__ __launch_bounds__(64 * PCR_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void atq_pcr_kernel(PcArgs A) {
-  typedef PcGeom<TI> G;
-  __shared__ __attribute__((aligned(16))) char ring_lds[PCR_WAVES * 2 * G::STAGE];
+__global__ __launch_bounds__(64 * PCR_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void atq_pcr_kernel(PcGroup G) {
+  typedef PcGeom<TI> G_;
+  __shared__ __attribute__((aligned(16))) char ring_lds[PCR_WAVES * 2 * G_::STAGE];
+  int wg;
+  const PcArgs A = pc_linear(G, wg);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   PcRegs<TI, NW> R{A, lane, lane & 15, lane >> 4, 0, false, {}, {}};
-  const int row0 = ((int)blockIdx.x * PCR_WAVES + wave) * 4;
+  const int row0 = (wg * PCR_WAVES + wave) * 4;
   R.i = row0 + R.r;
   R.valid = R.i < A.n;
   if (!R.valid) R.i = 0;
   const char* rowp[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) rowp[q] = (const char*)A.W + (long)(row0 + q < A.n ? row0 + q : 0) * A.ldw * 2;
-  R.load(rowp, (lds_char*)ring_lds + wave * 2 * G::STAGE);
+  R.load(rowp, (lds_char*)ring_lds + wave * 2 * G_::STAGE);
   pc_rows<TO>(R);
 }
 
@@ -462,34 +493,53 @@ bool pt2q_atq_pc_supported(const void* W, int wdtype, long ldw, int m) {
   return PC_WAVES * pc_wave_bytes(stage, ceil_div(m, PC_COLS)) <= 160 * 1024;
 }
 
-int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const float* S1, const float* d,
-                       int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
-                       int* counters, hipStream_t st) {
-  PcArgs A{W, ldw, n, m, S1, d, max_iter, alpha, mu, T, ldt, iters, counters};
-  if (m == PC_COLS * PCR_NW && wdtype == PT2Q_BF16 && pt2q_tuning().atq_pc_regs) {
+// Up to PT2Q_PC_GROUP_MAX linears of width m (every W accepted by pt2q_atq_pc_supported) in one
+// launch; their row counts may differ.
+int pt2q_launch_atq_pc_group(int count, const PcLinear* lin, int wdtype, int m, int max_iter, int tdtype,
+                             hipStream_t st) {
+  if (count <= 0 || count > PT2Q_PC_GROUP_MAX) return PT2Q_E_ARG;
+  const bool regs = m == PC_COLS * PCR_NW && wdtype == PT2Q_BF16 && pt2q_tuning().atq_pc_regs;
+  const int rows_wg = 4 * (regs ? PCR_WAVES : PC_WAVES);
+  PcGroup G{};
+  G.count = count;
+  int wg = 0;
+  for (int z = 0; z < count; ++z) {
+    const PcLinear& L = lin[z];
+    G.a[z] = PcArgs{L.W, L.ldw, L.n, m, L.S1, L.d, max_iter, L.alpha, L.mu, L.T, L.ldt, L.iters, L.counters};
+    G.wg0[z] = wg;
+    wg += ceil_div(L.n, rows_wg);
+  }
+  G.wg0[count] = wg;
+  if (wg == 0) return PT2Q_OK;
+  const bool i8 = tdtype == PT2Q_I8;
+  if (regs) {
     auto gor = [&](auto ti, auto to) {
-      hipLaunchKernelGGL((atq_pcr_kernel<decltype(ti), decltype(to), PCR_NW>), dim3(ceil_div(n, 4 * PCR_WAVES)),
-                         dim3(64 * PCR_WAVES), 0, st, A);
+      hipLaunchKernelGGL((atq_pcr_kernel<decltype(ti), decltype(to), PCR_NW>), dim3(wg), dim3(64 * PCR_WAVES), 0,
+                         st, G);
       PT2Q_LAUNCH_CHECK();
       return PT2Q_OK;
     };
-    const bool i8 = tdtype == PT2Q_I8;
     return i8 ? gor(uint16_t{}, int8_t{}) : gor(uint16_t{}, float{});
   }
-  const int grid = ceil_div(n, 4 * PC_WAVES);
   auto go = [&](auto ti, auto to) {
     typedef decltype(ti) TI;
     typedef decltype(to) TO;
     const size_t lds = PC_WAVES * pc_wave_bytes(PcGeom<TI>::STAGE, ceil_div(m, PC_COLS));
-    hipLaunchKernelGGL((atq_pc_kernel<TI, TO>), dim3(grid), dim3(64 * PC_WAVES), lds, st, A);
+    hipLaunchKernelGGL((atq_pc_kernel<TI, TO>), dim3(wg), dim3(64 * PC_WAVES), lds, st, G);
     PT2Q_LAUNCH_CHECK();
     return PT2Q_OK;
   };
-  const bool i8 = tdtype == PT2Q_I8;
   switch (wdtype) {
     case PT2Q_F32: return i8 ? go(float{}, int8_t{}) : go(float{}, float{});
     case PT2Q_F16: return i8 ? go(_Float16{}, int8_t{}) : go(_Float16{}, float{});
     case PT2Q_BF16: return i8 ? go(uint16_t{}, int8_t{}) : go(uint16_t{}, float{});
   }
   return PT2Q_E_ARG;
+}
+
+int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const float* S1, const float* d,
+                       int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
+                       int* counters, hipStream_t st) {
+  const PcLinear L{W, ldw, n, S1, d, alpha, mu, T, ldt, iters, counters, nullptr};
+  return pt2q_launch_atq_pc_group(1, &L, wdtype, m, max_iter, tdtype, st);
 }

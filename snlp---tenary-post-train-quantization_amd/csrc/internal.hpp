@@ -35,6 +35,28 @@ int pt2q_launch_atq_pc(const void* W, int wdtype, long ldw, int n, int m, const 
 int pt2q_launch_atq_wide_rm(const void* W, int wdtype, long ldw, int n, int b, const float* S1, const float* d,
                             int max_iter, float* alpha, float* mu, void* T, int tdtype, long ldt, int* iters,
                             int* counters, hipStream_t st);
+// grouped per-channel rows: up to PT2Q_PC_GROUP_MAX linears of one width m and W dtype (row counts
+// may differ) in one launch sequence; S1 / d per linear (nullable S1: no AGA); counters (2 ints,
+// zeroed) and *iters (zeroed) per linear
+constexpr int PT2Q_PC_GROUP_MAX = 16;
+struct PcLinear {
+  const void* W;
+  long ldw;
+  int n;
+  const float* S1;
+  const float* d;
+  float* alpha;
+  float* mu;
+  void* T;
+  long ldt;
+  int* iters;
+  int* counters;
+  int64_t* perm;  // the setup's [0, m) (pt2q_quantize_perchannel_group), unused by the kernels
+};
+int pt2q_launch_atq_pc_group(int count, const PcLinear* lin, int wdtype, int m, int max_iter, int tdtype,
+                             hipStream_t st);
+int pt2q_launch_atq_rm_group(int count, const PcLinear* lin, int wdtype, int m, int max_iter, int tdtype,
+                             hipStream_t st);
 int pt2q_launch_atq_block(const float* Wt, long ldw, int n, const int* blk, int b,
                           const float* S1, const float* d, int max_iter, float* alpha, float* mu,
                           int8_t* Tt, long ldt, float* Et, long lde, int* iters, int* counters,

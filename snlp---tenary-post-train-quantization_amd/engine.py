@@ -265,6 +265,59 @@ def quantize_blocks_group(Ws, As, Hinvs, block_size: int = 128, use_ssr: bool = 
     return outs
 
 
+PC_GROUP_MAX = 16  # linears per pt2q_quantize_perchannel_group call (PT2Q_PC_GROUP_MAX)
+
+
+def perchannel_group_supported(m: int) -> bool:
+    """Per-channel linears (one block, block_size >= m) the grouped entry takes: m > 512."""
+    return m > 512
+
+
+def quantize_perchannel_group(Ws, s1ds=None, max_iter: int = 100, t_dtype=torch.int8,
+                              workspace: Optional[torch.Tensor] = None, outs=None, check: bool = True):
+    """Per-channel block loops (block_size >= m: one block of every column; main.py:158-230,
+    BASELINE C5) of up to PC_GROUP_MAX linears of one width m and dtype in ONE launch sequence
+    (pt2q_quantize_perchannel_group): their rows share one grid, so a 5120-row linear no longer
+    ends its launch in a partial wave.  Ws[z] (n_z x m; row counts may differ), s1ds[z] = S1 then
+    d of its raw Gram (s1_from_gram_batched's row, m + 1 fp32; None = no AGA).  Each result is
+    bit-identical to quantize_blocks(Ws[z], G, None, block_size=m, s1d=s1ds[z])."""
+    Ws = [_float_input(W) for W in Ws]
+    count = len(Ws)
+    if not 1 <= count <= PC_GROUP_MAX:
+        raise ValueError(f"quantize_perchannel_group: 1..{PC_GROUP_MAX} linears (got {count})")
+    m, dev, dt = Ws[0].shape[1], Ws[0].device, Ws[0].dtype
+    if not perchannel_group_supported(m) or any(W.shape[1] != m or W.dtype != dt or W.device != dev for W in Ws):
+        raise ValueError("quantize_perchannel_group: linears of one width m > 512, one dtype and device")
+    if s1ds is not None:
+        if len(s1ds) != count:
+            raise ValueError("quantize_perchannel_group: one s1d per linear")
+        for t in s1ds:
+            if t is not None and (t.numel() != m + 1 or t.dtype != torch.float32 or not t.is_contiguous()
+                                  or t.device != dev):
+                raise ValueError("quantize_perchannel_group: s1d must be m + 1 contiguous fp32 on W's device")
+    if outs is None:
+        outs = [LayerOutput(torch.empty((W.shape[0], 1), dtype=torch.float32, device=dev),
+                            torch.empty((W.shape[0], 1), dtype=torch.float32, device=dev),
+                            torch.empty((W.shape[0], m), dtype=t_dtype, device=dev),
+                            torch.empty(m, dtype=torch.int64, device=dev),
+                            torch.zeros(1, dtype=torch.int32, device=dev)) for W in Ws]
+    nbytes = _lib.lib().pt2q_quantize_perchannel_group_workspace_bytes(count)
+    ws = workspace if workspace is not None and workspace.numel() >= nbytes else _lib.workspace(nbytes, dev)
+    import ctypes
+    ns = (ctypes.c_int * count)(*[W.shape[0] for W in Ws])
+    arrs = [_lib.ptr_array(x) for x in (Ws, [None] * count if s1ds is None else s1ds, [o.alpha for o in outs],
+                                        [o.mu for o in outs], [o.T for o in outs], [o.perm for o in outs],
+                                        [o.iters for o in outs])]
+    p = [a[0] for a in arrs]
+    rc = _lib.lib().pt2q_quantize_perchannel_group(
+        count, p[0], _lib.dtype_code(Ws[0]), m, ctypes.cast(ns, ctypes.c_void_p), m, p[1], int(max_iter),
+        p[2], p[3], p[4], _lib.dtype_code(outs[0].T), p[5], p[6], _lib.ptr(ws), ws.numel(), _lib.stream_of(dev))
+    _lib.check(rc, "pt2q_quantize_perchannel_group")
+    if check:
+        _lib.check_status(ws, "pt2q_quantize_perchannel_group")
+    return outs
+
+
 def hessian_inverse(G: torch.Tensor, nsamples: int, percdamp: float = 0.01):
     """main.py:129-141 on a raw Gram: damped H, then Hinv (pinv on Cholesky breakdown).
     Returns (Hinv, spd)."""

@@ -91,90 +91,120 @@ def model_units(model: str, layers: Optional[int] = None, tokens: Optional[int] 
     return c["units"](c["layers"] if layers is None else layers, c["tokens"] if tokens is None else tokens)
 
 
-# Measured single-MI355X rates behind unit_cost (profiles/r02f_summary.md): the
-# 16-bit Gram moves ~1.05e15 N·m² per second; the Cholesky inverse costs m³ at ~1e14/s plus a
-# ~25 µs critical-path step per 64 columns; a block of the block loop costs ~30 µs of launch
-# latency plus n·r·7.5e-12 s (error-feedback MFMA + SSR passes over the r remaining columns).
-_GRAM_RATE, _CHOL_RATE, _CHOL_STEP = 1.05e15, 1.0e14, 25e-6
-_BLOCK_FIXED, _BLOCK_NR = 30e-6, 7.5e-12
+# ----------------------------------------------------------------- cost model
+# One rank's grams-first step (GramsFirst: every Gram, then the batched inverses -- or, for
+# per-channel units, S1 / d -- then the grouped block loops on the lanes), phase by phase, with the
+# fixed latencies that do NOT shrink with a shard written out.  Constants fitted (round 6) to the
+# phase walls of the whole 7B / 13B steps and of their 8-rank shards timed alone on one MI355X
+# (bench.py --gpus 8 --shard all; profiles/r06a_shards_c4.json, r06a_shards_c5.json): the model
+# reproduces all four within 3 % (C4 2236 vs 2232 ms, its shards 302 vs 298-306 ms; C5 112 vs 112
+# ms, its shards 15.9 vs 15.3-15.8 ms).
+#   Gram: the batched 16-bit Gram runs 256 x 256 tiles in waves of one tile per CU; a wave costs
+#     N * 2 * 256^2 / GRAM_TILE_RATE (a CU's MFMA rate under the power limit) + GRAM_TILE_FIXED
+#     (the tile's ramp and its 512 KiB mirrored epilogue: 54 us, which dominates at N = 4096).
+#   Inverse: per chunk of <= 32 items, m / 64 serial panel steps of INV_STEP each, plus the
+#     trailing updates at INV_RATE m^3 per second.
+#   S1 / d (per-channel units): S1_FIXED + the Grams' bytes at S1_BW.
+#   Tails: the block loops' work LOOP_NR per n * r (error feedback + SSR passes over the remaining
+#     columns) plus LOOP_BLOCK per block of each group (its launch chain), the latter spread over
+#     the lanes; per-channel groups LOOP_PC per element plus LOOP_PC_GROUP per group (its last,
+#     slowest wave).
+SHARD_MODEL = dict(
+    cus=256,
+    gram_tile_rate=4.887e12, gram_tile_fixed=5.43e-5, gram_batch=128,
+    inv_step=4.53e-5, inv_rate=1.134e14, chunk=32,
+    s1_fixed=5.9e-4, s1_bw=4.47e12,
+    loop_nr=4.056e-12, loop_block=8.53e-5, loop_pc=3.28e-12, loop_pc_group=9.0e-4,
+    lanes=3, group=16, pc_group=16,
+)
+
+
+def _rsum(m: int, block_size: int) -> int:
+    nblk = -(-m // block_size) if block_size < m else 1
+    return sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))
 
 
 def block_loop_cost(n: int, m: int, block_size: int = 128) -> float:
-    """Modelled seconds of one n x m linear's block loop (see unit_cost)."""
-    nblk = -(-m // block_size) if block_size < m else 1
-    rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))  # remaining columns per block
-    return nblk * _BLOCK_FIXED + float(n) * rsum * _BLOCK_NR
+    """Modelled busy seconds of one n x m linear's block loop inside a full group (SHARD_MODEL)."""
+    c = SHARD_MODEL
+    if block_size >= m:
+        return float(n) * m * c["loop_pc"] + c["loop_pc_group"] / (c["pc_group"] * c["lanes"])
+    nblk = -(-m // block_size)
+    return float(n) * _rsum(m, block_size) * c["loop_nr"] + nblk * c["loop_block"] / (c["group"] * c["lanes"])
+
+
+def _gram_tiles(m: int) -> int:
+    t = -(-m // 256)
+    return t * (t + 1) // 2
 
 
 def unit_cost(unit, block_size: int = 128) -> float:
-    """Modelled seconds of one work unit on one MI355X (its Gram, Cholesky inverse and every
-    linear's block loop).  LPT balances ranks on this; a pure flop count (N·m² dominates) would
+    """Modelled seconds of one work unit (its Gram, Cholesky inverse or S1 / d, and every
+    linear's block loop) as its share of a full step (SHARD_MODEL, per-item shares of the
+    per-launch latencies).  LPT balances ranks on this; a pure flop count (N·m² dominates) would
     put a q/k/v unit level with an o unit although its three block loops make it ~1.6x longer."""
+    c = SHARD_MODEL
     _, linears, N = unit
     m = linears[0][2]
-    t = float(N) * m * m / _GRAM_RATE + float(m) ** 3 / _CHOL_RATE + (m / 64.0) * _CHOL_STEP
+    t = _gram_tiles(m) * (float(N) * 2 * 256 * 256 / c["gram_tile_rate"] + c["gram_tile_fixed"]) / c["cus"]
+    if block_size < m:
+        t += float(m) ** 3 / c["inv_rate"] + (m / 64.0) * c["inv_step"] / c["chunk"]
+    else:
+        t += float(m) * m * 4 / c["s1_bw"]
     for _, n, _ in linears:
         t += block_loop_cost(n, m, block_size)
     return t
 
 
-# Phase model of one rank's grams-first step (GramsFirst: every Gram, then the batched inverses,
-# then the grouped block loops on the lanes) -- what a rank's SHARD costs, as opposed to unit_cost's
-# additive per-unit seconds.  The fixed latencies that do not shrink with the shard are explicit:
-# the batched inverse's serial panel chain per chunk (each chunk of <= chunk items of one width
-# walks m / 64 dependent panel steps whatever its size) and the grouped loop's per-block launch
-# chain (every block of a group is a short sequence of dependent launches).  Constants: see
-# fit notes at SHARD_MODEL.
-SHARD_MODEL = dict(
-    gram_rate=1.19e15,      # N·m·(m+1) per second, the batched 16-bit Gram (work done)
-    gram_launch=4e-4,       # s per batched launch (ramp + last partial wave)
-    inv_rate=1.25e14,       # m³ per second, the trailing updates of the batched inverse (gemmx)
-    inv_step=1.7e-4,        # s per 64-column panel step of one chunk (the serial chain)
-    loop_nr=6.5e-12,        # s per n·r (error feedback + SSR passes over the remaining columns)
-    loop_block=4.5e-5,      # s per block of one grouped loop (its launch chain), any group size
-    loop_pc=4.0e-11,        # s per n·m of a per-channel linear (one block: ATQ passes)
-    lanes=3,                # tail lanes the groups spread over
-)
+def _groups(count: int, cap: int, lanes: int):
+    """GramsFirst.tails' group sizes for `count` same-class linears."""
+    size = max(1, min(cap, -(-count // lanes)))
+    return [min(size, count - g0) for g0 in range(0, count, size)]
 
 
-def shard_cost(units, block_size: int = 128, chunk: int = 32, group: int = 16, model=None) -> float:
-    """Modelled seconds of ONE rank's grams-first step over `units` (see SHARD_MODEL)."""
+def shard_phases(units, block_size: int = 128, io_bytes: int = 2, model=None):
+    """{gram, inverse, tails} modelled seconds of ONE rank's grams-first step over `units`."""
     c = dict(SHARD_MODEL, **(model or {}))
-    by_w = {}
-    lins = []
+    by_w, lins = {}, []
     for _, ls, N in units:
         m = ls[0][2]
-        by_w.setdefault((m, int(N)), []).append(len(ls))
+        by_w[(m, int(N))] = by_w.get((m, int(N)), 0) + 1
         lins += [(n, m) for _, n, _ in ls]
-    t_gram = sum(len(v) * float(N) * m * (m + 1) / c["gram_rate"] + c["gram_launch"] for (m, N), v in by_w.items())
-    t_inv = 0.0
-    for (m, N), v in by_w.items():
+    f32 = 16.0 if io_bytes == 4 else 1.0  # f32 MFMA: 1/16 of the 16-bit rate
+    gram = 0.0
+    for (m, N), cnt in by_w.items():
+        for z0 in range(0, cnt, c["gram_batch"]):
+            k = min(c["gram_batch"], cnt - z0)
+            waves = -(-k * _gram_tiles(m) // c["cus"])
+            gram += waves * (f32 * N * 2 * 256 * 256 / c["gram_tile_rate"] + c["gram_tile_fixed"])
+    inv, s1_bytes = 0.0, 0.0
+    for (m, N), cnt in by_w.items():
         if block_size >= m:
-            continue  # per-channel: no inverse
-        cnt = len(v)
-        t_inv += -(-cnt // chunk) * (m / 64.0) * c["inv_step"] + cnt * float(m) ** 3 / c["inv_rate"]
-    # tails: same-shape linears in groups of <= group (at least one group per lane), groups on
-    # the lanes longest first; a group's time is its per-block launch chain or its work, the
-    # larger, and the phase is the busiest lane or the chip's total work, the larger
+            s1_bytes += cnt * 4.0 * m * m
+            continue
+        inv += -(-cnt // c["chunk"]) * (m / 64.0) * c["inv_step"] + cnt * float(m) ** 3 / c["inv_rate"]
+    if s1_bytes:
+        inv += c["s1_fixed"] + s1_bytes / c["s1_bw"]
     shapes = {}
     for n, m in lins:
         shapes[(n, m)] = shapes.get((n, m), 0) + 1
-    groups, busy = [], 0.0
+    tails, pc_count = 0.0, {}
     for (n, m), cnt in shapes.items():
-        nblk = -(-m // block_size) if block_size < m else 1
-        rsum = sum(max(m - (k + 1) * block_size, 0) for k in range(nblk))
-        per = float(n) * rsum * c["loop_nr"] if nblk > 1 else float(n) * m * c["loop_pc"]
-        size = max(1, min(group, -(-cnt // c["lanes"])))
-        for g0 in range(0, cnt, size):
-            g = min(size, cnt - g0)
-            groups.append(max(nblk * c["loop_block"], g * per))
-            busy += g * per
-    load = [0.0] * c["lanes"]
-    for t in sorted(groups, reverse=True):
-        i = min(range(len(load)), key=lambda k: load[k])
-        load[i] += t
-    t_tail = max(max(load) if load else 0.0, busy)
-    return t_gram + t_inv + t_tail
+        if block_size >= m:
+            tails += cnt * float(n) * m * c["loop_pc"]
+            pc_count[m] = pc_count.get(m, 0) + cnt  # per-channel groups: by width, any row count
+            continue
+        nblk = -(-m // block_size)
+        tails += cnt * float(n) * _rsum(m, block_size) * c["loop_nr"]
+        tails += len(_groups(cnt, c["group"], c["lanes"])) * nblk * c["loop_block"] / c["lanes"]
+    for m, cnt in pc_count.items():
+        tails += len(_groups(cnt, c["pc_group"], c["lanes"])) * c["loop_pc_group"] / c["lanes"]
+    return {"gram": gram, "inverse": inv, "tails": tails}
+
+
+def shard_cost(units, block_size: int = 128, io_bytes: int = 2, model=None) -> float:
+    """Modelled seconds of ONE rank's grams-first step over `units` (shard_phases summed)."""
+    return sum(shard_phases(units, block_size, io_bytes, model).values())
 
 
 # ----------------------------------------------------------------- heterogeneous result gather
@@ -483,6 +513,7 @@ class GramsFirst:
         self.scratch = {}
         self.ows = {}        # per-lane workspaces of the per-linear ("one") block loops
         self.stall = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self._s1_streams = []  # per-channel S1 / d of the second, third, ... width
 
     @property
     def percdamp(self):
@@ -575,9 +606,27 @@ class GramsFirst:
         if not self.batched:
             return
         caller = torch.cuda.current_stream(self.dev)
-        for g in sorted(self.groups):  # per-channel groups: S1 / d once per Gram (caller's stream)
-            grp = self.groups[g]
-            if grp.get("S1d") is not None:
+        # per-channel groups: S1 / d once per Gram; the widths' launch pairs run side by side (one
+        # stream each, joined back into the caller's): each pair ends in serial d chains and a
+        # partial last wave, which a shard's few items no longer hide (bit-identical either way)
+        s1g = [g for g in sorted(self.groups) if self.groups[g].get("S1d") is not None]
+        if len(s1g) > 1 and self.dev.type == "cuda":
+            while len(self._s1_streams) < len(s1g) - 1:
+                self._s1_streams.append(torch.cuda.Stream(self.dev))
+            for k, g in enumerate(s1g):
+                grp = self.groups[g]
+                if k == 0:
+                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
+                    continue
+                st = self._s1_streams[k - 1]
+                st.wait_stream(caller)
+                with torch.cuda.stream(st):
+                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
+            for st in self._s1_streams[:len(s1g) - 1]:
+                caller.wait_stream(st)
+        else:
+            for g in s1g:
+                grp = self.groups[g]
                 self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
         self.inv_done = {}
         live = [g for g in sorted(self.groups) if self.groups[g]["Hinv"] is not None]
@@ -663,6 +712,10 @@ class GramsFirst:
                 n, m = W.shape
                 if eng.group_supported(n, m, bs, flags):
                     classes.setdefault((n, m, W.dtype), []).append((run, k, W, grp["G"][z], Hz))
+                elif S1z is not None and eng.perchannel_group_supported(m):
+                    # per-channel (one block) with its Gram's S1 / d formed: grouped by width and
+                    # dtype whatever the row count (pt2q_quantize_perchannel_group)
+                    classes.setdefault(("pc", m, W.dtype), []).append((run, k, W, grp["G"][z], Hz, S1z))
                 else:  # a lone linear of an unsupported shape: its own loop on the next lane
                     classes.setdefault(("one", j, k), []).append((run, k, W, grp["G"][z], Hz, S1z))
         caller = torch.cuda.current_stream(self.dev)
@@ -671,11 +724,13 @@ class GramsFirst:
         # longest first onto the least-loaded lane (LPT on the block-loop cost model)
         plan = []
         for ckey, items in classes.items():
-            size = max(1, min(self.group, -(-len(items) // len(lanes))))
+            cap = eng.PC_GROUP_MAX if ckey[0] == "pc" else self.group
+            size = max(1, min(cap, -(-len(items) // len(lanes))))
             for c0 in range(0, len(items), size):
                 chunk = items[c0:c0 + size]
-                n, m = chunk[0][2].shape
-                plan.append((len(chunk) * block_loop_cost(n, m, bs), ckey, chunk))
+                cost = sum(block_loop_cost(c[2].shape[0], c[2].shape[1], bs) if ckey[0] != "pc"
+                           else c[2].shape[0] * c[2].shape[1] * SHARD_MODEL["loop_pc"] for c in chunk)
+                plan.append((cost, ckey, chunk))
         plan.sort(key=lambda x: -x[0])
         load = [0.0] * len(lanes)
         for cost, ckey, chunk in plan:
@@ -686,6 +741,18 @@ class GramsFirst:
             for key in {c[0].key for c in chunk}:
                 self._wait_inverse(ln.stream, key)
             with torch.cuda.stream(ln.stream):
+                if ckey[0] == "pc":  # one launch sequence over the chunk's rows (lane workspace)
+                    nbytes = lib.lib().pt2q_quantize_perchannel_group_workspace_bytes(eng.PC_GROUP_MAX)
+                    okey = ("pc", id(ln))
+                    if okey not in self.ows:
+                        self.ows[okey] = lib.workspace(nbytes, self.dev)
+                    ws = self.ows[okey]
+                    outs = eng.quantize_perchannel_group([c[2] for c in chunk], [c[5] for c in chunk], mi,
+                                                         workspace=ws, check=False)
+                    state.statuses.append(lib.status_view(ws).clone())
+                    for (run, k, _, _, _, _), out in zip(chunk, outs):
+                        run.outs[k] = out
+                    continue
                 if ckey[0] == "one":  # stream-ordered like a group: lane workspace, status read in finish()
                     run, k, W, G, H, S1z = chunk[0]
                     n, m = W.shape

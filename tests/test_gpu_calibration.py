@@ -23,10 +23,14 @@ pytestmark = pytest.mark.gpu
                                          ((13, 100, 7, 1, 333, 5), 256, torch.float16),
                                          ((3, 2, 1, 1, 701), 200, torch.bfloat16),
                                          ((5, 64, 3), 96, torch.float32)])
-def test_gram_continue_equals_concatenated(pt2q, splits, m, dt):
+@pytest.mark.parametrize("buffer_rows", [32768, 0, 104])
+def test_gram_continue_equals_concatenated(pt2q, splits, m, dt, buffer_rows):
+    """The streamed Gram == the Gram of the concatenated rows, bit for bit: staged through the
+    default buffer, per batch (buffer_rows=0: remainder rows carried), and through a 104-row buffer
+    that fills and flushes mid-batch many times (chains continued at multiples of 8 rows)."""
     X = synth.activations(21 + m, sum(splits), m)
     Xd = cuda(X).to(dt)
-    acc = pt2q.GramAccumulator(m, "cuda")
+    acc = pt2q.GramAccumulator(m, "cuda", buffer_rows=buffer_rows)
     s = 0
     for k in splits:
         acc.add(Xd[s:s + k])

@@ -252,3 +252,55 @@ def test_s1_batched_equals_per_item_and_given(pt2q, m, batch):
         b = pt2q.engine.quantize_blocks(Wd, Gs[1], None, block_size=m, s1d=S1d[1])
         for x, y in ((a.T, b.T), (a.alpha, b.alpha), (a.mu, b.mu), (a.iters, b.iters)):
             assert bits_equal(host(x.float()), host(y.float()))
+
+
+@pytest.mark.parametrize("m,dt,ns,tdt", [
+    (5120, torch.bfloat16, (333, 80, 600, 16), torch.int8),      # register rows, mixed row counts
+    (5120, torch.bfloat16, (70, 45), torch.float32),             # fp32 codes
+    (4104, torch.float16, (77, 130, 33), torch.int8),            # streamed rows, ragged last chunk
+    (13824, torch.bfloat16, (40, 24), torch.int8),               # the C5 down projection's width
+    (1000, torch.float32, (50, 17), torch.int8)])
+def test_perchannel_group_equals_per_linear(pt2q, m, dt, ns, tdt):
+    """pt2q_quantize_perchannel_group: every linear of the group (row counts differ, one of them
+    all-zero so its launch takes the grouped repair, another with NO AGA) == quantize_blocks on
+    that linear alone (block_size = m, the same S1 / d): codes, alpha, mu, perm, ITF count."""
+    eng = pt2q.engine
+    Ws, s1ds = [], []
+    G = pt2q.gram(pt2q.fill_synthetic((384, m), m + 5, std=1.0, outliers=True).to(dt))
+    S1d = eng.s1_from_gram_batched(G.unsqueeze(0).contiguous())[0]
+    for z, n in enumerate(ns):
+        W = pt2q.fill_synthetic((n, m), 1000 * z + n + m, std=0.02)
+        if z == 1:
+            W.zero_()  # every row's init codes zero: the whole-block repair (quantizer.py:164)
+        Ws.append(W.to(dt))
+        s1ds.append(None if z == len(ns) - 1 and len(ns) > 2 else S1d)
+    outs = eng.quantize_perchannel_group(Ws, s1ds, t_dtype=tdt)
+    torch.cuda.synchronize()
+    for z, (W, s1, out) in enumerate(zip(Ws, s1ds, outs)):
+        if s1 is None:
+            ref = eng.quantize_blocks(W, None, None, block_size=m, aga=pt2q._lib.AGA_NONE, t_dtype=tdt)
+        else:
+            ref = eng.quantize_blocks(W, G, None, block_size=m, t_dtype=tdt, s1d=s1)
+        for x, y in ((out.T, ref.T), (out.alpha, ref.alpha), (out.mu, ref.mu), (out.perm, ref.perm),
+                     (out.iters, ref.iters)):
+            assert bits_equal(host(x.float()), host(y.float())), z
+    assert int(host(outs[1].iters)[0]) == 0 and not host(outs[1].T).any()
+
+
+def test_perchannel_group_of_sixteen_vs_oracle(pt2q):
+    """A full group (16 linears, the C5 q/k/v/o and gate/up row counts scaled down) vs the oracle,
+    each with its own Gram's S1 / d, in one launch sequence."""
+    eng = pt2q.engine
+    m, dt = 5120, torch.bfloat16
+    Gs = torch.stack([pt2q.gram(pt2q.fill_synthetic((256, m), 500 + z, std=1.0, outliers=True).to(dt))
+                      for z in range(4)]).contiguous()
+    S1d = eng.s1_from_gram_batched(Gs)
+    Ws = [pt2q.fill_synthetic((48 + 16 * (z % 3), m), 900 + z, std=0.02).to(dt) for z in range(16)]
+    outs = eng.quantize_perchannel_group(Ws, [S1d[z % 4] for z in range(16)])
+    torch.cuda.synchronize()
+    orc.set_threads(16)
+    for z in (0, 5, 10, 15):
+        ref = orc.quantize_blocks(host(Ws[z].float()), host(Gs[z % 4]), np.zeros((1, 1), np.float32), m, True, 1)
+        np.testing.assert_array_equal(host(outs[z].T.float()), ref["T"].astype(np.float32))
+        assert bits_equal(host(outs[z].alpha), ref["alpha"]) and bits_equal(host(outs[z].mu), ref["mu"])
+        np.testing.assert_array_equal(host(outs[z].iters), ref["iters"])

@@ -349,6 +349,11 @@ def test_bench_gpus8_dry_run_full_models(model, linears):
         want = sum(sh.unit_cost(units[i], bs) for i in shards[r["rank"]])
         assert abs(r["predicted_cost_s"] - want) <= 1e-9 * want
     assert d["lpt_balance"]["predicted_max_over_mean"] <= 1.10
+    # the refitted phase model of every rank's step (fixed per-launch latencies included)
+    assert d["lpt_balance"]["shard_model_max_over_mean"] <= 1.10
+    for r in d["ranks"]:
+        want = sh.shard_cost([units[i] for i in shards[r["rank"]]], bs, 2)
+        assert abs(r["predicted_shard_s"] - want) <= 1e-9 * want
 
 
 def test_bench_refuses_gpus_world_size_mismatch():
@@ -383,3 +388,26 @@ def test_grams_first_keeps_an_early_stall():
     with pytest.raises(pt2q._lib.Pt2qError, match="Gram partial-tile"):
         gf.check()
     gf.check()  # cleared after the read
+
+
+@pytest.mark.parametrize("model,bs,prof", [("llama-2-7b", 128, "r06a_shards_c4.json"),
+                                           ("llama-2-13b", 1 << 14, "r06a_shards_c5.json")])
+def test_shard_model_matches_measured_shards(model, bs, prof):
+    """sharding.shard_cost / shard_phases against the one-GPU shard timings of C4 and C5 committed
+    under profiles/ (bench.py --gpus 8 --shard all): every shard's step and the whole step within
+    10 %, and each modelled phase of the whole step within 10 % of its measured wall."""
+    import json
+    sh = _sharding()
+    with open(os.path.join(ROOT, "profiles", prof)) as f:
+        d = json.load(f)
+    units = sh.model_units(model)
+    shards = sh.assign_lpt([sh.unit_cost(u, bs) for u in units], 8)
+    for rec in d["shards"]:
+        mine = [units[i] for i in shards[rec["rank"]]]
+        assert len(mine) == rec["units"]
+        pred = sh.shard_cost(mine, bs) * 1e3
+        assert abs(pred - rec["ms_per_step"]) <= 0.10 * rec["ms_per_step"], (rec["rank"], pred, rec["ms_per_step"])
+    whole = sh.shard_phases(units, bs)
+    assert abs(sum(whole.values()) * 1e3 - d["t1_ms"]) <= 0.10 * d["t1_ms"]
+    for k, v in d["t1_phase_s"].items():
+        assert abs(whole[k] - v) <= 0.10 * v, (k, whole[k], v)
