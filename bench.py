@@ -751,7 +751,7 @@ MI355X_VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 STAGE_KERNELS = {"gram": "gram16b_kernel / gram_streamk_kernel", "inverse": "chol_* + rank_update2 + gemmx_kernel",
                  "setup": "transpose_to_f32 + group_init", "ssr": "ssr_wbar_* + ssr_sim* + ssr_topk",
-                 "atq": "atq_block_kernel / atq_wide_* + atq_finish", "ef": "ef2_gemm_kernel (ef_gemm_kernel with PT2Q_EF_V2=0)",
+                 "atq": "atq_block_kernel + atq_finish_kernel", "ef": "ef2_gemm_kernel<4, true>",
                  "out": "transpose_i8 / transpose_f32"}
 
 
@@ -790,8 +790,9 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
     if b["atq"] > 0:
         st["atq"] = {"bound": "hbm/latency", "kernel_busy_s": b["atq"], "bytes": work["atq_bytes"],
                      "frac_hbm": work["atq_bytes"] / b["atq"] / HBM, "source": src}
-        if work["atq_valu"] > 0:  # per-channel rows: VALU-bound ITF passes
-            st["atq"].update(bound="valu", valu_lane_ops=work["atq_valu"],
+        if work["atq_valu"] > 0:  # per-channel rows: HBM fraction headline, the ITF passes' VALU beside it
+            st["atq"].update(kernels="atq_pcr_kernel / atq_pc_kernel (pt2q_quantize_perchannel_group)",
+                             valu_lane_ops=work["atq_valu"],
                              frac_valu=work["atq_valu"] / b["atq"] / (MI355X_VALU_PEAK_TOPS * 1e12),
                              valu_peak_tops=MI355X_VALU_PEAK_TOPS)
     io = b["setup"] + b["out"]
@@ -825,8 +826,12 @@ def stage_roofline(work, phase_s, busy, ms_per_step, world, gram_peak_tf, commit
         fl = work["chol_fl"] if dom == "inverse" else work["ef_fl"]
         d.update(bound="mfma", unit="TFLOP/s", achieved=fl / b[dom] / 1e12, peak=MI355X_F32_MFMA_PEAK_TFLOPS)
     elif dom == "atq" and work["atq_valu"] > 0:
-        d.update(bound="valu", unit="Tlane-op/s", achieved=work["atq_valu"] / b[dom] / 1e12, peak=MI355X_VALU_PEAK_TOPS,
-                 hbm_frac=work["atq_bytes"] / b[dom] / HBM)
+        # per-channel rows: the headline is the HBM fraction of the bytes the stage must move (W
+        # read once, codes written, the Gram read once for S1); its VALU work rides beside it
+        d.update(kernels="atq_pcr_kernel / atq_pc_kernel (pt2q_quantize_perchannel_group)", bound="hbm",
+                 unit="GB/s", achieved=work["atq_bytes"] / b[dom] / 1e9, peak=MI355X_HBM_PEAK_GBS,
+                 valu_achieved_tlane_ops=work["atq_valu"] / b[dom] / 1e12, valu_peak_tlane_ops=MI355X_VALU_PEAK_TOPS,
+                 frac_valu=work["atq_valu"] / b[dom] / (MI355X_VALU_PEAK_TOPS * 1e12))
     else:
         by = work["ssr_bytes"] if dom == "ssr" else work["atq_bytes"]
         d.update(bound="hbm", unit="GB/s", achieved=by / b[dom] / 1e9, peak=MI355X_HBM_PEAK_GBS)

@@ -955,6 +955,97 @@ __global__ __launch_bounds__(128) void s1_row_wg_kernel(const float* A, long lda
   S1[j] = s;
 }
 
+// S1 of whole wide Grams (the batched per-channel S1 / d, m > 512; m % 4 == 0, 16-byte aligned
+// rows): the same sequential row chains as s1_rows_kernel, fed by a wave-private LDS-DMA ring.
+// s1_rows_kernel staged each tile by register loads whose LDS stores waited for them before the
+// chains ran, one tile in flight per workgroup: ~3.5 TB/s, and a shard's few Grams could not
+// hide the round trips (1.8 ms for the S1 phase of one rank's C5 shard).  Here a one-wave
+// workgroup owns 64 rows (lane l: row r0 + l's chain) and DMAs them 32 columns per tile (8 KiB,
+// 8 x 1 KiB global_load_lds_dwordx4) into an S1R_STAGES-deep LDS ring, S1R_STAGES - 1 tiles ahead,
+// with no barrier.  32 KiB per workgroup: five share a CU, so a shard's 1,080 row groups of its
+// m = 13824 Grams are resident at once (256-row workgroups left a second round of 14 on a few CUs,
+// doubling the launch).  LDS layout: row rr at 128 rr bytes,
+// its 16-byte chunk k at slot k ^ ((rr >> 1) & 7) -- the DMA lanes load the permuted chunks, so
+// the chain lanes' ds_read_b128 of one chunk index hit 16 distinct bank groups per 16 lanes.
+constexpr int S1R_COLS = 32, S1R_STAGES = 4, S1R_WROWS = 64;
+constexpr int S1R_WSTAGE = S1R_WROWS * S1R_COLS * 4;  // 8 KiB per wave and stage
+
+typedef float s1f4 __attribute__((ext_vector_type(4)));
+
+template <int N>
+PT2Q_DEV void s1r_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+PT2Q_DEV void s1r_vmcnt(int younger) {  // tiles still in flight after the one to read (x 8 DMAs)
+  switch (younger) {
+    case 0: s1r_vm<0>(); break;
+    case 1: s1r_vm<8>(); break;
+    case 2: s1r_vm<16>(); break;
+    case 3: s1r_vm<24>(); break;
+    default: s1r_vm<32>(); break;
+  }
+}
+
+__global__ __launch_bounds__(64) void s1_ring_kernel(const float* G, long ldg, int m, float* S1, long sG, long sS) {
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[S1R_STAGES * S1R_WSTAGE];
+  typedef __attribute__((address_space(3))) void* lptr;
+  const int lane = threadIdx.x & 63;
+  G += blockIdx.y * sG;
+  S1 += blockIdx.y * sS;
+  const int r0 = blockIdx.x * S1R_WROWS;
+  uint8_t* wring = ring;
+  const uint32_t wlds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)wring;
+  const int ntile = (m + S1R_COLS - 1) / S1R_COLS;
+  // this lane's DMA source in each of a tile's 8 instructions: row rr = 8 q + lane / 8, chunk
+  // k = (lane % 8) ^ ((rr >> 1) & 7) -- rows past m read row 0 (results dropped)
+  const float* src[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int rr = 8 * q + (lane >> 3);
+    const int row = r0 + rr < m ? r0 + rr : 0;
+    src[q] = G + (long)row * ldg + 4 * ((lane & 7) ^ ((rr >> 1) & 7));
+  }
+  auto issue = [&](int t) {
+    uint8_t* stg = wring + (t % S1R_STAGES) * S1R_WSTAGE;
+    const int c0 = t * S1R_COLS;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      // chunks past m (only in the last tile; m % 4 == 0) read column 0 and are masked below
+      const int col = c0 + 4 * ((lane & 7) ^ (((8 * q + (lane >> 3)) >> 1) & 7));
+      __builtin_amdgcn_global_load_lds(col < m ? src[q] + c0 : src[q] - 4 * ((lane & 7) ^ (((8 * q + (lane >> 3)) >> 1) & 7)),
+                                       (lptr)(stg + q * 1024), 16, 0, 0);
+    }
+  };
+  const int pre = ntile < S1R_STAGES - 1 ? ntile : S1R_STAGES - 1;
+  for (int t = 0; t < pre; ++t) issue(t);
+  const int f = (lane >> 1) & 7;
+  float s = 0.0f;
+  for (int t = 0; t < ntile; ++t) {
+    if (t + S1R_STAGES - 1 < ntile) issue(t + S1R_STAGES - 1);
+    const int ahead = ntile - 1 - t;  // tiles issued after tile t
+    s1r_vmcnt(ahead < S1R_STAGES - 1 ? ahead : S1R_STAGES - 1);
+    const uint32_t base = wlds + (t % S1R_STAGES) * S1R_WSTAGE + lane * 128;
+    s1f4 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(x[k]) : "v"(base + ((k ^ f) << 4)));
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                 :: "memory");
+    if ((t + 1) * S1R_COLS <= m) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s = s + x[k][u];
+    } else {  // the last, partial tile: only the columns < m (whole chunks)
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (t * S1R_COLS + 4 * k < m)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) s = s + x[k][u];
+    }
+  }
+  if (r0 + lane < m) S1[r0 + lane] = s;
+}
+
 // d = sequential sum of S1 (j ascending); S1 is staged through LDS in chunks so the serial
 // chain never waits on a global load.
 __global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, float* d, long sS, long sD) {
@@ -968,13 +1059,24 @@ __global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, f
     for (int j = threadIdx.x; j < len; j += 256) v[j] = S1[j0 + j];
     __syncthreads();
     if (threadIdx.x == 0) {
+      // the next 16 values are read while the current 16 are added (the chain never waits on LDS)
       int j = 0;
-      for (; j + 8 <= len; j += 8) {
-        float t[8];
+      if (len >= 16) {
+        float t[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = v[j + u];
+        for (int u = 0; u < 16; ++u) t[u] = v[u];
+        for (; j + 32 <= len; j += 16) {
+          float nx[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dd = dd + t[u];
+          for (int u = 0; u < 16; ++u) nx[u] = v[j + 16 + u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) dd = dd + t[u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) t[u] = nx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) dd = dd + t[u];
+        j += 16;
       }
       for (; j < len; ++j) dd = dd + v[j];
     }
@@ -1117,7 +1219,10 @@ int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, 
     return PT2Q_OK;
   }
   const long sS = m + 1;
-  if (m > 512)
+  const bool ring = m % 4 == 0 && ldg % 4 == 0 && sG % 4 == 0 && ((uintptr_t)G & 15) == 0;
+  if (m > 512 && ring)
+    hipLaunchKernelGGL(s1_ring_kernel, dim3(ceil_div(m, S1R_WROWS), batch), dim3(64), 0, st, G, ldg, m, S1d, sG, sS);
+  else if (m > 512)
     hipLaunchKernelGGL(s1_rows_kernel, dim3(ceil_div(m, S1W_ROWS), batch), dim3(256), 0, st, G, ldg, nullptr, m,
                        S1d, sG, sS);
   else

@@ -231,7 +231,7 @@ def test_per_channel_zero_block(pt2q, m, dt):
     assert not host(out.T).any() and not host(out.alpha).any() and not host(out.mu).any()
 
 
-@pytest.mark.parametrize("m,batch", [(5120, 3), (1000, 2), (300, 2), (100, 3)])
+@pytest.mark.parametrize("m,batch", [(5120, 3), (1000, 2), (300, 2), (100, 3), (13824, 2), (4104, 5), (516, 1)])
 def test_s1_batched_equals_per_item_and_given(pt2q, m, batch):
     """pt2q_s1_from_gram_batched (S1 = S·1, d = 1ᵀS1 of several Grams in one launch pair) ==
     pt2q_s1_from_gram per item, bit for bit; a per-channel block loop fed the formed S1 / d
@@ -248,8 +248,9 @@ def test_s1_batched_equals_per_item_and_given(pt2q, m, batch):
         assert bits_equal(host(S1d[z, :m]), host(S1)) and bits_equal(host(S1d[z, m:]), host(d))
     if m > 512:
         Wd = pt2q.fill_synthetic((96, m), 77, std=0.02).to(torch.bfloat16)
-        a = pt2q.engine.quantize_blocks(Wd, Gs[1], None, block_size=m)
-        b = pt2q.engine.quantize_blocks(Wd, Gs[1], None, block_size=m, s1d=S1d[1])
+        z = batch - 1
+        a = pt2q.engine.quantize_blocks(Wd, Gs[z], None, block_size=m)
+        b = pt2q.engine.quantize_blocks(Wd, Gs[z], None, block_size=m, s1d=S1d[z])
         for x, y in ((a.T, b.T), (a.alpha, b.alpha), (a.mu, b.mu), (a.iters, b.iters)):
             assert bits_equal(host(x.float()), host(y.float()))
 
