@@ -96,9 +96,9 @@ def model_units(model: str, layers: Optional[int] = None, tokens: Optional[int] 
 # per-channel units, S1 / d -- then the grouped block loops on the lanes), phase by phase, with the
 # fixed latencies that do NOT shrink with a shard written out.  Constants fitted (round 6) to the
 # phase walls of the whole 7B / 13B steps and of their 8-rank shards timed alone on one MI355X
-# (bench.py --gpus 8 --shard all; profiles/r06a_shards_c4.json, r06a_shards_c5.json): the model
-# reproduces all four within 3 % (C4 2236 vs 2232 ms, its shards 302 vs 298-306 ms; C5 112 vs 112
-# ms, its shards 15.9 vs 15.3-15.8 ms).
+# (bench.py --gpus 8 --shard all; profiles/r06a_shards_c4.json, and r06e_shards_c5.json after the
+# S1 ring kernel): the model reproduces all four within 6 % (C4 2236 vs 2232 ms, its shards 302 vs
+# 298-306 ms; C5 112 vs 112 ms, its shards 15.6 vs 14.9-15.5 ms).
 #   Gram: the batched 16-bit Gram runs 256 x 256 tiles in waves of one tile per CU; a wave costs
 #     N * 2 * 256^2 / GRAM_TILE_RATE (a CU's MFMA rate under the power limit) + GRAM_TILE_FIXED
 #     (the tile's ramp and its 512 KiB mirrored epilogue: 54 us, which dominates at N = 4096).
@@ -113,7 +113,7 @@ SHARD_MODEL = dict(
     cus=256,
     gram_tile_rate=4.887e12, gram_tile_fixed=5.43e-5, gram_batch=128,
     inv_step=4.53e-5, inv_rate=1.134e14, chunk=32,
-    s1_fixed=5.9e-4, s1_bw=4.47e12,
+    s1_fixed=5.4e-4, s1_bw=6.48e12,
     loop_nr=4.056e-12, loop_block=8.53e-5, loop_pc=3.28e-12, loop_pc_group=9.0e-4,
     lanes=3, group=16, pc_group=16,
 )
