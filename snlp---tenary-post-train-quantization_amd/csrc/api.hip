@@ -59,6 +59,8 @@ Pt2qTuning load_tuning() {
   geti("PT2Q_ATQ_PROBE", t.atq_probe);
   geti("PT2Q_EF2_STAGGER", t.ef2_stagger);
   geti("PT2Q_EF2_PER_CU", t.ef2_per_cu);
+  geti("PT2Q_EF2_TEAMS", t.ef2_teams);
+  geti("PT2Q_EF2_TEAM_OFFSET", t.ef2_team_offset);
   getb("PT2Q_EF2_G1LDS", t.ef2_g1lds);
   if (t.ef2_per_cu != 1) t.ef2_per_cu = 2;
   if (t.wide_waves != 8) t.wide_waves = 4;

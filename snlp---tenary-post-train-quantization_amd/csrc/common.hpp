@@ -143,6 +143,8 @@ struct Pt2qTuning {
   int ef_v2 = 1;               // PT2Q_EF_V2: 1 = ef2_gemm_kernel (two workgroups per CU, default), 0 = ef_gemm_kernel
   bool ef2_g1lds = true;       // PT2Q_EF2_G1LDS=0: column group 1's old values loaded in the epilogue
   int ef2_per_cu = 2;          // PT2Q_EF2_PER_CU: ef2 workgroups per CU (1 or 2)
+  int ef2_teams = 1;           // PT2Q_EF2_TEAMS: 2 = one 8-wave workgroup of two barrier-coupled teams per CU
+  int ef2_team_offset = 5;     // PT2Q_EF2_TEAM_OFFSET: barriers team 1 starts behind team 0
   int ef2_stagger = 0;         // PT2Q_EF2_STAGGER: ef2 start de-phasing (0: off)
   int ef2_probe = 0;           // PT2Q_EF2_PROBE: ef2 knock-out mask (tools only; results garbage)
   int atq_probe = 0;           // PT2Q_ATQ_PROBE (DEV_PROBES builds only; results garbage): block-ATQ

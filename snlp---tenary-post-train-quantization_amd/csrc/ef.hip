@@ -40,6 +40,9 @@ constexpr unsigned EF_DROP = 0x80000000u;    // buffer offset past any Wt (dropp
 
 __device__ uint4 ef_zero16;  // DMA source of the k rows past bs (zero-initialised)
 
+// wave index inside a team of 4 waves (a workgroup is one team, or two: ef2_gemm_kernel TEAMS)
+PT2Q_DEV int ef_wave() { return (int)(threadIdx.x >> 6) & 3; }
+
 struct EfArgs {
   const float* Ck;  // C[k][e], ld m
   long ldk;
@@ -55,6 +58,7 @@ struct EfArgs {
   int stagger;      // ef2: the grid's second half first sleeps stagger x 4K cycles (PT2Q_EF2_STAGGER)
   int probe;        // ef2 development knock-outs (PT2Q_EF2_PROBE, tools only; results garbage):
                     // 1 = Wt traffic dropped, 2 = operand DMAs from one hot chunk, 4 = no MFMAs
+  int toff;         // ef2 TEAMS = 2: barriers team 1 starts behind team 0
 };
 
 // The arguments of linear z (its workspace slice).
@@ -74,7 +78,7 @@ PT2Q_DEV EfArgs ef_linear(const EfArgs& a0, int z) {
 // the data come from row 0 (garbage in rows / columns whose results are dropped), so every wave
 // issues exactly EF_DMA instructions.
 PT2Q_DEV void ef_stage_q(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, int q, bool withB) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
   typedef __attribute__((address_space(3))) void* lptr;
   const int kr = (wave * 8 + q) * 2 + (lane >> 5);  // k row inside the stage
   const int k = h * EF_KH + kr;
@@ -107,7 +111,7 @@ struct EfVo {
 };
 
 PT2Q_DEV void ef_voff(const EfArgs& a, EfVo& v) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int kr = (wave * 8 + q) * 2 + (lane >> 5), d = 4 * (lane & 31);
@@ -128,7 +132,7 @@ PT2Q_DEV int ef_stage_any(const EfArgs& a, int e0, int i0, int h, uint8_t* stg, 
   const bool fast = (h + 1) * EF_KH <= a.bs && e0 + EF_T <= a.nr && i0 + EF_T <= a.ldw &&
                     !probe::ef_zero_dma && !probe::ef_no_dma;
   if (!fast) return ef_stage(a, e0, i0, h, stg, withB);
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(ef_wave());
   const char* ba = (const char*)(a.Ck + (long)h * EF_KH * a.ldk + e0);
   const char* bb = (const char*)(a.Et + (long)h * EF_KH * a.ldw + i0);
   const uint32_t mA = stg_lds + (uint32_t)(wv * 8 * 1024), mB = mA + EF_PANEL;
@@ -214,7 +218,7 @@ struct EfAccT {
   // the KS / 2 k-pairs of one stage (k rows past bs are zero in LDS: exact no-op steps)
   template <class IO>
   PT2Q_DEV void half(uint32_t stg, IO& io) {
-    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+    const int lane = threadIdx.x & 63, wave = ef_wave();
     const int wr = wave >> 1, wc = wave & 1, li = lane & 31, lk = lane >> 5;
     const uint32_t bA = stg + lk * EF_ROWB + (wr * 64 + li) * 4;
     const uint32_t bB = stg + KS * EF_ROWB + lk * EF_ROWB + (wc * 64 + li) * 4;
@@ -228,11 +232,11 @@ struct EfAccT {
 using EfAcc = EfAccT<EF_KH>;
 
 PT2Q_DEV int ef_row(int e0, int rm) {
-  const int lane = threadIdx.x & 63, wr = (threadIdx.x >> 6) >> 1;
+  const int lane = threadIdx.x & 63, wr = ef_wave() >> 1;
   return e0 + wr * 64 + rm * 32 + (lane & 31);
 }
 PT2Q_DEV int ef_col(int i0, int rn, int q) {
-  const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
+  const int lane = threadIdx.x & 63, wc = ef_wave() & 1;
   return i0 + wc * 64 + rn * 32 + 8 * q + 4 * (lane >> 5);
 }
 
@@ -248,7 +252,7 @@ PT2Q_DEV unsigned ef_coff(const EfArgs& a, const int (&wrow)[2], int i0, int rm,
 // bytes (the constant folds into the buffer instruction's offset field), rb[rm] = EF_DROP for a row
 // past nr or a column half past ldw (ldw % 64 == 0, so a wave's 64 columns are in or out together)
 PT2Q_DEV void ef_rowbase(const EfArgs& a, const int (&wrow)[2], int i0, uint32_t (&rb)[2]) {
-  const int lane = threadIdx.x & 63, wc = (threadIdx.x >> 6) & 1;
+  const int lane = threadIdx.x & 63, wc = ef_wave() & 1;
   const int i = i0 + wc * 64 + 4 * (lane >> 5);
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
@@ -294,7 +298,7 @@ constexpr int EF_RED = 512; // LDS floats: [wave][64] sums + [wave][64] spare sl
 template <int J>
 PT2Q_DEV void ef_wbar_step(const int (&prow)[2], const u32x4 (&pend)[EF_CV], float* red) {
   constexpr int rn = J >> 4, q = (J >> 2) & 3, u = J & 3;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
   const float v0 = prow[0] >= 0 ? __uint_as_float(pend[rn * 4 + q][u]) : 0.0f;
   const float v1 = prow[1] >= 0 ? __uint_as_float(pend[(2 + rn) * 4 + q][u]) : 0.0f;
   float x = bfly16(v0 + v1);
@@ -342,7 +346,7 @@ PT2Q_DEV void ef_wb_c(EfWb2& w) {
 
 template <int J>
 PT2Q_DEV void ef_wb_d(EfWb2& w, float* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
   const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w.x0), 0x142, 0xA, 0xF, false));
   const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w.x1), 0x142, 0xA, 0xF, false));
   const float y0 = w.x0 + r0, y1 = w.x1 + r1;  // row_bcast:15
@@ -418,7 +422,7 @@ PT2Q_DEV void ef_vmcnt(int n) {
 // lane reads (b128, all in flight) and every wave issues exactly EF_PS buffer stores (real ones:
 // lanes 0 and 32 of the row-half-0 waves, i < n; the rest dropped).
 PT2Q_DEV void ef_wbar_store(int n, __amdgpu_buffer_rsrc_t rp, bool valid, int e0, int i0, const float* red) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wr = wave >> 1, wc = wave & 1;
+  const int lane = threadIdx.x & 63, wave = ef_wave(), wr = wave >> 1, wc = wave & 1;
   const int h = lane >> 5;
   const bool mine = valid && wr == 0 && (lane & 31) == 0;
   const long cb = (long)(e0 / EF_T) * n;
@@ -601,7 +605,7 @@ constexpr int E2_STAGE = 2 * E2_PANEL;     // A + B: 32 KiB
 // One 16-B chunk q (< 4) of stage s of tile (e0, i0) by per-lane addresses (ragged stages); the
 // conventions of ef_stage_q (zero chunk past bs, in-range garbage in dropped rows / columns).
 PT2Q_DEV void e2_stage_q(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, int q, bool withB) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
   typedef __attribute__((address_space(3))) void* lptr;
   const int kr = (wave * 4 + q) * 2 + (lane >> 5);
   const int k = s * E2_KS + kr;
@@ -620,7 +624,7 @@ struct E2Vo {
 };
 
 PT2Q_DEV void e2_voff(const EfArgs& a, E2Vo& v) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = ef_wave();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int kr = (wave * 4 + q) * 2 + (lane >> 5), d = 4 * (lane & 31);
@@ -635,7 +639,7 @@ PT2Q_DEV int e2_stage(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, uint
                       bool withB) {
   if (a.probe & 2) {  // knock-out: every DMA from the one zero chunk (L2-hot)
     typedef __attribute__((address_space(3))) void* lptr;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = __builtin_amdgcn_readfirstlane(ef_wave());
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       __builtin_amdgcn_global_load_lds(&ef_zero16, (lptr)(stg + (wv * 4 + q) * 1024), 16, 0, 0);
@@ -649,7 +653,7 @@ PT2Q_DEV int e2_stage(const EfArgs& a, int e0, int i0, int s, uint8_t* stg, uint
     for (int q = 0; q < 4; ++q) e2_stage_q(a, e0, i0, s, stg, q, withB);
     return withB ? 8 : 4;
   }
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(ef_wave());
   const char* ba = (const char*)(a.Ck + (long)s * E2_KS * a.ldk + e0);
   const char* bb = (const char*)(a.Et + (long)s * E2_KS * a.ldw + i0);
   const uint32_t mA = stg_lds + (uint32_t)(wv * 4 * 1024), mB = mA + E2_PANEL;
@@ -729,7 +733,7 @@ PT2Q_DEV uint32_t e2_g1_chunk(int wv, int j) {
 }
 PT2Q_DEV void e2_g1_dma(__amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2], uint8_t* slot) {
   typedef __attribute__((address_space(3))) void* lptr;
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(ef_wave());
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     // row 8 j + lane / 8 of the wave: row block rm = j / 4, its base from that row's h = 0 lane
@@ -739,7 +743,7 @@ PT2Q_DEV void e2_g1_dma(__amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2], uint
   }
 }
 PT2Q_DEV void e2_g1_read(u32x4 (&c)[EF_CV], const uint8_t* slot) {
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(ef_wave());
   const int li = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
@@ -763,15 +767,28 @@ PT2Q_DEV void e2_g1_read(u32x4 (&c)[EF_CV], const uint8_t* slot) {
 // tile to tile (par).  Issue order: [rows: 2] [stage 2, 3 after compute 0, 1] [group 1: 8 after
 // compute 2] [group 0 loads: 8] [next stage 0 after compute 3] [epilogue: stores 0: 8, next stage
 // 1, stores 1: 8, w-bar: P].  Same products, same order: the same bits.
-template <int NST, bool G1L = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void ef2_gemm_kernel(
+//
+// TEAMS = 2 (development builds only, PT2Q_EF2_TEAMS): the two co-resident workgroups of a CU as
+// the two teams (waves 0-3, 4-7) of one 8-wave workgroup, each with its own ring, tiles and w-bar
+// scratch -- the same per-team code and bits -- but with every s_barrier common to both and team 1
+// started a0.toff barriers behind team 0, to hold one team's epilogue under the other's MFMAs.
+// Measured slower at every offset (13.9-14.4 vs 13.24 ms per 16-linear 4096^2 loop, offsets 0-7,
+// tools/ef2_teams_ab.sh): the loop's MFMA work (6.8 ms at the f32 peak) and its Wt read-modify-
+// write (33 GB, 6.6 ms at 5 TB/s) add up to the measured time, and the clock drops while both run
+//  -- the coupling only adds barrier waits.
+template <int NST, bool G1L = false, int TEAMS = 1>
+__global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 2))) void ef2_gemm_kernel(
     EfArgs a0, long wt_bytes, long part_bytes) {
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * E2_STAGE];
-  __shared__ __attribute__((aligned(16))) float red[EF_RED];  // w-bar wave sums (ef_wbar_step)
+  __shared__ __attribute__((aligned(1024))) uint8_t smem_all[TEAMS][2 * E2_STAGE];
+  __shared__ __attribute__((aligned(16))) float red_all[TEAMS][EF_RED];  // w-bar wave sums (ef_wbar_step)
+  const int team = TEAMS > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
+  uint8_t* const smem = smem_all[team];
+  float* const red = red_all[team];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   const int total = a0.ntile * a0.nz;
-  int t = blockIdx.x;
-  if (t >= total) return;
+  const int tstride = (int)gridDim.x * TEAMS;
+  int t = (int)blockIdx.x * TEAMS + team;
+  if (t >= total) return;  // (a terminated wave leaves every later s_barrier of its workgroup)
   auto corner = [&](int t, EfArgs& a, int& e0, int& i0) {
     const int z = t / a0.ntile, tl = t - z * a0.ntile;
     a = ef_linear(a0, z);
@@ -796,11 +813,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int z = a0.stagger; z > 0; --z) __builtin_amdgcn_s_sleep(64);
   e2_stage(a, e0, i0, 0, smem, lds0, vo, true);
   int Dn1 = e2_stage(a, e0, i0, 1, smem + E2_STAGE, lds0 + E2_STAGE, vo, true);
+  if (TEAMS > 1 && team == 1)  // behind team 0 (10 barriers per tile)
+    for (int k = 0; k < a0.toff; ++k) asm volatile("s_barrier" ::: "memory");
   int SP = 0;
   int par = 0;  // G1L: the slot of this tile's stage 0 (stage s in slot (s + par) & 1)
   static_assert(!G1L || NST == 4, "G1L: four K stages per tile");
   for (;;) {
-    const int tn = t + (int)gridDim.x;
+    const int tn = t + tstride;
     const bool more = tn < total;
     int en = e0, in = i0, nrow[2];
     EfArgs an = a;
@@ -900,7 +919,8 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
   if (part && (n <= 0 || n % 4 || n > ldw || (uintptr_t)part % 16 || part_bytes >= (long)EF_DROP))
     return PT2Q_E_UNSUPPORTED;
   EfArgs a{Ck, ldk, Et, Wt, ldw, crow, nr, bs, ceil_div(nr, EF_T), ceil_div(ldw, EF_T), 0, bs > EF_KH ? 2 : 1,
-           grp ? grp->ws : 0l, (int)grp_z(grp), part, n, pt2q_tuning().ef2_stagger, pt2q_tuning().ef2_probe};
+           grp ? grp->ws : 0l, (int)grp_z(grp), part, n, pt2q_tuning().ef2_stagger, pt2q_tuning().ef2_probe,
+           pt2q_tuning().ef2_team_offset};
   a.ntile = a.te * a.ti;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -908,6 +928,16 @@ int pt2q_launch_ef(const float* Ck, long ldk, const float* Et, float* Wt, long l
     // workgroups per CU (PT2Q_EF2_PER_CU, 1 or 2): with one, another lane's latency-bound
     // kernels (SSR, ATQ) find registers and LDS beside the error feedback on every CU
     const int grid2 = std::min(a.ntile * a.nz, pt2q_tuning().ef2_per_cu * cus);
+#ifdef PT2Q_DEV_PROBES
+    // two barrier-coupled teams (development A/B only: 13.9-14.4 vs 13.24 ms per 16-linear loop
+    // at every offset, tools/ef2_teams_ab.sh)
+    if (bs > 2 * E2_KS && pt2q_tuning().ef2_teams == 2) {  // one 8-wave workgroup of two teams per CU
+      const int gridt = std::min(ceil_div(a.ntile * a.nz, 2), cus);
+      hipLaunchKernelGGL((ef2_gemm_kernel<4, true, 2>), dim3(gridt), dim3(512), 0, st, a, wt_bytes, part_bytes);
+      PT2Q_LAUNCH_CHECK();
+      return PT2Q_OK;
+    }
+#endif
     if (bs <= 2 * E2_KS)
       hipLaunchKernelGGL(ef2_gemm_kernel<2>, dim3(grid2), dim3(256), 0, st, a, wt_bytes, part_bytes);
 #ifdef PT2Q_DEV_PROBES
