@@ -129,6 +129,12 @@ int pt2q_gram(const void* X, int xdtype, int64_t N, int m, int64_t ldx, float* G
  * gate/up inputs of all decoder layers). */
 int pt2q_gram_batched(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
                       float* G, void* stream);
+/* pt2q_gram_batched (16-bit X only) storing ONLY the upper triangle of each G (G[z][r][c] for
+ * c >= r; the strictly lower part is left as it was): a per-channel unit's Gram feeds nothing but
+ * S1 / d (quantizer.py:215-218), which pt2q_s1_from_upper_batched forms from the upper triangle
+ * with the same bits -- half the epilogue's stores.  PT2Q_E_UNSUPPORTED for fp32 X. */
+int pt2q_gram_batched_upper(int batch, const void* const* X, int xdtype, int64_t N, int m, int64_t ldx,
+                            float* G, void* stream);
 
 /* H = G / nsamples; H_ii += percdamp * mean(diag H).  Replaces main.py:129-133 and
  * gptq.py:94-98.  damp_dev (nullable) receives the damping value. */
@@ -239,6 +245,12 @@ int pt2q_s1_from_gram(const float* S, int64_t lds, int b, float* S1, float* d_de
  * Gram instead of once per linear (q/k/v and gate/up share one, main.py:289-299). */
 int pt2q_s1_from_gram_batched(const float* S, int64_t lds, int m, int batch, int64_t item_stride, float* S1d,
                               void* stream);
+/* pt2q_s1_from_gram_batched reading only the upper triangle of each S (S[c][r] for c < r taken
+ * from S[r][c]: the Gram's mirror is an exact copy) -- bit-identical on a symmetric S, and valid
+ * on pt2q_gram_batched_upper's output.  m > 512, m % 4 == 0, 16-byte aligned rows (else
+ * PT2Q_E_UNSUPPORTED). */
+int pt2q_s1_from_upper_batched(const float* S, int64_t lds, int m, int batch, int64_t item_stride, float* S1d,
+                               void* stream);
 
 /* compute_column_similarity_to_mean + select_next_block_ssr (reorder.py:36-61,107-143) on W
  * (n x m row-major fp32).  rem: r int64 ascending.  Writes min(b,r) entries of blk (selection

@@ -57,6 +57,7 @@ _SIGS = {
     "pt2q_gram_workspace_bytes": (SZ, [I]),
     "pt2q_gram": (I, [P, I, I64, I, I64, P, I64, I, P, SZ, P]),
     "pt2q_gram_batched": (I, [I, P, I, I64, I, I64, P, P]),
+    "pt2q_gram_batched_upper": (I, [I, P, I, I64, I, I64, P, P]),
     "pt2q_prepare_hessian": (I, [P, I64, I, I64, F, P, I64, P, P]),
     "pt2q_cholesky_inverse": (I, [P, I64, I, P, I64, P, SZ, P, P]),
     "pt2q_hessian_inverse_batched_workspace_bytes": (SZ, [I, I]),
@@ -73,6 +74,7 @@ _SIGS = {
     "pt2q_atq_stage": (I, [I, P, I64, I, I, P, P, P, I64, P, P, I, P, P, SZ, P]),
     "pt2q_s1_from_gram": (I, [P, I64, I, P, P, P]),
     "pt2q_s1_from_gram_batched": (I, [P, I64, I, I, I64, P, P]),
+    "pt2q_s1_from_upper_batched": (I, [P, I64, I, I, I64, P, P]),
     "pt2q_ssr_select": (I, [P, I64, I, I, P, I, I, P, P, P, P, SZ, P]),
     "pt2q_dequantize": (I, [P, P, P, I, P, I, I, I, P, P]),
     "pt2q_error_feedback_workspace_bytes": (SZ, [I, I, I]),

@@ -631,6 +631,14 @@ extern "C" int pt2q_gram_batched(int batch, const void* const* X, int xdtype, in
   return pt2q_launch_gram16_batched(X, xdtype, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream);
 }
 
+extern "C" int pt2q_gram_batched_upper(int batch, const void* const* X, int xdtype, int64_t N, int m,
+                                       int64_t ldx, float* G, void* stream) {
+  if (batch <= 0 || !X || !G || N < 0 || N > INT_MAX || m <= 0 || ldx < m) return PT2Q_E_ARG;
+  if (xdtype != PT2Q_F16 && xdtype != PT2Q_BF16) return PT2Q_E_UNSUPPORTED;
+  StageScope ts(PT2Q_TIMER_GRAM, (hipStream_t)stream);
+  return pt2q_launch_gram16_batched(X, xdtype, N, m, ldx, G, (long)m * m, batch, (hipStream_t)stream, true);
+}
+
 extern "C" int pt2q_prepare_hessian(const float* G, int64_t ldg, int m, int64_t nsamples,
                                     float percdamp, float* H, int64_t ldh, float* damp_dev,
                                     void* stream) {
@@ -862,6 +870,14 @@ extern "C" int pt2q_s1_from_gram_batched(const float* S, int64_t lds, int m, int
   if (batch == 0) return PT2Q_OK;
   StageScope ts(PT2Q_TIMER_ATQ, (hipStream_t)stream);  // the AGA's S1 / d (quantizer.py:215-218)
   return pt2q_launch_s1_batched(S, lds, m, batch, item_stride, S1d, (hipStream_t)stream);
+}
+
+extern "C" int pt2q_s1_from_upper_batched(const float* S, int64_t lds, int m, int batch, int64_t item_stride,
+                                          float* S1d, void* stream) {
+  if (!S || !S1d || m <= 0 || batch < 0 || lds < m || (batch > 1 && item_stride < lds * m)) return PT2Q_E_ARG;
+  if (batch == 0) return PT2Q_OK;
+  StageScope ts(PT2Q_TIMER_ATQ, (hipStream_t)stream);
+  return pt2q_launch_s1_batched(S, lds, m, batch, item_stride, S1d, (hipStream_t)stream, true);
 }
 
 extern "C" int pt2q_ssr_select(const float* W, int64_t ldw, int n, int m, const int64_t* rem, int r,

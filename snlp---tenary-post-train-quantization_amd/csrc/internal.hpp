@@ -83,7 +83,8 @@ int pt2q_launch_ssr_topk(const float* sim, const int* rem, int r, int b, int* bl
                          int* status = nullptr, const Grp* grp = nullptr);
 int pt2q_launch_select_seq(int mode, int p0, int bs, int m, const int* rem, int* blk,
                            int* newrem, int64_t* perm_out, hipStream_t st, const Grp* grp = nullptr);
-int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st);
+int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st,
+                           bool upper = false);
 int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b, float* S1,
                        float* d, hipStream_t st);
 int pt2q_launch_ef_coeffs(const float* Hinv, long ldh, const int* blk, int bs, const int* rem,
@@ -139,7 +140,7 @@ size_t pt2q_gram_flags_ints(int m);
 int pt2q_launch_gram16(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);
 size_t pt2q_gram16_flags_ints(int m);
 int pt2q_launch_gram16_batched(const void* const* X, int dtype, long N, int m, long ldx, float* G, long gstride,
-                               int batch, hipStream_t st);
+                               int batch, hipStream_t st, bool upper = false);
 
 // ---- misc (misc.hip)
 int pt2q_launch_transpose_to_f32(const void* src, int dtype, long lds, int rows, int cols,

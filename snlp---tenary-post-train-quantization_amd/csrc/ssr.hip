@@ -1046,6 +1046,116 @@ __global__ __launch_bounds__(64) void s1_ring_kernel(const float* G, long ldg, i
   if (r0 + lane < m) S1[r0 + lane] = s;
 }
 
+// S1 of UPPER-only Grams (G[r][c] stored for c >= r only: pt2q_gram_batched_upper): row j's chain
+// takes G[l][j] for l < j and G[j][l] for l >= j, l ascending -- on a Gram whose mirror is an
+// exact copy these are s1_ring_kernel's values in s1_ring_kernel's order, so S1 is bit-identical.
+// A one-wave workgroup owns rows j0 .. j0 + 63 (lane: row j = j0 + lane) and streams 8 KiB tiles
+// through the same four-stage LDS-DMA ring:
+//  * column tiles t < nA = j0 / 32: G rows l = 32 t .. 32 t + 31, columns j0 .. j0 + 63 (natural
+//    layout, 256 B per row; 16 lanes x 16 B per row in a DMA): lane j reads its column, l < j;
+//  * row tiles u = t - nA: rows j0 .. j0 + 63, columns j0 + 32 u .. + 31 (s1_ring_kernel's
+//    swizzled layout): lane j reads its own row, l >= j -- except in the two diagonal tiles
+//    (u = 0, 1), where l < j reads element (l, j) of the tile holding column j (both resident).
+__global__ __launch_bounds__(64) void s1_upper_ring_kernel(const float* G, long ldg, int m, float* S1, long sG,
+                                                           long sS) {
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[S1R_STAGES * S1R_WSTAGE];
+  typedef __attribute__((address_space(3))) void* lptr;
+  const int lane = threadIdx.x & 63;
+  G += blockIdx.y * sG;
+  S1 += blockIdx.y * sS;
+  const int j0 = blockIdx.x * S1R_WROWS;
+  const int j = j0 + lane;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)ring;
+  const int nA = j0 / S1R_COLS, nC = (m - j0 + S1R_COLS - 1) / S1R_COLS, ntile = nA + nC;
+  auto issue = [&](int t) {
+    uint8_t* stg = ring + (t % S1R_STAGES) * S1R_WSTAGE;
+    if (t < nA) {  // rows 32 t + 4 q + lane / 16, 16-byte chunk lane % 16 of columns j0 ..
+      const int col = j0 + 4 * (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int row = S1R_COLS * t + 4 * q + (lane >> 4);
+        __builtin_amdgcn_global_load_lds(G + (long)row * ldg + (col < m ? col : 0), (lptr)(stg + q * 1024), 16, 0, 0);
+      }
+    } else {  // s1_ring_kernel's row tile at columns c0
+      const int c0 = j0 + S1R_COLS * (t - nA);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 8 * q + (lane >> 3);
+        const int row = j0 + rr < m ? j0 + rr : 0;
+        const int col = c0 + 4 * ((lane & 7) ^ ((rr >> 1) & 7));
+        __builtin_amdgcn_global_load_lds(G + (long)row * ldg + (col < m ? col : 0), (lptr)(stg + q * 1024), 16, 0,
+                                         0);
+      }
+    }
+  };
+  const int pre = ntile < S1R_STAGES - 1 ? ntile : S1R_STAGES - 1;
+  for (int t = 0; t < pre; ++t) issue(t);
+  const int f = (lane >> 1) & 7;
+  float s = 0.0f;
+  for (int t = 0; t < ntile; ++t) {
+    if (t + S1R_STAGES - 1 < ntile) issue(t + S1R_STAGES - 1);
+    // this tile landed -- and at the first diagonal tile the second one too
+    const int need = (t == nA && nC > 1) ? t + 1 : t;
+    const int ahead = ntile - 1 - need;
+    s1r_vmcnt(ahead < S1R_STAGES - 1 - (need - t) ? ahead : S1R_STAGES - 1 - (need - t));
+    const uint32_t st0 = lds0 + (t % S1R_STAGES) * S1R_WSTAGE;
+    if (t < nA) {  // column tile: l = 32 t + r < j0 <= j
+      float x[S1R_COLS];
+#pragma unroll
+      for (int r = 0; r < S1R_COLS; ++r)
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(x[r]) : "v"(st0 + 4 * lane), "i"(256 * r));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < S1R_COLS; ++r) s = s + x[r];
+      continue;
+    }
+    const int u = t - nA;
+    const int c0 = j0 + S1R_COLS * u;
+    if (u >= 2) {  // own row only (l >= j0 + 64 > j)
+      s1f4 x[8];
+      const uint32_t base = st0 + lane * 128;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(x[k]) : "v"(base + ((k ^ f) << 4)));
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                   :: "memory");
+      if (c0 + S1R_COLS <= m) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s = s + x[k][q];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (c0 + 4 * k < m)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s = s + x[k][q];
+      }
+      continue;
+    }
+    // diagonal tile u (l = c0 + c): l < j -> element (l, j) of the tile holding column j; else
+    // element (j, l) of this tile (own row)
+    const int uj = lane >> 5, cj = lane & 31;  // column j's tile (0 / 1) and column in it
+    const uint32_t colj = lds0 + ((nA + uj) % S1R_STAGES) * S1R_WSTAGE + (uint32_t)((cj & 3) << 2);
+    float x[S1R_COLS];
+#pragma unroll
+    for (int c = 0; c < S1R_COLS; ++c) {
+      const int l = c0 + c, rr = l - j0;  // row of the diagonal block
+      const uint32_t a_col = colj + rr * 128 + ((((cj >> 2) ^ ((rr >> 1) & 7))) << 4);
+      const uint32_t a_row = st0 + lane * 128 + ((((c >> 2) ^ f)) << 4) + ((c & 3) << 2);
+      asm volatile("ds_read_b32 %0, %1" : "=v"(x[c]) : "v"(l < j ? a_col : a_row));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < S1R_COLS; ++c)
+      if (c0 + c < m) s = s + x[c];
+  }
+  if (j < m) S1[j] = s;
+}
+
 // d = sequential sum of S1 (j ascending); S1 is staged through LDS in chunks so the serial
 // chain never waits on a global load.
 __global__ __launch_bounds__(256) void s1_total_kernel(const float* S1, int b, float* d, long sS, long sD) {
@@ -1209,7 +1319,18 @@ int pt2q_launch_aga_s1(int src, const float* A, long lda, const int* blk, int b,
 // S1d[z * (m + 1) + j] = S1[j] of item z, S1d[z * (m + 1) + m] = its d.  Same kernels and order as
 // pt2q_launch_aga_s1 (src 1, no block indices), so every value is bit-identical to the per-item
 // call; the batch fills the chip where one item's serial d chain ran on one workgroup.
-int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st) {
+int pt2q_launch_s1_batched(const float* G, long ldg, int m, int batch, long sG, float* S1d, hipStream_t st,
+                           bool upper) {
+  if (upper) {  // upper-only Grams: the ring kernel's DMA conditions are required
+    if (m <= 512 || m % 4 || ldg % 4 || sG % 4 || ((uintptr_t)G & 15)) return PT2Q_E_UNSUPPORTED;
+    const long sS = m + 1;
+    hipLaunchKernelGGL(s1_upper_ring_kernel, dim3(ceil_div(m, S1R_WROWS), batch), dim3(64), 0, st, G, ldg, m, S1d,
+                       sG, sS);
+    PT2Q_LAUNCH_CHECK();
+    hipLaunchKernelGGL(s1_total_kernel, dim3(batch), dim3(256), 0, st, S1d, m, S1d + m, sS, sS);
+    PT2Q_LAUNCH_CHECK();
+    return PT2Q_OK;
+  }
   if (m <= 128) {
     for (int z = 0; z < batch; ++z) {
       const int rc = pt2q_launch_aga_s1(1, G + z * sG, ldg, nullptr, m, S1d + (long)z * (m + 1),

@@ -79,11 +79,13 @@ def gram_batched_supported(X: torch.Tensor) -> bool:
             and X.data_ptr() % 16 == 0 and m % 8 == 0)
 
 
-def gram_batched(Xs, G: torch.Tensor) -> torch.Tensor:
+def gram_batched(Xs, G: torch.Tensor, upper_only: bool = False) -> torch.Tensor:
     """G[z] = Xs[z]ᵀ Xs[z] for every item (main.py:128 per unit) in data-parallel launches of up to
     GRAM_BATCH_MAX items (pt2q_gram_batched): G is a contiguous fp32 (batch, m, m) tensor, the Xs
     fp16 / bf16 (m % 256 == 0) or fp32 (N, m) of one shape.  Each G[z] is bit-identical to
-    gram(Xs[z])."""
+    gram(Xs[z]).  upper_only (16-bit Xs): only the upper triangle (c >= r) is written, the rest of
+    G is left as it was (pt2q_gram_batched_upper; for Grams that feed only S1 / d,
+    s1_from_gram_batched(upper_only=True))."""
     Xs = [X.reshape(-1, X.shape[-1]) for X in Xs]
     N, m = Xs[0].shape
     if G.shape != (len(Xs), m, m) or G.dtype != torch.float32 or not G.is_contiguous():
@@ -94,8 +96,9 @@ def gram_batched(Xs, G: torch.Tensor) -> torch.Tensor:
     for z0 in range(0, len(Xs), GRAM_BATCH_MAX):
         chunk = Xs[z0:z0 + GRAM_BATCH_MAX]
         arr, keep = _lib.ptr_array(chunk)
-        _lib.check(_lib.lib().pt2q_gram_batched(len(chunk), arr, _lib.dtype_code(chunk[0]), N, m, m,
-                                                _lib.ptr(G[z0]), _lib.stream_of(G.device)), "pt2q_gram_batched")
+        fn = _lib.lib().pt2q_gram_batched_upper if upper_only else _lib.lib().pt2q_gram_batched
+        _lib.check(fn(len(chunk), arr, _lib.dtype_code(chunk[0]), N, m, m, _lib.ptr(G[z0]), _lib.stream_of(G.device)),
+                   "pt2q_gram_batched" + ("_upper" if upper_only else ""))
     return G
 
 
@@ -196,10 +199,12 @@ def quantize_blocks(W: torch.Tensor, A: Optional[torch.Tensor], Hinv: Optional[t
     return LayerOutput(alpha, mu, T, perm, iters)
 
 
-def s1_from_gram_batched(G: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def s1_from_gram_batched(G: torch.Tensor, out: Optional[torch.Tensor] = None, upper_only: bool = False) -> torch.Tensor:
     """S1 = S·1 and d = 1ᵀS1 (quantizer.py:215-218) of every m x m raw Gram in G (batch, m, m) in
     one launch pair: row z of the (batch, m + 1) result is S1 then d of item z, bit-identical to
-    pt2q_s1_from_gram per item (quantize_blocks(..., s1d=row) consumes it)."""
+    pt2q_s1_from_gram per item (quantize_blocks(..., s1d=row) consumes it).  upper_only: read only
+    the upper triangle (c >= r) of each Gram -- gram_batched(upper_only=True)'s output -- with the
+    same bits (pt2q_s1_from_upper_batched; m > 512, m % 4 == 0)."""
     _lib.require_device(G)
     if G.dim() != 3 or G.shape[1] != G.shape[2] or G.dtype != torch.float32 or not G.is_contiguous():
         raise ValueError("s1_from_gram_batched: G must be a contiguous fp32 (batch, m, m) device tensor")
@@ -209,9 +214,9 @@ def s1_from_gram_batched(G: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     elif (out.shape != (b, m + 1) or out.dtype != torch.float32 or not out.is_contiguous()
           or out.device != G.device):
         raise ValueError("s1_from_gram_batched: out must be a contiguous fp32 (batch, m + 1) tensor on G's device")
-    _lib.check(_lib.lib().pt2q_s1_from_gram_batched(_lib.ptr(G), G.stride(1), m, b, G.stride(0) if b > 1 else m * m,
-                                                    _lib.ptr(out), _lib.stream_of(G.device)),
-               "pt2q_s1_from_gram_batched")
+    fn = _lib.lib().pt2q_s1_from_upper_batched if upper_only else _lib.lib().pt2q_s1_from_gram_batched
+    _lib.check(fn(_lib.ptr(G), G.stride(1), m, b, G.stride(0) if b > 1 else m * m, _lib.ptr(out),
+                  _lib.stream_of(G.device)), "pt2q_s1_from_" + ("upper" if upper_only else "gram") + "_batched")
     return out
 
 

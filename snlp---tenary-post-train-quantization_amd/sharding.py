@@ -96,12 +96,13 @@ def model_units(model: str, layers: Optional[int] = None, tokens: Optional[int] 
 # per-channel units, S1 / d -- then the grouped block loops on the lanes), phase by phase, with the
 # fixed latencies that do NOT shrink with a shard written out.  Constants fitted (round 6) to the
 # phase walls of the whole 7B / 13B steps and of their 8-rank shards timed alone on one MI355X
-# (bench.py --gpus 8 --shard all; profiles/r06a_shards_c4.json, and r06e_shards_c5.json after the
-# S1 ring kernel): the model reproduces all four within 6 % (C4 2236 vs 2232 ms, its shards 302 vs
-# 298-306 ms; C5 112 vs 112 ms, its shards 15.6 vs 14.9-15.5 ms).
+# (bench.py --gpus 8 --shard all; profiles/r06a_shards_c4.json, and r06i_shards_c5.json after the
+# S1 ring kernel and the upper-only per-channel Grams): the model reproduces all four within 6 %
+# (C4 2236 vs 2232 ms, its shards 302 vs 298-306 ms; C5 105 vs 105 ms, its shards 14.6-15.4 ms).
 #   Gram: the batched 16-bit Gram runs 256 x 256 tiles in waves of one tile per CU; a wave costs
 #     N * 2 * 256^2 / GRAM_TILE_RATE (a CU's MFMA rate under the power limit) + GRAM_TILE_FIXED
-#     (the tile's ramp and its 512 KiB mirrored epilogue: 54 us, which dominates at N = 4096).
+#     (the tile's ramp and its 512 KiB mirrored epilogue: 54 us, which dominates at N = 4096; 36 us
+#     for a per-channel unit's upper-only Gram, pt2q_gram_batched_upper).
 #   Inverse: per chunk of <= 32 items, m / 64 serial panel steps of INV_STEP each, plus the
 #     trailing updates at INV_RATE m^3 per second.
 #   S1 / d (per-channel units): S1_FIXED + the Grams' bytes at S1_BW.
@@ -111,7 +112,7 @@ def model_units(model: str, layers: Optional[int] = None, tokens: Optional[int] 
 #     slowest wave).
 SHARD_MODEL = dict(
     cus=256,
-    gram_tile_rate=4.887e12, gram_tile_fixed=5.43e-5, gram_batch=128,
+    gram_tile_rate=4.887e12, gram_tile_fixed=5.43e-5, gram_tile_fixed_upper=3.6e-5, gram_batch=128,
     inv_step=4.53e-5, inv_rate=1.134e14, chunk=32,
     s1_fixed=5.4e-4, s1_bw=6.48e12,
     loop_nr=4.056e-12, loop_block=8.53e-5, loop_pc=3.28e-12, loop_pc_group=9.0e-4,
@@ -146,7 +147,8 @@ def unit_cost(unit, block_size: int = 128) -> float:
     c = SHARD_MODEL
     _, linears, N = unit
     m = linears[0][2]
-    t = _gram_tiles(m) * (float(N) * 2 * 256 * 256 / c["gram_tile_rate"] + c["gram_tile_fixed"]) / c["cus"]
+    fixed = c["gram_tile_fixed_upper"] if block_size >= m else c["gram_tile_fixed"]
+    t = _gram_tiles(m) * (float(N) * 2 * 256 * 256 / c["gram_tile_rate"] + fixed) / c["cus"]
     if block_size < m:
         t += float(m) ** 3 / c["inv_rate"] + (m / 64.0) * c["inv_step"] / c["chunk"]
     else:
@@ -176,7 +178,8 @@ def shard_phases(units, block_size: int = 128, io_bytes: int = 2, model=None):
         for z0 in range(0, cnt, c["gram_batch"]):
             k = min(c["gram_batch"], cnt - z0)
             waves = -(-k * _gram_tiles(m) // c["cus"])
-            gram += waves * (f32 * N * 2 * 256 * 256 / c["gram_tile_rate"] + c["gram_tile_fixed"])
+            fixed = c["gram_tile_fixed_upper"] if block_size >= m and io_bytes == 2 else c["gram_tile_fixed"]
+            gram += waves * (f32 * N * 2 * 256 * 256 / c["gram_tile_rate"] + fixed)
     inv, s1_bytes = 0.0, 0.0
     for (m, N), cnt in by_w.items():
         if block_size >= m:
@@ -550,7 +553,7 @@ class GramsFirst:
                                   if inv else None,
                                   "S1d": torch.empty((c, m + 1), dtype=torch.float32, device=self.dev)
                                   if s1 else None,
-                                  "info": torch.zeros(c, dtype=torch.int32, device=self.dev)}
+                                  "info": torch.zeros(c, dtype=torch.int32, device=self.dev), "upper": False}
         for g in [g for g in self.groups if g not in count]:
             del self.groups[g]
         self.G = {}
@@ -589,8 +592,14 @@ class GramsFirst:
             grp = self.groups[g]
             if [z for z, _ in items] == list(range(grp["G"].shape[0])) and \
                     len({(X.shape, X.dtype) for _, X in items}) == 1:
-                self.engine.gram_batched([X for _, X in items], grp["G"])
+                # a per-channel group's Grams feed only S1 / d: their upper triangles suffice
+                # (pt2q_gram_batched_upper; inverses() then reads them with s1 upper_only)
+                X0 = items[0][1]
+                grp["upper"] = (grp.get("S1d") is not None and X0.dtype in (torch.float16, torch.bfloat16)
+                                and X0.shape[1] % 4 == 0)
+                self.engine.gram_batched([X for _, X in items], grp["G"], upper_only=grp["upper"])
             else:
+                grp["upper"] = False
                 m = grp["G"].shape[1]
                 if m not in self.ws:
                     self.ws[m] = self.lib.workspace(self.lib.lib().pt2q_gram_workspace_bytes(m), self.dev)
@@ -616,18 +625,18 @@ class GramsFirst:
             for k, g in enumerate(s1g):
                 grp = self.groups[g]
                 if k == 0:
-                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
+                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"], upper_only=grp.get("upper", False))
                     continue
                 st = self._s1_streams[k - 1]
                 st.wait_stream(caller)
                 with torch.cuda.stream(st):
-                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
+                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"], upper_only=grp.get("upper", False))
             for st in self._s1_streams[:len(s1g) - 1]:
                 caller.wait_stream(st)
         else:
             for g in s1g:
                 grp = self.groups[g]
-                self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"])
+                self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"], upper_only=grp.get("upper", False))
         self.inv_done = {}
         live = [g for g in sorted(self.groups) if self.groups[g]["Hinv"] is not None]
         if self.inv_stream is None and self.inv_streams > 1 and self.dev.type == "cuda":

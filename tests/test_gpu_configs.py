@@ -305,3 +305,34 @@ def test_perchannel_group_of_sixteen_vs_oracle(pt2q):
         np.testing.assert_array_equal(host(outs[z].T.float()), ref["T"].astype(np.float32))
         assert bits_equal(host(outs[z].alpha), ref["alpha"]) and bits_equal(host(outs[z].mu), ref["mu"])
         np.testing.assert_array_equal(host(outs[z].iters), ref["iters"])
+
+
+@pytest.mark.parametrize("m,batch", [(5120, 2), (13824, 1), (1000, 2), (548, 1), (544, 1), (576, 3), (4104, 1)])
+def test_s1_from_upper_equals_full(pt2q, m, batch):
+    """pt2q_s1_from_upper_batched reads only the upper triangle (the lower one is NaN here) and
+    gives S1 / d bit-identical to pt2q_s1_from_gram_batched on the full symmetric Gram: column
+    tiles above the diagonal block, the two diagonal tiles (mixed), row tiles after it, ragged
+    last blocks (548: a 36-row last block, 544: one diagonal tile)."""
+    eng = pt2q.engine
+    Gs = torch.stack([pt2q.gram(pt2q.fill_synthetic((384, m), 61 + z, std=1.0, outliers=True).half())
+                      for z in range(batch)]).contiguous()
+    want = eng.s1_from_gram_batched(Gs)
+    low = torch.tril(torch.ones(m, m, dtype=torch.bool, device=DEV), diagonal=-1)
+    Gu = Gs.masked_fill(low, float("nan"))
+    got = eng.s1_from_gram_batched(Gu, upper_only=True)
+    assert bits_equal(host(got), host(want))
+
+
+@pytest.mark.parametrize("m,dt", [(5120, torch.bfloat16), (768, torch.float16)])
+def test_gram_batched_upper(pt2q, m, dt):
+    """pt2q_gram_batched_upper: the upper triangle (diagonal included) equals the full batched
+    Gram's bit for bit, the strictly lower part is left untouched."""
+    eng = pt2q.engine
+    Xs = [pt2q.fill_synthetic((1024, m), 71 + z, std=1.0, outliers=True).to(dt) for z in range(3)]
+    full = torch.empty((3, m, m), device=DEV)
+    eng.gram_batched(Xs, full)
+    up = torch.full((3, m, m), 7.0, device=DEV)
+    eng.gram_batched(Xs, up, upper_only=True)
+    upper = torch.triu(torch.ones(m, m, dtype=torch.bool, device=DEV))
+    assert bits_equal(host(up[:, upper]), host(full[:, upper]))
+    assert bool((up[:, ~upper] == 7.0).all())
