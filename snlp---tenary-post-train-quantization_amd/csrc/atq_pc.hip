@@ -80,6 +80,8 @@ struct PcArgs {
   long ldt;
   int* iters;        // atomicMax of the wave iteration counts
   int* counters;     // [0] rows whose init codes are all zero
+  int probe;         // development knock-outs (PT2Q_ATQ_PROBE, DEV_PROBES builds; results garbage):
+                     // 1 = no code stores, 2 = AGA with S1 = 1 (no S1 loads), 4 = ITF skipped
 };
 
 __host__ __device__ inline size_t pc_wave_bytes(int stage, int nchunks) { return 2 * (size_t)stage + (size_t)nchunks * 64 * 8; }
@@ -338,6 +340,27 @@ struct PcAgaOut {
       if (TAIL && j >= jn) continue;
       const uint32_t bit = 1u << (PC_J - 1 - j);
       const float t = (mk.x & bit) ? ((mk.y & bit) ? -1.0f : 1.0f) : 0.0f;
+#ifdef PT2Q_DEV_PROBES
+      if (A.probe & 2) {
+        const float w = x[j], cv = 1.0f;
+        pv = fmaf(t, cv, pv);
+        pws = fmaf(w, cv, pws);
+        pwts = fmaf(w * t, cv, pwts);
+        pt2s = fmaf(t * t, cv, pt2s);
+        if (R.valid && !(A.probe & 1)) trow[16 * j] = (TO)t;
+        continue;
+      }
+      if (A.probe & 1) {
+        if (s1) {
+          const float w = x[j], cv = s1[16 * j];
+          pv = fmaf(t, cv, pv);
+          pws = fmaf(w, cv, pws);
+          pwts = fmaf(w * t, cv, pwts);
+          pt2s = fmaf(t * t, cv, pt2s);
+        }
+        continue;
+      }
+#endif
       if (s1) {
         const float w = x[j], cv = s1[16 * j];
         pv = fmaf(t, cv, pv);
@@ -373,6 +396,9 @@ PT2Q_DEV void pc_rows(R& rows) {
   // iterative_ternary_fitting (quantizer.py:136-175), wave-level stop (atq.hip wide_itf)
   int it = 0;
   bool any = true;
+#ifdef PT2Q_DEV_PROBES
+  if (A.probe & 4) any = false;
+#endif
   for (; it < A.max_iter; ++it) {
     if (!any) break;
     {
@@ -505,7 +531,8 @@ int pt2q_launch_atq_pc_group(int count, const PcLinear* lin, int wdtype, int m, 
   int wg = 0;
   for (int z = 0; z < count; ++z) {
     const PcLinear& L = lin[z];
-    G.a[z] = PcArgs{L.W, L.ldw, L.n, m, L.S1, L.d, max_iter, L.alpha, L.mu, L.T, L.ldt, L.iters, L.counters};
+    G.a[z] = PcArgs{L.W, L.ldw, L.n, m, L.S1, L.d, max_iter, L.alpha, L.mu, L.T, L.ldt, L.iters, L.counters,
+                    pt2q_tuning().atq_probe};
     G.wg0[z] = wg;
     wg += ceil_div(L.n, rows_wg);
   }

@@ -893,7 +893,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[mt][nt][q] = 0.0f;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counts its own DMAs
+    // No wait for the previous tile's stores: they overlap this tile's first DMAs.  The chain's
+    // hand-counted waits stay exact bounds -- a wait for at most K outstanding operations with the
+    // stores older than every DMA still means the oldest DMAs (loads complete in order) landed; it
+    // may only wait longer.  (A vmcnt(0) here held every tile's ramp behind its predecessor's 256-512
+    // KiB of stores: most of the ~40-54 us fixed cost per tile that dominates at N = 4096.)
     gw_chain<GW_B, BF16>(acc, b.X[z], b.ldx, b.M, i0, j0, 0, b.K, true, smem);
     // upper tile and its mirror, as gram16w_kernel's final store
     const bool diag = ti == tj;

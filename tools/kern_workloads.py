@@ -1,5 +1,5 @@
 """PMC workloads (dev tool):
-python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT | pc N M COUNT} [reps]
+python tools/kern_workloads.py {inverse M BATCH | group N M COUNT | grams N M COUNT | pc N M COUNT | pcg M COUNT} [reps]
 inverse: engine.hessian_inverse_batched on BATCH synthetic Grams of order M (N = 262144 scale);
 group:   pt2q_quantize_blocks_group of COUNT fp16 N x M linears (SSR, variant M);
 pc:      per-channel block loops (block_size = M, config C5) of COUNT bf16 N x M linears;
@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import pt2q_loader
 pt2q = pt2q_loader.load()
 kind = sys.argv[1]
-reps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+reps = int(sys.argv[5]) if len(sys.argv) > 5 and sys.argv[1] != "pcg" else (int(sys.argv[4]) if sys.argv[1] == "pcg" and len(sys.argv) > 4 else 3)
 if kind == "inverse":
     m, batch = int(sys.argv[2]), int(sys.argv[3])
     X = pt2q.fill_synthetic((4 * m, m), 77, outliers=True).half()
@@ -32,6 +32,16 @@ elif kind == "grams":
         pt2q.engine.gram_batched([Xs[z % nd] for z in range(count)], G)
     torch.cuda.synchronize()
     print("grams done", float(G[0, 0, 0]))
+elif kind == "pcg":  # grouped per-channel rows (C5's q/k/v/o and gate/up row counts): pcg M COUNT
+    m, count = int(sys.argv[2]), int(sys.argv[3])
+    X = pt2q.fill_synthetic((4096, m), 78, outliers=True).bfloat16()
+    G = pt2q.gram(X)
+    S1d = pt2q.engine.s1_from_gram_batched(G.unsqueeze(0).contiguous())[0]
+    Ws = [pt2q.fill_synthetic((5120 if z % 3 else 13824, m), 900 + z, std=0.02).bfloat16() for z in range(count)]
+    for _ in range(reps):
+        outs = pt2q.engine.quantize_perchannel_group(Ws, [S1d] * count)
+    torch.cuda.synchronize()
+    print("pcg done", int(outs[0].iters[0]))
 elif kind == "pc":
     n, m, count = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     X = pt2q.fill_synthetic((4096, m), 78, outliers=True).bfloat16()
