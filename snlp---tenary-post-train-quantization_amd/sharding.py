@@ -516,7 +516,8 @@ class GramsFirst:
         self.scratch = {}
         self.ows = {}        # per-lane workspaces of the per-linear ("one") block loops
         self.stall = torch.zeros(1, dtype=torch.int32, device=self.dev)
-        self._s1_streams = []  # per-channel S1 / d of the second, third, ... width
+        self._s1_streams = []  # per-channel S1 / d, one stream per width (inverses())
+        self.s1_done = {}      # per-channel group -> event: its S1 / d formed
 
     @property
     def percdamp(self):
@@ -535,6 +536,8 @@ class GramsFirst:
         reused while the step's shape does not change."""
         count = {}
         self.slot = {}
+        if self.dev.type == "cuda":
+            self.join_side()  # a previous step's S1 / d still reading the buffers reused below
         for key, m, N in units:
             g = (m, int(N))
             self.slot[key] = (g, count.get(g, 0))
@@ -615,24 +618,24 @@ class GramsFirst:
         if not self.batched:
             return
         caller = torch.cuda.current_stream(self.dev)
-        # per-channel groups: S1 / d once per Gram; the widths' launch pairs run side by side (one
-        # stream each, joined back into the caller's): each pair ends in serial d chains and a
-        # partial last wave, which a shard's few items no longer hide (bit-identical either way)
+        # per-channel groups: S1 / d once per Gram, each width's launch pair on a side stream of its
+        # own with an event (s1_done): a lane's per-channel block loops wait for their width's S1 /
+        # d only (_wait_inverse), so the narrow widths' loops start while a wider width's S1 runs --
+        # each pair ends in serial d chains and a partial last wave.  Bit-identical either way.
         s1g = [g for g in sorted(self.groups) if self.groups[g].get("S1d") is not None]
-        if len(s1g) > 1 and self.dev.type == "cuda":
-            while len(self._s1_streams) < len(s1g) - 1:
+        self.s1_done = {}
+        if s1g and self.dev.type == "cuda":
+            while len(self._s1_streams) < len(s1g):
                 self._s1_streams.append(torch.cuda.Stream(self.dev))
             for k, g in enumerate(s1g):
                 grp = self.groups[g]
-                if k == 0:
-                    self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"], upper_only=grp.get("upper", False))
-                    continue
-                st = self._s1_streams[k - 1]
-                st.wait_stream(caller)
+                st = self._s1_streams[k]
+                st.wait_stream(caller)  # the Grams
                 with torch.cuda.stream(st):
                     self.engine.s1_from_gram_batched(grp["G"], out=grp["S1d"], upper_only=grp.get("upper", False))
-            for st in self._s1_streams[:len(s1g) - 1]:
-                caller.wait_stream(st)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.s1_done[g] = ev
         else:
             for g in s1g:
                 grp = self.groups[g]
@@ -680,11 +683,18 @@ class GramsFirst:
                 self.inv_done[g] = ev
 
     def _wait_inverse(self, stream, key):
-        """`stream` waits for the inverses of `key`'s group (batched schedule)."""
+        """`stream` waits for the inverses -- or the per-channel S1 / d -- of `key`'s group."""
         if self.batched and key in self.slot:
-            ev = self.inv_done.get(self.slot[key][0])
-            if ev is not None:
-                stream.wait_event(ev)
+            g = self.slot[key][0]
+            for ev in (self.inv_done.get(g), self.s1_done.get(g)):
+                if ev is not None:
+                    stream.wait_event(ev)
+
+    def join_side(self):
+        """The caller's stream waits for the side streams (per-channel S1 / d)."""
+        caller = torch.cuda.current_stream(self.dev)
+        for st in self._s1_streams:
+            caller.wait_stream(st)
 
     def tail(self, key, Ws, nsamples):
         if key in self.slot:
@@ -787,7 +797,7 @@ class GramsFirst:
                 state.statuses.append(lib.status_view(ws).clone())
                 for (run, k, _, _, _), out in zip(chunk, outs):
                     run.outs[k] = out
-        state.join = lambda: [caller.wait_stream(x) for x in [ln.stream for ln in lanes] +
+        state.join = lambda: [caller.wait_stream(x) for x in [ln.stream for ln in lanes] + self._s1_streams +
                               ([self.inv_stream] if self.inv_stream is not None else [])]
         return runs
 
