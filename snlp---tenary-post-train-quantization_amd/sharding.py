@@ -114,7 +114,7 @@ SHARD_MODEL = dict(
     cus=256,
     gram_tile_rate=4.887e12, gram_tile_fixed=5.43e-5, gram_tile_fixed_upper=3.6e-5, gram_batch=128,
     inv_step=4.53e-5, inv_rate=1.134e14, chunk=32,
-    s1_fixed=5.4e-4, s1_bw=6.48e12,
+    s1_fixed=5.4e-4, s1_bw=7.2e12,
     loop_nr=4.056e-12, loop_block=8.53e-5, loop_pc=3.28e-12, loop_pc_group=9.0e-4,
     lanes=3, group=16, pc_group=16,
 )
