@@ -138,6 +138,7 @@ struct Pt2qTuning {
   bool sim_split = true;       // PT2Q_SIM_SPLIT=0: one wave per column for n > 4096 (256 VGPRs)
   int gemmx_stages = 2;        // PT2Q_GEMMX_STAGES: LDS stages of the f32 chain GEMM (2: 64 KiB, 2 WGs per CU;
                                // batched inverse 596 -> 534 ms per 7B step vs 3)
+  bool gemmx_gram = true;      // PT2Q_GEMMX_GRAM=0: batched f32 Grams on the generic GEMM
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
   bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM
   int ef_v2 = 1;               // PT2Q_EF_V2: 1 = ef2_gemm_kernel (two workgroups per CU, default), 0 = ef_gemm_kernel

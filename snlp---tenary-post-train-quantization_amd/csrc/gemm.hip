@@ -882,6 +882,11 @@ int pt2q_launch_gemm(const GemmDesc& g, hipStream_t st) {
 int pt2q_launch_gram_f32_batched(const float* const* X, long N, int m, long ldx, float* G, long gstride, int batch,
                                  hipStream_t st) {
   if (batch <= 0 || batch > GF_MAX || m <= 0 || N < 0 || N > INT_MAX || ldx < m || !G) return PT2Q_E_ARG;
+  // the LDS-DMA kernel where the operands allow it (aligned rows)
+  if (pt2q_tuning().gemmx_gram) {
+    const int rc = pt2q_launch_gemmx_gram(X, N, m, ldx, G, gstride, batch, st);
+    if (rc != PT2Q_E_UNSUPPORTED) return rc;
+  }
   GemmDesc g{};
   g.M = m; g.N = m; g.K = (int)N;
   g.lda = ldx; g.a_layout = LAY_KMAJOR;

@@ -224,11 +224,11 @@ struct XArgs {
   int order;  // 0 row-major tiles, 1 upper (XCD super-tiles), 2 upper by columns (lauum)
 };
 
+// One workgroup's tile of item blockIdx.y: operands Ab / Bb, output Cz (the item's bases).
 template <int NS, int KR>
-__global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
+PT2Q_DEV void gemmx_tile(const XArgs& X, const float* Ab, const float* Bb, float* const Cz, uint8_t* smem) {
   using GE = XGeo<KR>;
   constexpr int XSTG = GE::STG, XPANEL = GE::PANEL, XDMA = GE::DMA, XK = KR;
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * XSTG];
   const GemmDesc& g = X.g;
   int ti, tj;
   const int bid = blockIdx.x;
@@ -249,10 +249,6 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
   const int kbeg = g.kstart_diag == 2 ? j0 : (g.kstart_diag == 1 ? i0 : 0);
   const int kend = g.K;
   const int nst = kend > kbeg ? (kend - kbeg + XK - 1) / XK : 0;
-  const long zo = (long)blockIdx.y * g.bstride;  // batch item (grid.y)
-  const float* Ab = (const float*)g.A + zo;
-  const float* Bb = (const float*)g.B + zo;
-  float* const Cz = g.C + zo;
   // the C tile (chain modes) is loaded first, so that waiting for it does not wait for the DMA
   // prologue issued after it; accumulators: lane <-> C row, register groups of 4 <-> 4
   // consecutive C columns
@@ -356,7 +352,56 @@ __global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
     }
 }
 
+template <int NS, int KR>
+__global__ __launch_bounds__(256) void gemmx_kernel(XArgs X) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * XGeo<KR>::STG];
+  const long zo = (long)blockIdx.y * X.g.bstride;  // batch item (grid.y)
+  gemmx_tile<NS, KR>(X, (const float*)X.g.A + zo, (const float*)X.g.B + zo, X.g.C + zo, smem);
+}
+
+// Symmetric Grams G[z] = X[z]ᵀX[z] of a batch with their own activation pointers: X[z] (N x m,
+// row-major) is the K-major operand on both sides (A(i, k) = X[z][k][i]).
+struct XPtrs {
+  const float* X[PT2Q_GX_PTRS];
+};
+
+template <int NS, int KR>
+__global__ __launch_bounds__(256) void gemmx_gram_kernel(XArgs X, XPtrs P) {
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * XGeo<KR>::STG];
+  const float* Xz = P.X[blockIdx.y];
+  gemmx_tile<NS, KR>(X, Xz, Xz, X.g.C + (long)blockIdx.y * X.g.bstride, smem);
+}
+
 }  // namespace
+
+// A batch of f32 Grams (STORE, upper tiles mirrored) on the LDS-DMA kernel: every element is the
+// k-ascending chain over the N rows from 0, as the generic kernels form it (bit-identical).
+// E_UNSUPPORTED unless every X[z] is 16-byte aligned and ldx, m are multiples of 4.
+int pt2q_launch_gemmx_gram(const float* const* X, long N, int m, long ldx, float* G, long gstride, int batch,
+                           hipStream_t st) {
+  if (batch <= 0 || batch > PT2Q_GX_PTRS || m <= 0 || N < 0 || N > INT_MAX || ldx < m || !G) return PT2Q_E_ARG;
+  auto al = [](const void* p) { return (uintptr_t)p % 16 == 0; };
+  if (m % 4 || ldx % 4 || !al(G) || gstride % 4 || (long)m * m > gstride) return PT2Q_E_UNSUPPORTED;
+  XPtrs P{};
+  for (int z = 0; z < batch; ++z) {
+    if (!X[z] && N > 0) return PT2Q_E_ARG;
+    if (!al(X[z])) return PT2Q_E_UNSUPPORTED;
+    P.X[z] = X[z] ? X[z] : (const float*)G;  // N = 0: never read
+  }
+  GemmDesc g{};
+  g.M = m; g.N = m; g.K = (int)N;
+  g.lda = ldx; g.a_layout = LAY_KMAJOR;
+  g.ldb = ldx; g.b_layout = LAY_KMAJOR;
+  g.in_dtype = PT2Q_F32;
+  g.C = G; g.ldc = m;
+  g.mode = GEMM_STORE; g.upper = 1; g.mirror = 1;
+  g.batch = batch; g.bstride = gstride;
+  XArgs A{g, ceil_div(m, XT), ceil_div(m, XT), 1};
+  const dim3 grid((unsigned)((long)A.tiles_n * (A.tiles_n + 1) / 2), (unsigned)batch);
+  hipLaunchKernelGGL((gemmx_gram_kernel<2, 32>), grid, dim3(256), 0, st, A, P);
+  PT2Q_LAUNCH_CHECK();
+  return PT2Q_OK;
+}
 
 // E_UNSUPPORTED unless: f32, both operands K-major, no output-row gather, mode STORE / CHAIN_NEG /
 // CHAIN_POS, 16-byte aligned operands and C with leading dimensions and M, N multiples of 4.

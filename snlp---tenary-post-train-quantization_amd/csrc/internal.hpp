@@ -132,6 +132,10 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
 // f32 chain GEMM with K-major operands, LDS-DMA staged (gemmx.hip); E_UNSUPPORTED if the desc
 // does not fit it (then use pt2q_launch_gemm)
 int pt2q_launch_gemmx(const GemmDesc& g, hipStream_t st);
+// a batch of f32 Grams with their own activation pointers on the same kernel (gemmx.hip)
+constexpr int PT2Q_GX_PTRS = 128;
+int pt2q_launch_gemmx_gram(const float* const* X, long N, int m, long ldx, float* G, long gstride, int batch,
+                           hipStream_t st);
 // symmetric Gram (STORE/ADD); flags (nullable): pt2q_gram_flags_ints(m) ints of scratch
 // status (nullable): the caller's status word for stall reports (else a word of the flag area)
 int pt2q_launch_gram(const GemmDesc& g, int* flags, hipStream_t st, int* status = nullptr);

@@ -681,14 +681,16 @@ def test_blocks_group_vs_oracle_at_mlp_shapes(pt2q, n, m):
                                           (11008, 1024, 2, torch.float16), (8192, 256, 3, torch.bfloat16),
                                           (13824, 128, 2, torch.float16), (768, 2048, 5, torch.float32),
                                           (3072, 512, 3, torch.float32), (1000, 300, 4, torch.float32),
-                                          (200, 64, 130, torch.float32)])
+                                          (200, 64, 130, torch.float32), (514, 100, 3, torch.float32),
+                                          (3072, 2048, 12, torch.float32)])
 def test_gram_batched_equals_per_item(pt2q, m, N, batch, dt):
     """pt2q_gram_batched (one data-parallel launch for every item, 256 x 256 tiles, each tile one
     chain over all rows) == pt2q_gram on each item alone, bit for bit; ragged N, chains of 2 / 6 /
     130 stages (prologue only, steady + draining ring), m = 11008, bf16, and more items than one
     launch takes (130 > 128).  m = 8192 / 11008 / 13824 run the searched tile orders
     (gram_order.inc: every item's whole runs, then every item's partial-run tiles); fp32 items
-    (GPT-2 widths, a ragged m, 130 items) take the batched f32 chain GEMM."""
+    (GPT-2 widths at C2's 2048 rows, a ragged m, 130 items) take the LDS-DMA f32 chain GEMM
+    (gemmx_gram_kernel), m % 4 != 0 (514) the generic batched f32 GEMM."""
     Xs = [pt2q.fill_synthetic((N, m), 40 + z, outliers=True, device="cuda").to(dt) for z in range(batch)]
     G = torch.empty((batch, m, m), dtype=torch.float32, device="cuda")
     pt2q.engine.gram_batched(Xs, G)
