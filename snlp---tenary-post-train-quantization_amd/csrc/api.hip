@@ -46,6 +46,7 @@ Pt2qTuning load_tuning() {
   getb("PT2Q_EF_WBAR", t.ef_wbar);
   geti("PT2Q_GEMMX_STAGES", t.gemmx_stages);
   getb("PT2Q_GEMMX_GRAM", t.gemmx_gram);
+  getb("PT2Q_CHOL_LANE", t.chol_lane);
   getb("PT2Q_S1_IN_ATQ", t.s1_in_atq);
   getb("PT2Q_EF_GEMM", t.ef_kernel);
   geti("PT2Q_WIDE_WAVES", t.wide_waves);

@@ -201,6 +201,85 @@ __global__ __launch_bounds__(256) void chol_panel_trtri_kernel(float* U, long ld
     trtri_inblock(Ui, ld, p0, nb, blockIdx.x - npanel, Dus, dg, x);
 }
 
+// The same block step with one lane per panel column / inverse row (whole 64-row blocks only):
+// the lane keeps all 64 chains in registers, so it needs no broadcast and no padded zero terms.
+// The factored diagonal block is staged in LDS once per workgroup; every lane of a wave reads the
+// same U[k][j] (ds_read_b128 broadcasts, four entries per read).  Each chain takes exactly the
+// terms of the kernel above in the same order (that kernel's extra terms are zero factors, exact
+// no-ops), so the bits are equal.  Packed FMAs update two chains per instruction.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#include "chol_lane.inc"  // lane_stream_panel / lane_stream_inverse (tools/gen_chol_lane.py)
+
+PT2Q_DEV void lane_stage_block(float (*Ds)[NB], const float* U, long ld, int p0) {
+  const float* D = U + (long)p0 * ld + p0;
+#pragma unroll
+  for (int u = 0; u < NB * NB / 4 / 256; ++u) {
+    const int q = (int)threadIdx.x + 256 * u, r = q / (NB / 4), c4 = q % (NB / 4);
+    *(float4*)&Ds[r][4 * c4] = *(const float4*)(D + (long)r * ld + 4 * c4);
+  }
+}
+
+PT2Q_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// panel column i = p0 + NB + t
+PT2Q_DEV void lane_panel(float* U, long ld, int p0, int m, int t, float (*Ds)[NB]) {
+  const int i = p0 + NB + t;
+  const bool valid = i < m;
+  const float* col = U + (long)p0 * ld + (valid ? i : p0);
+  f32x2 xp[NB / 2];
+#pragma unroll
+  for (int r = 0; r < NB / 2; ++r) xp[r] = f32x2{col[(long)(2 * r) * ld], col[(long)(2 * r + 1) * ld]};
+  lane_stage_block(Ds, U, ld, p0);  // (the chains' loads in flight meanwhile)
+  __syncthreads();
+  lane_stream_panel(xp, lds_addr(&Ds[0][0]));
+  if (!valid) return;
+#pragma unroll
+  for (int r = 0; r < NB / 2; ++r) {
+    U[(long)(p0 + 2 * r) * ld + i] = xp[r].x;
+    U[(long)(p0 + 2 * r + 1) * ld + i] = xp[r].y;
+  }
+}
+
+// inverse row k: UiT[p0 + q][k] = Uinv[k][p0 + q], earlier blocks' chains for k < p0, zero otherwise
+PT2Q_DEV void lane_inverse(const float* U, float* Ui, long ld, int p0, int k, float (*Ds)[NB]) {
+  const bool prior = k < p0;
+  const float* row = Ui + (long)p0 * ld + (prior ? k : 0);
+  f32x2 xp[NB / 2];
+#pragma unroll
+  for (int q = 0; q < NB / 2; ++q) {
+    const float a = row[(long)(2 * q) * ld], b = row[(long)(2 * q + 1) * ld];  // branch-free loads
+    xp[q] = prior ? f32x2{a, b} : f32x2{0.0f, 0.0f};
+  }
+  lane_stage_block(Ds, U, ld, p0);
+  __syncthreads();
+  const int kl = k - p0;  // the row's own diagonal step (none for k < p0)
+  lane_stream_inverse(xp, lds_addr(&Ds[0][0]), kl);
+  if (k >= p0 + NB) return;
+  const int jb = kl > 0 ? kl : 0;
+#pragma unroll
+  for (int q = 0; q < NB / 2; ++q) {
+    Ui[(long)(p0 + 2 * q) * ld + k] = (2 * q >= jb) ? xp[q].x : 0.0f;  // UiT[p0+q][k]
+    Ui[(long)(p0 + 2 * q + 1) * ld + k] = (2 * q + 1 >= jb) ? xp[q].y : 0.0f;
+  }
+}
+
+// 256-thread workgroups: [0, npanel) one panel column per lane (columns p0 + NB + ...), the rest
+// one row k < p0 + NB of the inverse per lane.
+__global__ __launch_bounds__(256) void chol_panel_trtri_lane_kernel(float* U, long ld, int p0, int m, float* Ui,
+                                                                    int npanel, long bst) {
+  __shared__ __attribute__((aligned(16))) float Ds[NB][NB];
+  U += (long)blockIdx.y * bst;  // batch item (grid.y)
+  Ui += (long)blockIdx.y * bst;
+  if ((int)blockIdx.x < npanel)
+    lane_panel(U, ld, p0, m, (int)blockIdx.x * 256 + (int)threadIdx.x, Ds);
+  else
+    lane_inverse(U, Ui, ld, p0, ((int)blockIdx.x - npanel) * 256 + (int)threadIdx.x, Ds);
+}
+
 __global__ void copy_upper_kernel(const float* H, long ldh, float* A, long lda, int m, long bst) {
   H += (long)blockIdx.y * bst;  // batch item (grid.y)
   A += (long)blockIdx.y * bst;
@@ -309,6 +388,7 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
     PT2Q_LAUNCH_CHECK();
   }
   int rc;
+  const Pt2qTuning& tu = pt2q_tuning();
   // panel solve + in-block inverse of the block at p0 (its diagonal factor done: `factored`)
   auto factor = [&](int p0, int nb, bool factored) -> int {
     if (!factored) {
@@ -316,6 +396,14 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
       PT2Q_LAUNCH_CHECK();
     }
     const int rest = m - p0 - nb;
+    if (nb == NB && tu.chol_lane) {  // whole blocks: one lane per column / row
+      const int npanel = rest > 0 ? (int)ceil_div((long)rest, 256) : 0;
+      const int ninv = (int)ceil_div((long)(p0 + nb), 256);
+      hipLaunchKernelGGL(chol_panel_trtri_lane_kernel, dim3(npanel + ninv, batch), dim3(256), 0, st, U, ld, p0, m,
+                         Ui, npanel, bst);
+      PT2Q_LAUNCH_CHECK();
+      return PT2Q_OK;
+    }
     const int npanel = rest > 0 ? (int)ceil_div((long)rest * LPR, 256) : 0;
     const int ninv = (int)ceil_div((long)(p0 + nb) * LPR, 256);
     hipLaunchKernelGGL(chol_panel_trtri_kernel, dim3(npanel + ninv, batch), dim3(256), 0, st, U, ld, p0, nb,
@@ -328,7 +416,6 @@ int pt2q_launch_cholesky_inverse(const float* H, long ldh, int m, float* Hinv, l
   // columns of the inverse get the block's terms by rank-64 strip updates, whose first tile is
   // the next diagonal block, factored in the same launch); after the panel, its rank-CP terms
   // (gemmx) as described above.  Every chain takes its terms in ascending k.
-  const Pt2qTuning& tu = pt2q_tuning();
   const int tp = tu.chol_panel;
   // look-ahead from m > 6144 (measured: 4096 3.07 -> 3.24 ms with it, 11008 19.7 -> 18.6 ms with
   // it and 512-row panels); panel rows (a multiple of NB): 512, or 1024 for a large m alone

@@ -138,6 +138,7 @@ struct Pt2qTuning {
   bool sim_split = true;       // PT2Q_SIM_SPLIT=0: one wave per column for n > 4096 (256 VGPRs)
   int gemmx_stages = 2;        // PT2Q_GEMMX_STAGES: LDS stages of the f32 chain GEMM (2: 64 KiB, 2 WGs per CU;
                                // batched inverse 596 -> 534 ms per 7B step vs 3)
+  bool chol_lane = true;       // PT2Q_CHOL_LANE=0: the four-lanes-per-column panel / in-block inverse
   bool gemmx_gram = true;      // PT2Q_GEMMX_GRAM=0: batched f32 Grams on the generic GEMM
   bool s1_in_atq = true;       // PT2Q_S1_IN_ATQ=0: S1/d in the top-k launch
   bool ef_kernel = true;       // PT2Q_EF_GEMM=0: error feedback through the generic GEMM

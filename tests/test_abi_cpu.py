@@ -183,3 +183,29 @@ def test_gram_order_tables_cover_every_tile_once():
         panels = sum(len({p for t in tiles[r:r + 32] for p in t}) for r in range(0, nt, 32))
         assert panels == claimed[T][0] < claimed[T][1], T
     assert len(tab) == offs[-1] + Ts[-1] * (Ts[-1] + 1) // 2
+
+
+def test_chol_lane_stream_keeps_chain_order():
+    """csrc/chol_lane.inc (tools/gen_chol_lane.py): the committed stream is the generator's output,
+    and replaying its items symbolically, every chain receives the terms of rows 0, 1, 2, ... in
+    ascending order and row R's value is used only once chain R has all its terms and its
+    division -- the PT2Q chain order, so the one-lane kernel's bits are the oracle's."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_chol_lane", os.path.join(ROOT, "tools", "gen_chol_lane.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    src = open(gen.OUT).read()
+    assert gen.gen(False) in src and gen.gen(True) in src
+    NB = gen.NB
+    terms = [[] for _ in range(NB)]  # rows applied to each chain, in order
+    final = set()
+    for R, c, diag in gen.stream():
+        if diag:
+            assert terms[R] == list(range(R)), R  # chain R complete before its division
+            final.add(R)
+        assert R in final
+        for j in range(4 * c, 4 * c + 4):
+            if j > R:
+                terms[j].append(R)
+    assert all(terms[j] == list(range(j)) for j in range(NB))
+    assert final == set(range(NB))
