@@ -13,7 +13,7 @@ bench._load_runtime(False)
 bench.resolve(a)
 torch, sharding = bench.torch, bench.sharding
 dev = torch.device("cuda", 0)
-io = torch.float16
+io = {"fp16": torch.float16, "fp32": torch.float32, "bf16": torch.bfloat16}[a.io_dtype]
 work = bench.ModelStep(a, 0, 1, dev, io)
 gf = work.gf
 units = work.units
