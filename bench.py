@@ -160,7 +160,8 @@ def describe_units(units, layers):
 
 
 def config_runs(a, dev):
-    """extra.configs: one short grams-first run (2 warmup + 3 timed steps, same flags) of every
+    """extra.configs: one short grams-first run (2 warmup + 3 timed steps -- up to 20 for a step
+    under 0.1 s -- same flags) of every
     other BASELINE config's model workload on this GPU (C2 gpt2, C3 opt-1.3b, C5 llama-2-13b, or
     C4 when another model is the headline).  Two warmup steps: the second step of a fresh
     workload can still grow the caching allocator's pools (a C5 step once took 991 ms instead of
@@ -176,8 +177,12 @@ def config_runs(a, dev):
             tw = time.perf_counter()
             w = ModelStep(b, 0, 1, dev, io)
             for _ in range(b.warmup):
+                tws = time.perf_counter()
                 w.step()
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
+            # a short step (C2: ~16 ms) is timed over more steps (about 0.3 s, at most 20): the same
+            # work per step, less noise in the mean
+            b.steps = max(b.steps, min(20, int(0.3 / max(time.perf_counter() - tws, 1e-3))))
             t0 = time.perf_counter()
             step_ms = []
             for _ in range(b.steps):
