@@ -159,6 +159,23 @@ def describe_units(units, layers):
             f"shared-input units")
 
 
+class no_gc:
+    """Timed loops run with Python's cyclic garbage collector off (collected just before, as
+    timeit does): a collection landing inside a 16 ms step (C2) once took 68 ms and moved the
+    mean 20 %.  The GPU work is unchanged; the collector runs again right after the loop."""
+
+    def __enter__(self):
+        gc.collect()
+        self.was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
+
+
 def config_runs(a, dev):
     """extra.configs: one short grams-first run (2 warmup + 3 timed steps -- up to 20 for a step
     under 0.1 s -- same flags) of every
@@ -183,14 +200,15 @@ def config_runs(a, dev):
             # a short step (C2: ~16 ms) is timed over more steps (about 0.3 s, at most 20): the same
             # work per step, less noise in the mean
             b.steps = max(b.steps, min(20, int(0.3 / max(time.perf_counter() - tws, 1e-3))))
-            t0 = time.perf_counter()
-            step_ms = []
-            for _ in range(b.steps):
-                ts = time.perf_counter()
-                w.step()
-                torch.cuda.synchronize()
-                step_ms.append(1e3 * (time.perf_counter() - ts))
-            s = (time.perf_counter() - t0) / b.steps
+            with no_gc():
+                t0 = time.perf_counter()
+                step_ms = []
+                for _ in range(b.steps):
+                    ts = time.perf_counter()
+                    w.step()
+                    torch.cuda.synchronize()
+                    step_ms.append(1e3 * (time.perf_counter() - ts))
+                s = (time.perf_counter() - t0) / b.steps
             log(0, f"config {name}: setup + warmup {t0 - tw:.1f}s, steps {[round(x, 1) for x in step_ms]} ms")
             cols = sharding.units_cols(w.units)
             # live roofline of this config: phase walls + one-lane stage busy times (outside the timing)
@@ -242,11 +260,12 @@ def shard_runs(a, dev, io, world, ranks=None, t1_ms=None, t1_phase=None, steps=3
             w.step()
         torch.cuda.synchronize()
         step_ms = []
-        for _ in range(steps):
-            ts = time.perf_counter()
-            w.step()
-            torch.cuda.synchronize()
-            step_ms.append(1e3 * (time.perf_counter() - ts))
+        with no_gc():
+            for _ in range(steps):
+                ts = time.perf_counter()
+                w.step()
+                torch.cuda.synchronize()
+                step_ms.append(1e3 * (time.perf_counter() - ts))
         ph = w.phase_step() if w.gf is not None and a.schedule == "grams-first" else None
         units = [w.units[i] for i in w.mine]
         rec = {"rank": r, "units": len(units), "linears": sum(len(u[1]) for u in units),
@@ -1143,6 +1162,7 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     sync()
+    gcoff = no_gc().__enter__()
     t0 = time.perf_counter()
     step_ms = []
     for i in range(a.steps):
@@ -1154,6 +1174,7 @@ def main(argv=None):
             log(rank, f"step {i + 1}/{a.steps}")
     sync()
     t_rank = time.perf_counter() - t0
+    gcoff.__exit__(None, None, None)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
