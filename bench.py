@@ -99,9 +99,9 @@ def parse(argv=None):
     p.add_argument("--inv-streams", type=int, default=1,
                    help="model workload, grams-first: streams the batched inverse chunks spread over "
                         "(sharding.GramsFirst inv_streams)")
-    p.add_argument("--inv-chunk", type=str, default="32",
-                   help="model workload, grams-first: items per batched-inverse launch sequence, N or "
-                        "m:N,m:N (sharding.GramsFirst chunk)")
+    p.add_argument("--inv-chunk", type=str, default="auto",
+                   help="model workload, grams-first: items per batched-inverse launch sequence, auto, N "
+                        "or m:N,m:N (sharding.GramsFirst chunk)")
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
@@ -127,7 +127,10 @@ def parse(argv=None):
 
 
 def parse_chunk(v):
-    """--inv-chunk: "32" -> 32; "11008:16,4096:32" -> {11008: 16, 4096: 32}."""
+    """--inv-chunk: "auto" -> None (GramsFirst: 32, or one chunk for a small batch); "32" -> 32;
+    "11008:16,4096:32" -> {11008: 16, 4096: 32}."""
+    if v == "auto":
+        return None
     if ":" not in v:
         return int(v)
     return {int(k): int(c) for k, c in (x.split(":") for x in v.split(","))}

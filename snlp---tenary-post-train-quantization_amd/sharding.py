@@ -483,14 +483,15 @@ class GramsFirst:
     The damping is the pipeline's (pipe.percdamp) everywhere: batched inverses, the per-lane
     inverses of batched=False and the pinv fallback, so no path damps differently."""
 
-    def __init__(self, pipe, device, batched: bool = True, chunk: int = 32, group: int = 16,
+    def __init__(self, pipe, device, batched: bool = True, chunk=None, group: int = 16,
                  overlap: bool = False, batch_grams: bool = True, inv_streams: int = 1):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         # step 1 batched: the Grams of each (m, N) group in data-parallel launches
         # (pt2q_gram_batched) instead of one stream-K launch per unit
         self.batch_grams, self.pending = batch_grams, {}
-        # chunk: items per batched-inverse launch sequence, an int or {m: items} (others: 32)
+        # chunk: items per batched-inverse launch sequence, an int or {m: items} (others: 32), or
+        # None: 32, or the whole batch when small (_chunk)
         self.batched, self.chunk = batched, chunk
         # step 3 grouped: the block loops of up to `group` same-shape linears (across units) per
         # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
@@ -523,10 +524,22 @@ class GramsFirst:
     def percdamp(self):
         return self.pipe.percdamp
 
-    def _chunk(self, m: int) -> int:
+    # a width whose whole batch of H copies fits in this many bytes is factorised as ONE chunk:
+    # each chunk walks the full m / 64-step panel chain, so a short remainder chunk (GPT-2's 36
+    # m = 768 items: 32 + 4) costs a second chain for little work
+    ONE_CHUNK_BYTES = 1 << 30
+
+    def _chunk(self, m: int, count: int = 0) -> int:
+        """Items per batched-inverse launch sequence: chunk as given (int or {m: items}), or with
+        chunk=None ("auto") 32 -- the whole batch as one chunk when its H copies fit
+        ONE_CHUNK_BYTES."""
         if isinstance(self.chunk, dict):
             return int(self.chunk.get(m, 32))
-        return int(self.chunk)
+        if self.chunk is not None:
+            return int(self.chunk)
+        if count > 32 and count * m * m * 4 <= self.ONE_CHUNK_BYTES:
+            return count
+        return 32
 
     def needs_inverse(self, m: int) -> bool:
         return self.engine.needs_inverse(m, self.pipe.bs)
@@ -646,7 +659,7 @@ class GramsFirst:
             jobs = []
             for g in live:
                 c = self.groups[g]["G"].shape[0]
-                ch = self._chunk(g[0])
+                ch = self._chunk(g[0], c)
                 jobs += [(float(g[0]) ** 3 * min(ch, c - z0), g, z0, min(ch, c - z0)) for z0 in range(0, c, ch)]
             jobs.sort(key=lambda j: (-j[0], j[1], j[2]))
             while len(self._istreams) < min(self.inv_streams, len(jobs)):
@@ -670,14 +683,16 @@ class GramsFirst:
             for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
-                                                    info=grp["info"], scratch=self.scratch, chunk=self._chunk(g[0]))
+                                                    info=grp["info"], scratch=self.scratch,
+                                                    chunk=self._chunk(g[0], grp["G"].shape[0]))
             return
         self.inv_stream.wait_stream(caller)  # the Grams
         with torch.cuda.stream(self.inv_stream):
             for g in live:
                 grp = self.groups[g]
                 self.engine.hessian_inverse_batched(grp["G"], g[1], self.percdamp, Hinv=grp["Hinv"],
-                                                    info=grp["info"], scratch=self.scratch, chunk=self._chunk(g[0]))
+                                                    info=grp["info"], scratch=self.scratch,
+                                                    chunk=self._chunk(g[0], grp["G"].shape[0]))
                 ev = torch.cuda.Event()
                 ev.record(self.inv_stream)
                 self.inv_done[g] = ev
