@@ -527,7 +527,7 @@ class GramsFirst:
     # a width whose whole batch of H copies fits in this many bytes is factorised as ONE chunk:
     # each chunk walks the full m / 64-step panel chain, so a short remainder chunk (GPT-2's 36
     # m = 768 items: 32 + 4) costs a second chain for little work
-    ONE_CHUNK_BYTES = 1 << 30
+    ONE_CHUNK_BYTES = 4 << 30
 
     def _chunk(self, m: int, count: int = 0) -> int:
         """Items per batched-inverse launch sequence: chunk as given (int or {m: items}), or with
