@@ -1165,19 +1165,18 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     sync()
-    gcoff = no_gc().__enter__()
-    t0 = time.perf_counter()
-    step_ms = []
-    for i in range(a.steps):
-        ts = time.perf_counter()
-        work.step()
-        sync()  # per-step wall (box-to-box and step-to-step spread); the step ends in host reads anyway
-        step_ms.append(1e3 * (time.perf_counter() - ts))
-        if a.steps > 3:
-            log(rank, f"step {i + 1}/{a.steps}")
-    sync()
-    t_rank = time.perf_counter() - t0
-    gcoff.__exit__(None, None, None)
+    with no_gc():
+        t0 = time.perf_counter()
+        step_ms = []
+        for i in range(a.steps):
+            ts = time.perf_counter()
+            work.step()
+            sync()  # per-step wall (box-to-box and step-to-step spread); the step ends in host reads anyway
+            step_ms.append(1e3 * (time.perf_counter() - ts))
+            if a.steps > 3:
+                log(rank, f"step {i + 1}/{a.steps}")
+        sync()
+        t_rank = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
