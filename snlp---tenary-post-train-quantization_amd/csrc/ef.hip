@@ -789,6 +789,8 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
   const int tstride = (int)gridDim.x * TEAMS;
   int t = (int)blockIdx.x * TEAMS + team;
   if (t >= total) return;  // (a terminated wave leaves every later s_barrier of its workgroup)
+  a0.probe |= PT2Q_EF2_KPROBE;
+  PT2Q_EF2_CLK(0);
   auto corner = [&](int t, EfArgs& a, int& e0, int& i0) {
     const int z = t / a0.ntile, tl = t - z * a0.ntile;
     a = ef_linear(a0, z);
@@ -902,6 +904,7 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
     wrow[0] = nrow[0];
     wrow[1] = nrow[1];
   }
+  PT2Q_EF2_CLK(1);
 }
 
 }  // namespace

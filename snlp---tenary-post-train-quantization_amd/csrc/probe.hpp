@@ -41,3 +41,22 @@ __device__ long long ef_clk[64][8][2];
 #else
 #define PT2Q_EF_STAMP(tile, i)
 #endif
+
+#if (PT2Q_PROBE & 64) != 0
+// ef2_gemm_kernel: thread 0 of each workgroup, s_memtime (shader clock) and s_memrealtime
+// (100 MHz) at the kernel's start (i = 0) and end (i = 1): the clock the launch ran at
+__device__ long long ef2_clk[1024][4];
+#define PT2Q_EF2_CLK(i)                                                  \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {                           \
+    ef2_clk[blockIdx.x][2 * (i)] = __builtin_amdgcn_s_memtime();         \
+    ef2_clk[blockIdx.x][2 * (i) + 1] = __builtin_amdgcn_s_memrealtime(); \
+  }
+#else
+#define PT2Q_EF2_CLK(i)
+#endif
+
+// ef2_gemm_kernel's runtime knock-out mask, fixed at build time by a probe tool (tools/ef_probe.hip:
+// -DPT2Q_EF2_KPROBE=1 no Wt traffic, 2 operand DMAs from one chunk, 4 no MFMAs; results garbage)
+#ifndef PT2Q_EF2_KPROBE
+#define PT2Q_EF2_KPROBE 0
+#endif

@@ -53,55 +53,23 @@ int main(int argc, char** argv) {
   const double us = 1000.0 * ms / reps;
   const double fl = 2.0 * n * nr * bs;
   const long tiles = (long)((nr + 127) / 128) * ((n + 127) / 128);
-  printf("ef probe %d n=%d nr=%d bs=%d part=%d: %.1f us  %.1f TFLOP/s  Wt RMW %.0f GB/s  %.2f us/tile/CU\n",
-         PT2Q_PROBE, n, nr, bs, (int)part, us, fl / us / 1e6, 2.0 * n * nr * 4 / us / 1e3, us * 256 / tiles);
+  printf("ef probe %d/%d n=%d nr=%d bs=%d part=%d: %.1f us  %.1f TFLOP/s  Wt RMW %.0f GB/s  %.2f us/tile/CU\n",
+         PT2Q_PROBE, PT2Q_EF2_KPROBE, n, nr, bs, (int)part, us, fl / us / 1e6, 2.0 * n * nr * 4 / us / 1e3, us * 256 / tiles);
 #if (PT2Q_PROBE & 64) != 0
-  // phase durations (s_memrealtime ticks, 100 MHz -> us) of tiles 1..6 of the first 64 workgroups
-  // (the stamps of the last launch): 0 top, 1 stage 0 landed, 2 barrier, 3 half 0 done,
-  // 4 stage 1 landed, 5 barrier, 6 half 1 done, 7 old values landed
-  static long long st[64][8][12];
-  (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(ef_stamps), sizeof(st));
-  const char* nm[8] = {"wait stage0", "barrier0", "half0", "wait stage1", "barrier1", "half1", "wait old Wt", "epilogue+loop"};
-  {  // the mid-tile gap (3 -> 4) in pieces: lgkmcnt + barrier, next stage-0 DMA issue, w-bar store, vmcnt
-    double g[4] = {0};
-    int c2 = 0;
-    for (int w = 0; w < 64; ++w)
-      for (int t = 1; t < 7; ++t) {
-        if (!st[w][t][3] || !st[w][t][8]) continue;
-        g[0] += (double)(st[w][t][8] - st[w][t][3]);
-        g[1] += (double)(st[w][t][9] - st[w][t][8]);
-        g[2] += (double)(st[w][t][10] - st[w][t][9]);
-        g[3] += (double)(st[w][t][4] - st[w][t][10]);
-        ++c2;
-      }
-    if (c2)
-      printf("  mid-tile: barrier %.2f us, stage-0 DMA issue %.2f us, w-bar store %.2f us, stage-1 wait %.2f us\n",
-             g[0] / c2 / 100.0, g[1] / c2 / 100.0, g[2] / c2 / 100.0, g[3] / c2 / 100.0);
-  }
-  double sum[8] = {0};
-  int cnt = 0;
-  for (int w = 0; w < 64; ++w)
-    for (int t = 1; t < 7; ++t) {
-      if (!st[w][t][0] || !st[w][t + 1][0]) continue;
-      for (int i = 0; i < 7; ++i) sum[i] += (double)(st[w][t][i + 1] - st[w][t][i]);
-      sum[7] += (double)(st[w][t + 1][0] - st[w][t][7]);
-      ++cnt;
-    }
-  double tot = 0;
-  for (int i = 0; i < 8; ++i) tot += sum[i];
-  for (int i = 0; i < 8; ++i)
-    printf("  %-14s %7.2f us  %5.1f %%\n", nm[i], cnt ? sum[i] / cnt / 100.0 : 0.0, tot > 0 ? 100.0 * sum[i] / tot : 0.0);
-  printf("  tile           %7.2f us  (%d samples)\n", cnt ? tot / cnt / 100.0 : 0.0, cnt);
-  static long long ck[64][8][2];
-  (void)hipMemcpyFromSymbol(ck, HIP_SYMBOL(ef_clk), sizeof(ck));
+  // ef2_gemm_kernel's clock over the last launch: sum over workgroups of the s_memtime cycles
+  // divided by the s_memrealtime ticks (100 MHz)
+  static long long ck[1024][4];
+  (void)hipMemcpyFromSymbol(ck, HIP_SYMBOL(ef2_clk), sizeof(ck));
   double cyc = 0, rt = 0;
-  for (int w = 0; w < 64; ++w)
-    for (int t = 1; t < 7; ++t)
-      if (st[w][t][0] && st[w][t][7]) {
-        cyc += (double)(ck[w][t][1] - ck[w][t][0]);
-        rt += (double)(st[w][t][7] - st[w][t][0]);
-      }
-  printf("  clock          %7.2f GHz (s_memtime / s_memrealtime over the tiles)\n", rt > 0 ? cyc / rt * 0.1 : 0.0);
+  int wgs = 0;
+  for (int w = 0; w < 1024; ++w)
+    if (ck[w][1] && ck[w][3] > ck[w][1]) {
+      cyc += (double)(ck[w][2] - ck[w][0]);
+      rt += (double)(ck[w][3] - ck[w][1]);
+      ++wgs;
+    }
+  printf("  kprobe %d: clock %.2f GHz, workgroup %.1f us (%d workgroups)\n", PT2Q_EF2_KPROBE,
+         rt > 0 ? cyc / rt * 0.1 : 0.0, wgs ? rt / wgs / 100.0 : 0.0, wgs);
 #endif
   return 0;
 }
