@@ -833,6 +833,11 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
     uint32_t rb[2];
     ef_rowbase(a, wrow, i0, rb);
     if (a0.probe & 1) rb[0] = rb[1] = EF_DROP;
+    // probe tools only (build-time PT2Q_EF2_KPROBE 8 / 16): the old-value loads / the stores go to
+    // the first rows of Wt (L2-hot) -- same instructions and counts, results garbage
+    uint32_t rbl[2] = {rb[0], rb[1]}, rbs[2] = {rb[0], rb[1]};
+    if (a0.probe & 8) rbl[0] = rbl[1] = 0;
+    if (a0.probe & 16) rbs[0] = rbs[1] = 0;
     ef_rows(an, en, nrow);  // 2 loads, issued by every wave whether or not a next tile exists
     EfAccT<E2_KS> F;
 #pragma unroll
@@ -850,7 +855,7 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
                                  : X[s - 1];
       e2_vmcnt(young);
       asm volatile("s_barrier" ::: "memory");
-      if (s == NST - 1) e2_load<0>(c, rc, rb);  // their latency hides under the last stage
+      if (s == NST - 1) e2_load<0>(c, rc, rbl);  // their latency hides under the last stage
       const int sl = G1L ? (s + par) & 1 : s & 1;
       EfNoIO nio;
       if (!(a0.probe & 4)) F.half(lds0 + sl * E2_STAGE, nio);
@@ -860,7 +865,7 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
       if (s + 2 < NST) {
         X[s] = e2_stage(a, e0, i0, s + 2, slot, slot_lds, vo, true);
       } else if (G1L && s == NST - 2) {
-        e2_g1_dma(rc, rb, slot);  // column group 1's old values into the slot stage 2 freed
+        e2_g1_dma(rc, rbl, slot);  // column group 1's old values into the slot stage 2 freed
         X[s] = EF_CV / 2;
       } else if (G1L) {
         X[s] = more ? e2_stage(an, en, in, 0, slot, slot_lds, vo, newB) : 0;
@@ -873,8 +878,8 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
     }
     e2_vmcnt(X[NST - 1]);  // column group 0's old values landed (G1L: and group 1's, older)
     e2_sub<0>(c, F);
-    if constexpr (!G1L) e2_load<1>(c, rc, rb);  // before group 0's stores: waiting for it then leaves those in flight
-    e2_store<0>(c, rc, rb);
+    if constexpr (!G1L) e2_load<1>(c, rc, rbl);  // before group 0's stores: waiting for it then leaves those in flight
+    e2_store<0>(c, rc, rbs);
     if (P) {  // this tile's w-bar partials (the next block's SSR mean, DESIGN.md §3 CHUNK128)
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // red free (last readers done)
       ef_wbar_span<0, 16>(wrow, c, red);
@@ -889,7 +894,7 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
       e2_vmcnt(EF_CV / 2);  // group 1 landed (younger: group 0's stores)
     }
     e2_sub<1>(c, F);
-    e2_store<1>(c, rc, rb);
+    e2_store<1>(c, rc, rbs);
     if (P) {
       ef_wbar_span<16, 32>(wrow, c, red);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");

@@ -56,7 +56,8 @@ __device__ long long ef2_clk[1024][4];
 #endif
 
 // ef2_gemm_kernel's runtime knock-out mask, fixed at build time by a probe tool (tools/ef_probe.hip:
-// -DPT2Q_EF2_KPROBE=1 no Wt traffic, 2 operand DMAs from one chunk, 4 no MFMAs; results garbage)
+// -DPT2Q_EF2_KPROBE=1 no Wt traffic, 2 operand DMAs from one chunk, 4 no MFMAs, 8 old-value loads
+// from L2-hot rows, 16 stores to them; results garbage)
 #ifndef PT2Q_EF2_KPROBE
 #define PT2Q_EF2_KPROBE 0
 #endif
