@@ -836,8 +836,8 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
     // probe tools only (build-time PT2Q_EF2_KPROBE 8 / 16): the old-value loads / the stores go to
     // the first rows of Wt (L2-hot) -- same instructions and counts, results garbage
     uint32_t rbl[2] = {rb[0], rb[1]}, rbs[2] = {rb[0], rb[1]};
-    if (a0.probe & 8) rbl[0] = rbl[1] = 0;
-    if (a0.probe & 16) rbs[0] = rbs[1] = 0;
+    if constexpr ((PT2Q_EF2_KPROBE & 8) != 0) rbl[0] = rbl[1] = 0;
+    if constexpr ((PT2Q_EF2_KPROBE & 16) != 0) rbs[0] = rbs[1] = 0;
     ef_rows(an, en, nrow);  // 2 loads, issued by every wave whether or not a next tile exists
     EfAccT<E2_KS> F;
 #pragma unroll
