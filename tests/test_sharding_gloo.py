@@ -411,3 +411,19 @@ def test_shard_model_matches_measured_shards(model, bs, prof):
     assert abs(sum(whole.values()) * 1e3 - d["t1_ms"]) <= 0.10 * d["t1_ms"]
     for k, v in d["t1_phase_s"].items():
         assert abs(whole[k] - v) <= 0.10 * v, (k, whole[k], v)
+
+
+def test_grams_first_inverse_chunking_policy():
+    """GramsFirst._chunk: an explicit chunk (int or {m: items}) is used as given; chunk=None
+    (bench --inv-chunk auto) takes 32 items per batched-inverse launch sequence, or the whole
+    batch when its H copies fit ONE_CHUNK_BYTES (GPT-2's 36 m = 768 items: one chunk, not 32 + 4;
+    the 7B's 96 m = 4096 items: 6.4 GB, three chunks).  Chunking never changes a bit
+    (test_hessian_inverse_batched_equals_per_item); this is the schedule only."""
+    import pt2q_loader
+    pt2q_loader.load()
+    from pt2q import sharding as sh
+    auto = sh.GramsFirst(pipe=None, device="cpu")
+    assert auto._chunk(768, 36) == 36 and auto._chunk(3072, 12) == 32 and auto._chunk(2048, 72) == 72
+    assert auto._chunk(4096, 96) == 32 and auto._chunk(11008, 32) == 32 and auto._chunk(768, 0) == 32
+    assert sh.GramsFirst(pipe=None, device="cpu", chunk=16)._chunk(768, 36) == 16
+    assert sh.GramsFirst(pipe=None, device="cpu", chunk={768: 8})._chunk(768, 36) == 8
