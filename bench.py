@@ -102,6 +102,9 @@ def parse(argv=None):
     p.add_argument("--inv-chunk", type=str, default="auto",
                    help="model workload, grams-first: items per batched-inverse launch sequence, auto, N "
                         "or m:N,m:N (sharding.GramsFirst chunk)")
+    p.add_argument("--group-max", action="store_true",
+                   help="model workload, grams-first: shape classes cut into groups of --group linears "
+                        "instead of spread over the lanes (sharding.GramsFirst spread=False)")
     p.add_argument("--group", type=int, default=16,
                    help="model workload, grams-first: same-shape linears per grouped block-loop launch "
                         "sequence (pt2q_quantize_blocks_group; 1 = per-unit loops)")
@@ -621,7 +624,8 @@ class ModelStep:
         self.schedule = a.schedule
         self.gf = (sharding.GramsFirst(self.pipe, dev, batched=not a.no_batched_inverse, group=a.group,
                                        overlap=a.inverse_overlap, batch_grams=not a.no_batched_grams,
-                                       inv_streams=a.inv_streams, chunk=parse_chunk(a.inv_chunk))
+                                       inv_streams=a.inv_streams, chunk=parse_chunk(a.inv_chunk),
+                                       spread=not a.group_max)
                    if self.pipe is not None else None)
         self.X, self.W, self.ws = {}, {}, {}
         self.xi = {}  # unit -> which of this rank's activation tensors of its width it reads

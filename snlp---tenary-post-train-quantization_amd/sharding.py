@@ -484,7 +484,7 @@ class GramsFirst:
     inverses of batched=False and the pinv fallback, so no path damps differently."""
 
     def __init__(self, pipe, device, batched: bool = True, chunk=None, group: int = 16,
-                 overlap: bool = False, batch_grams: bool = True, inv_streams: int = 1):
+                 overlap: bool = False, batch_grams: bool = True, inv_streams: int = 1, spread: bool = True):
         from . import engine, _lib
         self.engine, self.lib, self.pipe, self.dev = engine, _lib, pipe, torch.device(device)
         # step 1 batched: the Grams of each (m, N) group in data-parallel launches
@@ -497,6 +497,12 @@ class GramsFirst:
         # pt2q_quantize_blocks_group launch sequence, groups spread over the pipeline's lanes
         self.group = group if batched else 0
         self.grouped = self.group > 1
+        # spread: a shape class of k linears that fits one group (k <= group) is ONE group -- its
+        # block chain is latency-bound, and one launch sequence over k linears costs little more
+        # than one over k / lanes (GPT-2: 15.9 -> 15.3 ms) -- and a larger class is cut into groups
+        # of ceil(k / lanes) (at most `group`) so every lane gets an even share (C5's 40 down_proj:
+        # 14 / 14 / 12, not 16 / 16 / 8: 107.7 -> 106.0 ms).  False: groups of `group`.
+        self.spread = spread
         self.gws = {}
         # overlap=True: the batched inverses run on a stream of their own, one event per (m, N)
         # group, and a unit's block loops wait only for its own width's inverses, so the narrow
@@ -759,7 +765,8 @@ class GramsFirst:
         plan = []
         for ckey, items in classes.items():
             cap = eng.PC_GROUP_MAX if ckey[0] == "pc" else self.group
-            size = max(1, min(cap, -(-len(items) // len(lanes))))
+            k = len(items)
+            size = max(1, k if k <= cap else (min(cap, -(-k // len(lanes))) if self.spread else cap))
             for c0 in range(0, len(items), size):
                 chunk = items[c0:c0 + size]
                 cost = sum(block_loop_cost(c[2].shape[0], c[2].shape[1], bs) if ckey[0] != "pc"
