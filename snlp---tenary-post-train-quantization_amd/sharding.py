@@ -159,8 +159,8 @@ def unit_cost(unit, block_size: int = 128) -> float:
 
 
 def _groups(count: int, cap: int, lanes: int):
-    """GramsFirst.tails' group sizes for `count` same-class linears."""
-    size = max(1, min(cap, -(-count // lanes)))
+    """GramsFirst.tails' group sizes for `count` same-class linears (spread policy)."""
+    size = max(1, count if count <= cap else min(cap, -(-count // lanes)))
     return [min(size, count - g0) for g0 in range(0, count, size)]
 
 

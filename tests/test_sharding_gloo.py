@@ -390,8 +390,8 @@ def test_grams_first_keeps_an_early_stall():
     gf.check()  # cleared after the read
 
 
-@pytest.mark.parametrize("model,bs,prof", [("llama-2-7b", 128, "r06a_shards_c4.json"),
-                                           ("llama-2-13b", 1 << 14, "r06n_shards_c5.json")])
+@pytest.mark.parametrize("model,bs,prof", [("llama-2-7b", 128, "r06zi_shards_c4.json"),
+                                           ("llama-2-13b", 1 << 14, "r06zi_shards_c5.json")])
 def test_shard_model_matches_measured_shards(model, bs, prof):
     """sharding.shard_cost / shard_phases against the one-GPU shard timings of C4 and C5 committed
     under profiles/ (bench.py --gpus 8 --shard all): every shard's step and the whole step within
