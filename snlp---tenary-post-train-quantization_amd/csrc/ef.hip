@@ -711,13 +711,18 @@ PT2Q_DEV void e2_sub(u32x4 (&c)[EF_CV], const EfAccT<KS>& F) {
     }
 }
 
+// cache policy of the Wt stores (probe builds may set it: 16 = sc1, the line dropped from L2; 2 = nt)
+#ifndef PT2Q_EF2_STORE_AUX
+#define PT2Q_EF2_STORE_AUX 0
+#endif
 template <int RN>
 PT2Q_DEV void e2_store(const u32x4 (&c)[EF_CV], __amdgpu_buffer_rsrc_t rc, const uint32_t (&rb)[2]) {
 #pragma unroll
   for (int rm = 0; rm < 2; ++rm)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(c[(rm * 2 + RN) * 4 + q], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(c[(rm * 2 + RN) * 4 + q], rc, rb[rm] + 4 * (32 * RN + 8 * q), 0,
+                                             PT2Q_EF2_STORE_AUX);
 }
 
 // Column group 1's old values by LDS-DMA (G1L): 8 buffer-to-LDS loads per wave, 16 bytes per lane,
