@@ -92,3 +92,23 @@ def test_shard_mode_line():
     assert d["t1_ms"] > 0 and 0 < d["projected_efficiency"] < 2
     assert set(d["share_ratio"]) == {"gram", "inverse", "tails"}
     assert d["gather_bytes_to_rank0"] == d["shards"][1]["gather_send_bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_two_rank_launch_shared_gpu():
+    """`bench.py --gpus 2 --share-gpu` (TEST ONLY: both ranks on cuda:0, gloo gather -- RCCL refuses
+    two ranks on one device): the launcher starts its own torch.distributed.run child, each rank
+    quantises its LPT shard and rank 0 gathers every linear's device results; the line reports
+    both ranks and the whole job's columns."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu",
+                        "--layers", "2", "--hidden", "512", "--inter", "768", "--tokens", "2048",
+                        "--steps", "1", "--warmup", "1", "--no-extra", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and len(d["ranks"]) == 2
+    assert d["gathered_linears"] == 14 and sum(r["linears"] for r in d["ranks"]) == 14
+    assert d["value"] > 0
