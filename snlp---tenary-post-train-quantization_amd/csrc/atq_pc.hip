@@ -84,7 +84,15 @@ struct PcArgs {
                      // 1 = no code stores, 2 = AGA with S1 = 1 (no S1 loads), 4 = ITF skipped
 };
 
-__host__ __device__ inline size_t pc_wave_bytes(int stage, int nchunks) { return 2 * (size_t)stage + (size_t)nchunks * 64 * 8; }
+// A wave's LDS: ONE ring stage (the streamed kernel), then its code masks.  The stage is
+// wave-private and the LDS unit runs a wave's instructions in order, so the next chunk's stores
+// may follow the current chunk's read-back into the same bytes without a wait (a second stage
+// would only cost LDS: at m = 13824, 22.3 KiB per wave held the kernel to 6 waves per CU; one
+// stage, 18.0 KiB, lets the 8 its registers allow fit).
+constexpr int PC_RING = 1;
+__host__ __device__ inline size_t pc_wave_bytes(int stage, int nchunks) {
+  return PC_RING * (size_t)stage + (size_t)nchunks * 64 * 8;
+}
 
 // One wave's 4 rows, streamed pass by pass.
 template <class TI>
@@ -114,11 +122,11 @@ struct PcRows {
   PT2Q_DEV void store_stage(int st, const u32x4 (&src)[G::PIECES]) {  // registers -> LDS stage st
 #pragma unroll
     for (int p = 0; p < G::PIECES; ++p)
-      *(lds_t<u32x4>*)(ring + st * G::STAGE + (p % 4) * G::ROWB + (p / 4) * 1024 + 16 * lane) = src[p];
+      *(lds_t<u32x4>*)(ring + (st % PC_RING) * G::STAGE + (p % 4) * G::ROWB + (p / 4) * 1024 + 16 * lane) = src[p];
   }
   // this lane's 32 elements of the chunk in stage st (element j = column c*512 + l + 16 j)
   PT2Q_DEV void read_stage(int st, float (&x)[PC_J]) const {
-    const lds_char* b = ring + st * G::STAGE + r * G::ROWB + G::E * l;
+    const lds_char* b = ring + (st % PC_RING) * G::STAGE + r * G::ROWB + G::E * l;
 #pragma unroll
     for (int j = 0; j < PC_J; ++j) {
       uint32_t raw;
@@ -127,7 +135,7 @@ struct PcRows {
       x[j] = PcIn<TI>::cvt(raw);
     }
   }
-  // The stream: at the start of step q, stage q & 1 holds chunk q, register set (q + 1) & 1 chunk
+  // The stream: at the start of step q, the stage holds chunk q, register set (q + 1) & 1 chunk
   // q + 1 and set q & 1 chunk q + 2 (both in flight).  Every pass reads the same chunks in the
   // same order, so the stream wraps from one pass into the next without a cold restart, and each
   // chunk's loads are issued two chunks ahead.
@@ -141,7 +149,8 @@ struct PcRows {
   template <int P>
   PT2Q_DEV void step(float (&x)[PC_J]) {  // P = q & 1 (static: the register sets never move)
     read_stage(P, x);
-    store_stage(P ^ 1, stg[P ^ 1]);  // chunk q + 1 (stage of chunk q - 1: read)
+    asm volatile("" ::: "memory");   // (one stage: the stores below follow the reads in LDS order)
+    store_stage(P ^ 1, stg[P ^ 1]);  // chunk q + 1 (into the bytes just read back)
     load_chunk(c3, stg[P ^ 1]);      // chunk q + 3
     c3 = c3 + 1 == nc ? 0 : c3 + 1;
   }
@@ -481,7 +490,7 @@ __global__ __launch_bounds__(64 * PC_WAVES) void atq_pc_kernel(PcGroup G) {
     R.rowp[q] = (const char*)A.W + (long)iq * A.ldw * G_::E;
   }
   R.ring = (lds_char*)pc_lds + (size_t)wave * pc_wave_bytes(G_::STAGE, nc);
-  R.masks = R.ring + 2 * G_::STAGE;
+  R.masks = R.ring + PC_RING * G_::STAGE;
   R.prime();
   pc_rows<TO>(R);
 }
