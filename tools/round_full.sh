@@ -10,7 +10,8 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?; tail -3 $OUT/gputest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
 tail -1 $OUT/smoke.log
-timeout -k 10 500 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+ts=$(date +%s); timeout -k 10 500 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+echo "bench wall $(( $(date +%s) - ts )) s"
 python3 - $OUT/bench.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
