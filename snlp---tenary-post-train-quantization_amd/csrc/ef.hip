@@ -711,6 +711,12 @@ PT2Q_DEV void e2_sub(u32x4 (&c)[EF_CV], const EfAccT<KS>& F) {
     }
 }
 
+// Column group 0's old Wt values are loaded this many stages before the tile's last (clamped to
+// the first stage): 3 = at the tile's top, under all its MFMAs -- the grouped 16-linear 4096^2 loop
+// 13.26-13.34 -> 12.93-13.03 ms (1 and 2 stages: 13.22-13.26; tools/ef2_g0_lib_ab.sh)
+#ifndef PT2Q_EF2_G0_EARLY
+#define PT2Q_EF2_G0_EARLY 3
+#endif
 // cache policy of the Wt stores (probe builds may set it: 16 = sc1, the line dropped from L2; 2 = nt)
 #ifndef PT2Q_EF2_STORE_AUX
 #define PT2Q_EF2_STORE_AUX 0
@@ -762,7 +768,7 @@ PT2Q_DEV void e2_g1_read(u32x4 (&c)[EF_CV], const uint8_t* slot) {
 // NST = K stages per tile (2: bs <= 64, 4: bs <= 128; stages past bs are zero chunks: no-op pairs).
 // Issue order per tile, for the hand-counted vmcnt waits: [next rows: 2] [stage s + 2 after each
 // compute s (the last two: the next tile's stages 0 and 1)] with [old values, column group 0: 8]
-// just before the last stage's compute; the epilogue then [waits for group 0] [loads group 1: 8]
+// before stage G0S's compute (the tile's first; PT2Q_EF2_G0_EARLY); the epilogue then [waits for group 0] [loads group 1: 8]
 // [stores group 0: 8] [waits for group 1] [stores it: 8] [w-bar partials: P].  So at the next
 // tile's top only that tile's stores (SP) may still be in flight beside its stages.
 // G1L (NST = 4): column group 1's old values come by LDS-DMA (e2_g1_dma) issued after stage 2's
@@ -825,6 +831,7 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
   int SP = 0;
   int par = 0;  // G1L: the slot of this tile's stage 0 (stage s in slot (s + par) & 1)
   static_assert(!G1L || NST == 4, "G1L: four K stages per tile");
+  constexpr int G0S = NST - 1 - PT2Q_EF2_G0_EARLY < 0 ? 0 : NST - 1 - PT2Q_EF2_G0_EARLY;
   for (;;) {
     const int tn = t + tstride;
     const bool more = tn < total;
@@ -855,12 +862,13 @@ __global__ __launch_bounds__(256 * TEAMS) __attribute__((amdgpu_waves_per_eu(2, 
     for (int s = 0; s < NST; ++s) {
       // this stage landed: everything younger than it may still be in flight (G1L: the stage-1
       // DMA of this tile was issued after the previous tile's group-0 stores, not before them)
+      // (group 0's old values issued after stage 0's wait are younger than stage 1's DMAs)
       const int young = s == 0   ? Dn1 + SP + 2
-                        : s == 1 ? (G1L && SP > 0 ? SP - EF_CV / 2 : SP) + 2 + X[0]
+                        : s == 1 ? (G1L && SP > 0 ? SP - EF_CV / 2 : SP) + 2 + (G0S == 0 ? EF_CV / 2 : 0) + X[0]
                                  : X[s - 1];
       e2_vmcnt(young);
       asm volatile("s_barrier" ::: "memory");
-      if (s == NST - 1) e2_load<0>(c, rc, rbl);  // their latency hides under the last stage
+      if (s == G0S) e2_load<0>(c, rc, rbl);  // column group 0's old values (PT2Q_EF2_G0_EARLY)
       const int sl = G1L ? (s + par) & 1 : s & 1;
       EfNoIO nio;
       if (!(a0.probe & 4)) F.half(lds0 + sl * E2_STAGE, nio);
