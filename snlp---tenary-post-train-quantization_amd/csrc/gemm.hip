@@ -776,10 +776,14 @@ PT2Q_DEV void ru_tile(const GemmDesc& g, int tn, int bid, float (*As)[RU_T + 4],
   }
 }
 
+// KQ: operand rows the LDS panels hold (64: every K <= 64 -- the Cholesky's rank-64 strip updates --
+// at 34 KiB per workgroup, four per CU instead of two; 128 otherwise)
+template <int KQ>
 __global__ __launch_bounds__(256) void rank_update2_kernel(GemmDesc g0, int tn0, int n0, GemmDesc g1, int tn1,
                                                            RuDiag diag) {
-  __shared__ __attribute__((aligned(16))) float As[RU_K][RU_T + 4];
-  __shared__ __attribute__((aligned(16))) float Bs[RU_K][RU_T + 4];
+  __shared__ __attribute__((aligned(16))) float As[KQ][RU_T + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[KQ][RU_T + 4];
+  static_assert(KQ * (RU_T + 4) >= RU_T * (RU_T + 1), "the fused diagonal factor's D tile lives in As");
   const int b = blockIdx.x;
   if (b < n0)
     ru_tile(g0, tn0, b, As, Bs, diag);
@@ -835,8 +839,9 @@ int pt2q_launch_gemm2(const GemmDesc& g0, const GemmDesc& g1, hipStream_t st, fl
     const bool fuse = dA && n0 > 0 && g0.C == dA + (long)dp0 * dld + dp0 && g0.ldc == dld &&
                       dnb > 0 && dnb <= RU_T && g0.M >= dnb && g0.N >= dnb;
     RuDiag d{fuse ? dA : nullptr, dld, dp0, dnb, info};
-    hipLaunchKernelGGL(rank_update2_kernel, dim3((unsigned)(n0 + n1), (unsigned)nb), dim3(256), 0, st, g0,
-                       tn0, (int)n0, g1, tn1, d);
+    const bool k64 = (n0 == 0 || g0.K <= 64) && (n1 == 0 || g1.K <= 64);
+    hipLaunchKernelGGL(k64 ? rank_update2_kernel<64> : rank_update2_kernel<RU_K>, dim3((unsigned)(n0 + n1), (unsigned)nb),
+                       dim3(256), 0, st, g0, tn0, (int)n0, g1, tn1, d);
     PT2Q_LAUNCH_CHECK();
     if (fused) *fused = fuse;
     return PT2Q_OK;
