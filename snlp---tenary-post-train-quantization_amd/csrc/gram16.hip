@@ -880,7 +880,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int a = (int)(L - (long)z * b.ntile);
       gx_tile<1>(a, b.T, b.T, b.SJ, ti, tj);
     }
-    const int i0 = ti * GW_B, j0 = tj * GW_B;
+    // upper-only, off the diagonal: the TRANSPOSED tile (rows tj, columns ti), whose mirror
+    // stores -- 16 bytes per lane instead of 4 -- land in the upper triangle.  Its elements have
+    // the bits of the direct tile's: every MFMA group sums exact 16-bit products of the same k
+    // before one rounding, so G[j][i] == G[i][j] bit for bit (test_gram_batched_upper).  C5's
+    // per-channel Grams: 23.7 -> 21.7 ms per width launch (the dword stores' 256 instructions
+    // per wave, against a 63-deep vmcnt, held the next tile's first stage).
+    const bool diag = ti == tj, swap = b.upper && !diag;
+    const int i0 = (swap ? tj : ti) * GW_B, j0 = (swap ? ti : tj) * GW_B;
     float* const C = b.G + (long)z * b.gstride;
     const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wr = wu >> 1, wc = wu & 1;
@@ -899,8 +906,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // may only wait longer.  (A vmcnt(0) here held every tile's ramp behind its predecessor's 256-512
     // KiB of stores: most of the ~40-54 us fixed cost per tile that dominates at N = 4096.)
     gw_chain<GW_B, BF16>(acc, b.X[z], b.ldx, b.M, i0, j0, 0, b.K, true, smem);
-    // upper tile and its mirror, as gram16w_kernel's final store
-    const bool diag = ti == tj;
+    // upper tile and its mirror, as gram16w_kernel's final store (swap: the mirror only)
     const int dl = (wc * 128 + (lane & 31)) - (wr * 128 + 4 * (lane >> 5));
     const uint32_t lm = (uint32_t)(lane & 31) * (uint32_t)ldc + 4 * (lane >> 5);
 #pragma unroll
@@ -912,13 +918,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           const int rl = mt * 32 + 8 * g4;
           const f32x16& A = acc[mt][nt];
           const int dc = dl + nt * 32 - rl;
+          float* mp = C + (long)(jw + nt * 32) * ldc + iw + rl;
+          if (swap) {
+            *(float4*)(mp + lm) = make_float4(A[4 * g4], A[4 * g4 + 1], A[4 * g4 + 2], A[4 * g4 + 3]);
+            continue;
+          }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float* rp = C + (long)(iw + rl + u) * ldc + jw;
             if (!diag || dc >= u) rp[lo + nt * 32] = A[4 * g4 + u];
           }
           if (b.upper) continue;
-          float* mp = C + (long)(jw + nt * 32) * ldc + iw + rl;
           if (!diag || dc > 3) {
             *(float4*)(mp + lm) = make_float4(A[4 * g4], A[4 * g4 + 1], A[4 * g4 + 2], A[4 * g4 + 3]);
           } else {
@@ -935,7 +945,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // batch Grams G[z] = X[z]ᵀX[z] (STORE), X[z] N x m 16-bit (ld ldx), G packed (gstride floats apart,
 // ld m).  E_UNSUPPORTED unless m % 256 == 0 and the LDS-DMA staging conditions hold.  upper: only
 // the upper triangle is stored (a per-channel unit's Gram feeds nothing but S1 / d, which
-// s1_upper_ring_kernel forms from it): half the epilogue's stores, C5's Grams 55.4 -> 46.6 ms.
+// s1_upper_ring_kernel forms from it): half the epilogue's stores, C5's Grams 55.4 -> 46.6 ms;
+// off-diagonal tiles then computed transposed and stored by 16-byte mirror stores, -> ~43 ms.
 int pt2q_launch_gram16_batched(const void* const* X, int dtype, long N, int m, long ldx, float* G, long gstride,
                                int batch, hipStream_t st, bool upper) {
   if ((dtype != PT2Q_F16 && dtype != PT2Q_BF16) || batch <= 0 || m <= 0 || N < 0 || !G) return PT2Q_E_ARG;
