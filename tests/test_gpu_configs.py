@@ -323,12 +323,15 @@ def test_s1_from_upper_equals_full(pt2q, m, batch):
     assert bits_equal(host(got), host(want))
 
 
-@pytest.mark.parametrize("m,dt", [(5120, torch.bfloat16), (768, torch.float16)])
-def test_gram_batched_upper(pt2q, m, dt):
+@pytest.mark.parametrize("m,dt,N", [(5120, torch.bfloat16, 1024), (768, torch.float16, 1024),
+                                    (13824, torch.bfloat16, 1000), (1024, torch.float16, 328)])
+def test_gram_batched_upper(pt2q, m, dt, N):
     """pt2q_gram_batched_upper: the upper triangle (diagonal included) equals the full batched
-    Gram's bit for bit, the strictly lower part is left untouched."""
+    Gram's bit for bit, the strictly lower part is left untouched.  Off-diagonal tiles are formed
+    transposed there (gram16.hip), so this also pins G[j][i] == G[i][j]; N = 1000 / 328 end in a
+    ragged stage (N % 32 != 0), 328 rows are fewer than the chain's 2 x 5 ring stages."""
     eng = pt2q.engine
-    Xs = [pt2q.fill_synthetic((1024, m), 71 + z, std=1.0, outliers=True).to(dt) for z in range(3)]
+    Xs = [pt2q.fill_synthetic((N, m), 71 + z, std=1.0, outliers=True).to(dt) for z in range(3)]
     full = torch.empty((3, m, m), device=DEV)
     eng.gram_batched(Xs, full)
     up = torch.full((3, m, m), 7.0, device=DEV)
